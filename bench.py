@@ -1,0 +1,225 @@
+#!/usr/bin/env python
+"""Headline benchmark: RAG queries/sec + p50 end-to-end latency, bge-base + Llama-3-8B (BASELINE.json).
+
+One "step" = a batch of B user questions per GPU answered end to end through the engine's RAG path
+(``django_assistant_bot_amd.engine.rag.RAGPipeline``, the batched mirror of the reference's
+ContextService -> ChatCompletion chain):
+
+    bge-base query embedding (native encoder kernels)
+    -> exact top-250 question search over a 1M-row in-HBM index (fused MFMA score GEMM + radix top-k;
+       sharded across the ranks with all-gather merge when N > 1)
+    -> per-document aggregation (max_scores_n=5, top_n=5) -> FillInfo (<= 3 docs, 15 % of 8000)
+    -> FinalPrompt -> Llama-3-8B generation of a fixed number of tokens (ignore_eos) with the
+       reference's sampling (temperature 1, top_k 50, top_p 0.95), continuous batching + paged KV +
+       HIP-graph decode.
+
+Weights are random-init with the real architectures; corpus / questions are synthetic: each
+question has planted "paraphrase" rows near its embedding in 3-5 target documents so retrieval
+returns real documents and prompts have realistic length (~1k tokens).  Every rank uses TP=1
+(DP replicas; "scaling": weak -- per-GPU batch fixed).
+
+    python bench.py --gpus N --steps K --warmup W      (N > 1 under torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "RAG queries/sec + p50 end-to-end latency, bge-base + Llama-3-8B, 1/2/4/8 MI355X"
+BASELINE_QPS = None  # no published reference number; see benchmarks/reference_rerun.py
+
+_WORDS = ("account access admin answer api archive backup billing bot calendar campaign channel client cloud "
+          "config contact contract dashboard data deadline delivery deploy dialog document domain email error "
+          "export feature file filter form group guide invoice issue key language limit list login message "
+          "metric model module network notification order owner password payment plan policy price profile "
+          "project query queue quota refund region report request role schedule search server service session "
+          "setting storage subscription support task team template ticket token topic update upload user "
+          "version webhook wiki workflow").split()
+
+
+def synth_text(rng: np.random.Generator, n_words: int) -> str:
+    w = rng.choice(len(_WORDS), n_words)
+    out = []
+    for i, j in enumerate(w):
+        out.append(_WORDS[j])
+        if i % 13 == 12:
+            out[-1] += "."
+    return " ".join(out)
+
+
+class SyntheticDocuments(dict):
+    """Lazily materialised document store: doc id -> StoredDocument with ~200-300 words."""
+
+    def __init__(self, n_docs: int, seed: int):
+        super().__init__()
+        self.n_docs, self.seed = n_docs, seed
+
+    def __contains__(self, k):
+        return 0 <= int(k) < self.n_docs
+
+    def __getitem__(self, k):
+        from django_assistant_bot_amd.engine.rag import StoredDocument
+
+        k = int(k)
+        if not dict.__contains__(self, k):
+            rng = np.random.default_rng(self.seed * 7919 + k)
+            dict.__setitem__(self, k, StoredDocument(k, f"Document {k}", f"Wiki / Section {k // 100} / Document {k}",
+                                                     synth_text(rng, int(rng.integers(200, 300)))))
+        return dict.__getitem__(self, k)
+
+
+SYSTEM_TEXT = ("You are a helpful assistant of the company support team. Answer the user's questions about the "
+               "product, their account, billing and settings politely and precisely, in the user's language. "
+               "Use only the information provided to you, keep answers short and structured, and never invent "
+               "facts, prices, dates or links. If the question is unclear, ask the user to clarify it.")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64, help="questions per GPU per step")
+    ap.add_argument("--max-new-tokens", type=int, default=256)
+    ap.add_argument("--index-rows", type=int, default=1_000_000, help="question rows in the whole (sharded) index")
+    ap.add_argument("--rows-per-doc", type=int, default=10)
+    ap.add_argument("--embed-model", default="bge-base-en")
+    ap.add_argument("--llm-model", default="llama-3-8b")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--kv-gb", type=float, default=None)
+    ap.add_argument("--json-out", default=None)
+    args = ap.parse_args()
+
+    from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from django_assistant_bot_amd.engine.rag import RAGPipeline
+    from django_assistant_bot_amd.parallel import dist as pdist
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    info = pdist.init()
+    dev = info.device
+    W, R = info.world_size, info.rank
+    if W != args.gpus and R == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={W}", file=sys.stderr)
+    torch.manual_seed(args.seed + R)
+    B = args.batch
+    n_steps = args.warmup + args.steps
+
+    t_setup = time.perf_counter()
+    embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
+    llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * R, max_batch=B, max_model_len=4096,
+                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb,
+                    max_prefill_tokens=32768)
+    # ---- synthetic corpus: index rows (questions) grouped into documents
+    n_rows = args.index_rows
+    n_docs = max(1, n_rows // args.rows_per_doc)
+    docs = SyntheticDocuments(n_docs, args.seed)
+    index = ShardedIndex(embedder.dim, dev)
+    gen = torch.Generator(device=dev).manual_seed(args.seed * 31 + R)
+    chunk = 1 << 18
+    my_ids = np.arange(R, n_rows, W, dtype=np.int64)
+    for s in range(0, len(my_ids), chunk):
+        ids = my_ids[s:s + chunk]
+        v = torch.randn((len(ids), embedder.dim), device=dev, generator=gen)
+        index.add(ids, v, doc_ids=ids // args.rows_per_doc, groups=np.zeros(len(ids), dtype=np.int32))
+    # ---- questions of every rank / step (deterministic), embedded once to plant relevant rows
+    qrng = np.random.default_rng(args.seed + 12345)
+    all_q = [[[synth_text(qrng, int(qrng.integers(8, 16))) + "?" for _ in range(B)] for _ in range(n_steps)]
+             for _ in range(W)]
+    flat_q = [q for r in all_q for s in r for q in s]
+    q_emb = torch.nn.functional.normalize(embedder.embed(flat_q).float(), dim=-1)
+    prng = np.random.default_rng(args.seed + 999)
+    plant_ids, plant_vecs, plant_docs = [], [], []
+    for qi in range(len(flat_q)):
+        n_t = int(prng.integers(3, 6))
+        targets = prng.choice(n_docs, n_t, replace=False)
+        for rank_t, d in enumerate(targets):
+            rows = d * args.rows_per_doc + np.arange(min(args.rows_per_doc, 6))
+            rows = rows[rows < n_rows]
+            sigma = 0.02 + 0.004 * rank_t  # cos ~0.87..0.80: broad-search path, not the 0.05 shortcut
+            noise = torch.randn((len(rows), embedder.dim), device=dev, generator=torch.Generator(device=dev)
+                                .manual_seed(qi * 10 + rank_t)) * sigma
+            plant_ids.append(rows)
+            plant_vecs.append(q_emb[qi][None] + noise)
+            plant_docs.append(np.full(len(rows), d, dtype=np.int64))
+    index.add(np.concatenate(plant_ids), torch.cat(plant_vecs), doc_ids=np.concatenate(plant_docs),
+              groups=np.zeros(sum(len(x) for x in plant_ids), dtype=np.int32))
+    del q_emb
+    rag = RAGPipeline(embedder, index, llm, docs, system_text=SYSTEM_TEXT)
+    params = SamplingParams(max_new_tokens=args.max_new_tokens, ignore_eos=True, temperature=1.0, top_k=50,
+                            top_p=0.95)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    setup_s = time.perf_counter() - t_setup
+
+    latencies, prompt_lens, n_docs_used = [], [], []
+    for step in range(n_steps):
+        if step == args.warmup:
+            pdist.barrier(info)
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+        res = rag.answer(all_q[R][step], params, bot_group=0)
+        if step >= args.warmup:
+            latencies += [r.latency_s for r in res]
+            prompt_lens += [r.usage["prompt_tokens"] for r in res]
+            n_docs_used += [len(r.documents) for r in res]
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    pdist.barrier(info)
+    elapsed = pdist.max_over_ranks(time.perf_counter() - t0, dev)
+    p50 = float(np.median(latencies)) if latencies else float("nan")
+    p50 = pdist.max_over_ranks(p50, dev)
+    total_q = W * B * args.steps
+    qps = total_q / elapsed
+    out = {
+        "metric": METRIC,
+        "value": round(qps, 3),
+        "unit": "queries/s",
+        "n_gpus": W,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * elapsed / args.steps, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (round(qps / BASELINE_QPS, 3) if BASELINE_QPS else None),
+        "dtype": "bf16",
+        "data": "synthetic (random-init weights; synthetic corpus/questions)",
+        "p50_latency_ms": round(1000 * p50, 1),
+        "config": {
+            "model": f"{args.embed_model} + {args.llm_model}",
+            "global_batch": W * B,
+            "seq_len": int(np.mean(prompt_lens)) if prompt_lens else 0,
+            "max_new_tokens": args.max_new_tokens,
+            "parallelism": f"dp{W}",
+            "index_rows": n_rows,
+            "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
+            "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
+            "graphs": not args.no_graphs,
+            "setup_s": round(setup_s, 1),
+            "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
+        },
+    }
+    if R == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if args.json_out:
+            with open(args.json_out, "w") as f:
+                f.write(line + "\n")
+    pdist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+"""In-tree build of the native extension ``django_assistant_bot_amd/_native*.so``.
+
+Every ``csrc/kernels/*.hip`` file is compiled by ``hipcc --offload-arch=gfx950`` (CDNA4 only, no
+hipify, no CUDA path), the host runtime ``csrc/runtime/*.cpp`` and the pybind11 bindings are
+compiled by hipcc as host C++, and everything is linked into one shared object next to this file
+(so it travels with the repository snapshot to the GPU box).  Objects are rebuilt only when a
+source or header is newer than the object.
+
+    python -m django_assistant_bot_amd.build [--force] [-j N] [--debug]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+CSRC = PKG / "csrc"
+BUILD = PKG / "_build"
+ARCH = os.environ.get("DAB_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cand = Path(rocm) / "bin" / "hipcc"
+    return str(cand) if cand.exists() else "hipcc"
+
+
+def ext_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return PKG / f"_native{suffix}"
+
+
+def _headers() -> list[Path]:
+    return sorted(CSRC.rglob("*.h"))
+
+
+def _needs(obj: Path, src: Path, deps: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def _compile(cmd: list[str]) -> tuple[list[str], int, str]:
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    return cmd, p.returncode, p.stdout
+
+
+def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
+    import pybind11
+
+    BUILD.mkdir(exist_ok=True)
+    hipcc = _hipcc()
+    opt = ["-O0", "-g"] if debug else ["-O3"]
+    common = ["-std=c++17", "-fPIC", *opt, f"-I{CSRC}", "-Wno-unused-result", "-Wno-unused-command-line-argument"]
+    py_inc = [f"-I{sysconfig.get_paths()['include']}", f"-I{pybind11.get_include()}"]
+    deps = _headers()
+    jobs_list: list[tuple[list[str], Path]] = []
+    objs: list[Path] = []
+    for src in sorted((CSRC / "kernels").glob("*.hip")):
+        obj = BUILD / (src.stem + ".hip.o")
+        objs.append(obj)
+        if force or _needs(obj, src, deps):
+            jobs_list.append(([hipcc, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)], obj))
+    host_srcs = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
+    for src in host_srcs:
+        obj = BUILD / (src.stem + ".cpp.o")
+        objs.append(obj)
+        if force or _needs(obj, src, deps):
+            jobs_list.append(([hipcc, *common, *py_inc, "-fvisibility=hidden", "-c", str(src), "-o", str(obj)], obj))
+    out = ext_path()
+    n = jobs or min(16, os.cpu_count() or 4)
+    failed = []
+    with cf.ThreadPoolExecutor(max_workers=n) as ex:
+        for cmd, rc, log in ex.map(lambda j: _compile(j[0]), jobs_list):
+            if verbose or rc:
+                print(" ".join(cmd), file=sys.stderr)
+                print(log, file=sys.stderr)
+            if rc:
+                failed.append(cmd[-1])
+    if failed:
+        raise RuntimeError(f"native build failed for: {failed}")
+    if force or jobs_list or not out.exists():
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(out), "-lpthread"]
+        cmd, rc, log = _compile(link)
+        if rc:
+            print(" ".join(cmd), file=sys.stderr)
+            print(log, file=sys.stderr)
+            raise RuntimeError("native link failed")
+    return out
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--debug", action="store_true")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args()
+    print(build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+// pybind11 module `_native`: kernel launchers (raw device pointers + stream handles passed as
+// integers from the python ops layer, which owns shape/dtype validation) and the native host
+// runtime (tokenizer, paged-KV block manager, retrieval post-processing).
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "kernels/launchers.h"
+#include "runtime/kv_manager.h"
+#include "runtime/rag.h"
+#include "runtime/tokenizer.h"
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+#define VP(x) reinterpret_cast<void*>(x)
+#define CVP(x) reinterpret_cast<const void*>(x)
+#define ST(x) reinterpret_cast<hipStream_t>(x)
+
+static void check(int err, const char* name) {
+  if (err) throw std::runtime_error(std::string("dab kernel '") + name + "' failed: " + hipGetErrorString((hipError_t)err));
+}
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X (gfx950) kernels and native runtime of django_assistant_bot_amd";
+
+  // ---------------- kernels ----------------
+  m.def("rmsnorm", [](u out, u res_out, u x, u res_in, u w, int rows, int cols, float eps, u s) {
+    check(dab::rmsnorm(VP(out), VP(res_out), CVP(x), CVP(res_in), CVP(w), rows, cols, eps, ST(s)), "rmsnorm");
+  });
+  m.def("layernorm", [](u out, u x, u res_in, u gamma, u beta, int rows, int cols, float eps, u s) {
+    check(dab::layernorm(VP(out), CVP(x), CVP(res_in), CVP(gamma), CVP(beta), rows, cols, eps, ST(s)), "layernorm");
+  });
+  m.def("bert_embed", [](u out, u ids, u pos_ids, u type_ids, u word, u pos, u type, u gamma, u beta, int rows, int cols,
+                         float eps, u s) {
+    check(dab::bert_embed(VP(out), (const int*)ids, (const int*)pos_ids, (const int*)type_ids, CVP(word), CVP(pos),
+                          CVP(type), CVP(gamma), CVP(beta), rows, cols, eps, ST(s)),
+          "bert_embed");
+  });
+  m.def("embed_gather", [](u out, u ids, u table, int rows, int cols, u s) {
+    check(dab::embed_gather(VP(out), (const int*)ids, CVP(table), rows, cols, ST(s)), "embed_gather");
+  });
+  m.def("mean_pool", [](u out, u out_bf16, u hidden, u cu, int batch, int cols, int normalize, u s) {
+    check(dab::mean_pool((float*)out, VP(out_bf16), CVP(hidden), (const int*)cu, batch, cols, normalize, ST(s)),
+          "mean_pool");
+  });
+  m.def("gelu", [](u out, u x, u bias, size_t rows, int cols, u s) {
+    check(dab::gelu(VP(out), CVP(x), CVP(bias), rows, cols, ST(s)), "gelu");
+  });
+  m.def("silu_mul", [](u out, u x, size_t rows, int F, u s) {
+    check(dab::silu_mul(VP(out), CVP(x), rows, F, ST(s)), "silu_mul");
+  });
+  m.def("rope_kv_write", [](u qkv, int ld, u positions, u cos_sin, u q_out, u k_cache, u v_cache, u slots, int T,
+                            int Hq, int Hkv, int D, int block_size, u s) {
+    check(dab::rope_kv_write(CVP(qkv), ld, (const int*)positions, CVP(cos_sin), VP(q_out), VP(k_cache), VP(v_cache),
+                             (const int64_t*)slots, T, Hq, Hkv, D, block_size, ST(s)),
+          "rope_kv_write");
+  });
+  m.def("flash_attention",
+        [](u q, long qst, long qsh, u k, u v, long kvst, long kvsh, u kc, u vc, u bt, int max_blocks, int bs, u out,
+           long ost, long osh, u cu_q, u cu_k, u ctx_k, int batch, int max_sq, int Hq, int Hkv, int D, int causal,
+           int paged, float scale, u s) {
+          check(dab::flash_attention(CVP(q), qst, qsh, CVP(k), CVP(v), kvst, kvsh, CVP(kc), CVP(vc), (const int*)bt,
+                                     max_blocks, bs, VP(out), ost, osh, (const int*)cu_q, (const int*)cu_k,
+                                     (const int*)ctx_k, batch, max_sq, Hq, Hkv, D, causal, paged, scale, ST(s)),
+                "flash_attention");
+        });
+  m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
+                                     int batch, int Hq, int Hkv, int D, int part_size, int max_parts, float scale,
+                                     u s) {
+    check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
+                                      (float*)po, (float*)pm, (float*)pl, batch, Hq, Hkv, D, part_size, max_parts,
+                                      scale, ST(s)),
+          "paged_decode_attention");
+  });
+  m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
+                      int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s) {
+    check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
+                       (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s)),
+          "gemm_bt");
+  });
+  m.def("sample_tokens", [](u logits, int f32, long ld, int rows, int vocab, u temp, u top_k, u top_p,
+                            unsigned long long seed, u counters, u out_tokens, u out_logprobs, u s) {
+    check(dab::sample_tokens(CVP(logits), f32, ld, rows, vocab, (const float*)temp, (const int*)top_k,
+                             (const float*)top_p, seed, (int64_t*)counters, (int*)out_tokens, (float*)out_logprobs,
+                             ST(s)),
+          "sample_tokens");
+  });
+  m.def("topk_rows", [](u scores, long ld, int rows, int n, int k, u out_vals, u out_idx, long long base, u out_idx64,
+                        u s) {
+    check(dab::topk_rows((const float*)scores, ld, rows, n, k, (float*)out_vals, (int*)out_idx, base,
+                         (int64_t*)out_idx64, ST(s)),
+          "topk_rows");
+  });
+
+  // ---------------- tokenizer ----------------
+  py::class_<dab::TokenizerConfig>(m, "TokenizerConfig")
+      .def(py::init<>())
+      .def_readwrite("vocab_size", &dab::TokenizerConfig::vocab_size)
+      .def_readwrite("first_id", &dab::TokenizerConfig::first_id)
+      .def_readwrite("last_id", &dab::TokenizerConfig::last_id)
+      .def_readwrite("pad_id", &dab::TokenizerConfig::pad_id)
+      .def_readwrite("unk_id", &dab::TokenizerConfig::unk_id)
+      .def_readwrite("cls_id", &dab::TokenizerConfig::cls_id)
+      .def_readwrite("sep_id", &dab::TokenizerConfig::sep_id)
+      .def_readwrite("max_word_chars", &dab::TokenizerConfig::max_word_chars);
+  py::class_<dab::HashTokenizer>(m, "HashTokenizer")
+      .def(py::init<const dab::TokenizerConfig&>())
+      .def("encode", &dab::HashTokenizer::encode, py::arg("text"), py::arg("add_special") = true,
+           py::arg("max_len") = 0)
+      .def(
+          "encode_batch",
+          [](const dab::HashTokenizer& t, const std::vector<std::string>& texts, bool add_special, int max_len,
+             int threads) {
+            std::vector<int32_t> ids;
+            std::vector<int64_t> offs;
+            {
+              py::gil_scoped_release rel;
+              t.encode_batch(texts, add_special, max_len, threads, ids, offs);
+            }
+            py::array_t<int32_t> a(ids.size());
+            std::copy(ids.begin(), ids.end(), a.mutable_data());
+            py::array_t<int64_t> o(offs.size());
+            std::copy(offs.begin(), offs.end(), o.mutable_data());
+            return py::make_tuple(a, o);
+          },
+          py::arg("texts"), py::arg("add_special") = true, py::arg("max_len") = 0, py::arg("threads") = 8)
+      .def("decode", &dab::HashTokenizer::decode, py::arg("ids"), py::arg("skip_special") = true)
+      .def_static("count_words", &dab::HashTokenizer::count_words);
+
+  // ---------------- KV block manager ----------------
+  py::class_<dab::KVBlockManager>(m, "KVBlockManager")
+      .def(py::init<int, int, bool>(), py::arg("num_blocks"), py::arg("block_size"), py::arg("prefix_cache") = true)
+      .def("add_sequence", &dab::KVBlockManager::add_sequence)
+      .def("extend", &dab::KVBlockManager::extend)
+      .def("append_tokens", &dab::KVBlockManager::append_tokens)
+      .def("commit_prefix", &dab::KVBlockManager::commit_prefix)
+      .def("free_sequence", &dab::KVBlockManager::free_sequence)
+      .def("has", &dab::KVBlockManager::has)
+      .def("num_tokens", &dab::KVBlockManager::num_tokens)
+      .def("capacity_tokens", &dab::KVBlockManager::capacity_tokens)
+      .def("num_free_blocks", &dab::KVBlockManager::num_free_blocks)
+      .def("num_blocks", &dab::KVBlockManager::num_blocks)
+      .def("block_size", &dab::KVBlockManager::block_size)
+      .def("prefix_hits", &dab::KVBlockManager::prefix_hits)
+      .def("blocks", &dab::KVBlockManager::blocks)
+      .def("slot_mapping_into",
+           [](const dab::KVBlockManager& k, int64_t seq, int start, int n, u out) {
+             k.slot_mapping(seq, start, n, (int64_t*)out);
+           })
+      .def("block_table_into", [](const dab::KVBlockManager& k, const std::vector<int64_t>& seqs, int max_blocks,
+                                  u out) { k.block_table(seqs, max_blocks, (int32_t*)out); });
+
+  // ---------------- retrieval post-processing ----------------
+  m.def(
+      "aggregate_documents",
+      [](py::array_t<float, py::array::c_style | py::array::forcecast> dist,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_ids, int max_scores_n, int top_n) {
+        if (dist.size() != doc_ids.size()) throw std::invalid_argument("distances / doc_ids length mismatch");
+        auto r = dab::aggregate_documents(dist.data(), doc_ids.data(), (int)dist.size(), max_scores_n, top_n);
+        py::list out;
+        for (auto& d : r) out.append(py::make_tuple(d.doc_id, d.score));
+        return out;
+      },
+      py::arg("distances"), py::arg("doc_ids"), py::arg("max_scores_n"), py::arg("top_n"));
+  m.def(
+      "merge_topk",
+      [](py::array_t<float, py::array::c_style | py::array::forcecast> vals,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> ids, int k_out) {
+        if (vals.ndim() != 2 || ids.ndim() != 2 || vals.shape(0) != ids.shape(0) || vals.shape(1) != ids.shape(1))
+          throw std::invalid_argument("vals / ids must be [S, k] arrays of the same shape");
+        const int S = (int)vals.shape(0), k = (int)vals.shape(1);
+        py::array_t<float> ov(k_out);
+        py::array_t<int64_t> oi(k_out);
+        dab::merge_topk(vals.data(), ids.data(), S, k, k_out, ov.mutable_data(), oi.mutable_data());
+        return py::make_tuple(ov, oi);
+      },
+      py::arg("vals"), py::arg("ids"), py::arg("k_out"));
+}

@@ -1,0 +1,529 @@
+// Attention kernels on MFMA (v_mfma_f32_16x16x32_bf16) for gfx950.
+//
+//  flash_fwd   : variable-length, flash-style forward (online softmax) used for
+//                  - the BERT/bge encoder (bidirectional, K/V read from the packed QKV rows)   (N5)
+//                  - Llama prefill (causal, GQA, K/V read from the paged KV cache, so chunked
+//                    prefill and shared prefixes need no special path)                         (N10)
+//  paged_decode: single-token decode over the paged KV cache, split over key partitions
+//                (flash-decoding) + a small cross-partition reduce kernel                       (N9)
+//
+// Both compute S^T = K Q^T so that the MFMA C layout leaves the QUERY on the lane and the keys in
+// the registers; the probabilities P are then already the B operand of O^T = V^T P^T (no LDS round
+// trip for P), and V^T is fed from a row-major LDS V tile with ds_read_b64_tr_b16 (hardware
+// transpose).  K and V tiles are XOR-swizzled in LDS so that both the ds_read_b128 row reads of K
+// and the transposed reads of V are bank-conflict free (derivation in docs/kernels.md).
+//
+// Reference behaviour replaced: HF BertSelfAttention (ai/embedders/transformers.py:18-22) and the
+// HF Llama attention inside model.generate (ai/providers/transformers.py:57-66).
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+constexpr float kNegInf = -__builtin_huge_valf();
+
+// Byte offset of 16-byte chunk c of row r in a [rows][D] bf16 LDS tile.  The XOR keeps chunk
+// pairs (2j, 2j+1) together so that the 32-byte row pieces of a transposed read also spread.
+template <int D>
+__device__ __forceinline__ int swz(int r, int c) {
+  constexpr int RB = D * 2;
+  constexpr int CPR = D / 8;
+  constexpr int RPB = (256 / RB) > 0 ? (256 / RB) : 1;
+  return r * RB + 16 * (c ^ ((2 * (r / RPB)) & (CPR - 1)));
+}
+
+struct FlashParams {
+  const bf16* q;
+  long q_stride_tok, q_stride_head;
+  const bf16* k;
+  const bf16* v;
+  long kv_stride_tok, kv_stride_head;
+  const bf16* k_cache;
+  const bf16* v_cache;
+  const int* block_tables;
+  int max_blocks, block_size;
+  bf16* out;
+  long o_stride_tok, o_stride_head;
+  const int* cu_q;
+  const int* cu_k;
+  const int* ctx_k;
+  int Hq, Hkv;
+  float scale_log2;
+};
+
+// One workgroup = 64 queries (4 waves x 16) of one (sequence, head); 64-key tiles staged through
+// LDS with register prefetch of the next tile during compute (issue early / write late).
+template <int D, bool CAUSAL, bool PAGED>
+__global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
+  constexpr int KT = 64;
+  constexpr int NKK = D / 32;
+  constexpr int NTD = D / 16;
+  constexpr int CPR = D / 8;
+  constexpr int TILE_BYTES = KT * D * 2;
+  constexpr int CH = KT * CPR / 256;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+  char* ks = smem;
+  char* vs = smem + TILE_BYTES;
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int q_start = p.cu_q[b];
+  const int seqlen_q = p.cu_q[b + 1] - q_start;
+  const int q0 = blockIdx.x * 64;
+  if (q0 >= seqlen_q) return;
+  int kv_len, k_start = 0;
+  if (PAGED) {
+    kv_len = p.ctx_k[b];
+  } else {
+    k_start = p.cu_k[b];
+    kv_len = p.cu_k[b + 1] - k_start;
+  }
+  const int hk = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int my_q = q0 + w * 16 + li;
+  const bool q_valid = my_q < seqlen_q;
+  const int q_pos = kv_len - seqlen_q + my_q;
+
+  bf16x8 qf[NKK];
+  {
+    const bf16* qrow = p.q + (size_t)(q_start + (q_valid ? my_q : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[kk] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
+    }
+  }
+
+  int n_keys = kv_len;
+  if (CAUSAL) {
+    const int last_q = min(q0 + 63, seqlen_q - 1);
+    n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
+  }
+  const int n_tiles = div_up(n_keys, KT);
+
+  u32x4 kreg[CH], vreg[CH];
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * 256;
+      const int row = idx / CPR, ch = idx % CPR;
+      const int key = kt * KT + row;
+      u32x4 z = {0u, 0u, 0u, 0u};
+      kreg[c] = z;
+      vreg[c] = z;
+      if (key < kv_len) {
+        size_t off;
+        if (PAGED) {
+          const int blk = p.block_tables[(size_t)b * p.max_blocks + key / p.block_size];
+          off = (((size_t)blk * p.Hkv + hk) * p.block_size + (key % p.block_size)) * D;
+          kreg[c] = *reinterpret_cast<const u32x4*>(p.k_cache + off + ch * 8);
+          vreg[c] = *reinterpret_cast<const u32x4*>(p.v_cache + off + ch * 8);
+        } else {
+          off = (size_t)(k_start + key) * p.kv_stride_tok + (size_t)hk * p.kv_stride_head;
+          kreg[c] = *reinterpret_cast<const u32x4*>(p.k + off + ch * 8);
+          vreg[c] = *reinterpret_cast<const u32x4*>(p.v + off + ch * 8);
+        }
+      }
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * 256;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
+      *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
+    }
+  };
+
+  f32x4 o[NTD];
+#pragma unroll
+  for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+
+  if (n_tiles > 0) {
+    load_tile(0);
+    store_tile();
+  }
+  for (int kt = 0; kt < n_tiles; ++kt) {
+    __syncthreads();
+    if (kt + 1 < n_tiles) load_tile(kt + 1);
+    f32x4 s[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
+        s[m] = mfma16(a, qf[kk], s[m]);
+      }
+    }
+    float mx = kNegInf;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * KT + 16 * m + 4 * g + r;
+        float v = s[m][r] * p.scale_log2;
+        if (key >= kv_len || (CAUSAL && key > q_pos)) v = kNegInf;
+        s[m][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(s[m][r] - m_new);
+        s[m][r] = e;
+        ls += e;
+      }
+    }
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) o[t] *= alpha;
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[2 * ss][j]);
+        pb[j + 4] = (short)f2bf(s[2 * ss + 1][j]);
+      }
+      const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int t = 0; t < NTD; ++t) {
+        const int ch = 2 * t + (pp >> 1);
+        const int boff = 8 * (pp & 1);
+        const bf16x4 lo = ds_read_tr16(vs + swz<D>(32 * ss + 4 * g + qq, ch) + boff);
+        const bf16x4 hi = ds_read_tr16(vs + swz<D>(32 * ss + 16 + 4 * g + qq, ch) + boff);
+        const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[t] = mfma16(a, pb, o[t]);
+      }
+    }
+    __syncthreads();
+    if (kt + 1 < n_tiles) store_tile();
+  }
+
+  float l_tot = l_run;
+  l_tot += __shfl_xor(l_tot, 16, 64);
+  l_tot += __shfl_xor(l_tot, 32, 64);
+  if (!q_valid) return;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16* orow = p.out + (size_t)(q_start + my_q) * p.o_stride_tok + (size_t)h * p.o_stride_head;
+#pragma unroll
+  for (int t = 0; t < NTD; ++t) {
+    u32x2 v;
+    v[0] = pack2bf(o[t][0] * inv, o[t][1] * inv);
+    v[1] = pack2bf(o[t][2] * inv, o[t][3] * inv);
+    *reinterpret_cast<u32x2*>(orow + 16 * t + 4 * g) = v;
+  }
+}
+
+// -----------------------------------------------------------------------------------------------
+// Paged decode.  grid = (max_parts, Hkv, B); one workgroup reduces keys [part*part_size, +part_size)
+// of one (sequence, kv head) for all G = Hq/Hkv query heads of the GQA group (the MFMA N dimension,
+// padded to 16).  Each wave streams 32-key sub-tiles through a private LDS slot (no block barriers in
+// the loop), with the next sub-tile's global loads in flight during compute.
+
+struct DecodeParams {
+  const bf16* q;
+  const bf16* k_cache;
+  const bf16* v_cache;
+  const int* block_tables;
+  int max_blocks, block_size;
+  const int* ctx_lens;
+  bf16* out;
+  float* part_o;
+  float* part_m;
+  float* part_l;
+  int Hq, Hkv, part_size, max_parts;
+  float scale_log2;
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p) {
+  constexpr int KT = 32;
+  constexpr int NKK = D / 32;
+  constexpr int NTD = D / 16;
+  constexpr int CPR = D / 8;
+  constexpr int SUB_BYTES = KT * D * 2;
+  constexpr int CH = KT * CPR / 64;  // 16-B chunks per lane per sub-tile (K and V each)
+  constexpr int RED_BYTES = 4 * 16 * D * 4 + 2 * 4 * 16 * 4;
+  constexpr int STAGE_BYTES = 4 * 2 * SUB_BYTES;
+  __shared__ __attribute__((aligned(16))) char smem[STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES];
+
+  const int part = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
+  const int ctx = p.ctx_lens[b];
+  const int k_begin = part * p.part_size;
+  if (k_begin >= ctx) return;
+  const int k_end = min(ctx, k_begin + p.part_size);
+  const int G = p.Hq / p.Hkv;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  char* ks = smem + w * 2 * SUB_BYTES;
+  char* vs = ks + SUB_BYTES;
+
+  bf16x8 qf[NKK];
+  {
+    const bool qv = li < G;
+    const bf16* qrow = p.q + ((size_t)b * p.Hq + hk * G + (qv ? li : 0)) * D;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[kk] = qv ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
+    }
+  }
+
+  u32x4 kreg[CH], vreg[CH];
+  auto load_sub = [&](int k0) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = lane + c * 64;
+      const int row = idx / CPR, ch = idx % CPR;
+      const int key = k0 + row;
+      u32x4 z = {0u, 0u, 0u, 0u};
+      kreg[c] = z;
+      vreg[c] = z;
+      if (key < k_end) {
+        const int blk = p.block_tables[(size_t)b * p.max_blocks + key / p.block_size];
+        const size_t off = (((size_t)blk * p.Hkv + hk) * p.block_size + (key % p.block_size)) * D + ch * 8;
+        kreg[c] = *reinterpret_cast<const u32x4*>(p.k_cache + off);
+        vreg[c] = *reinterpret_cast<const u32x4*>(p.v_cache + off);
+      }
+    }
+  };
+
+  f32x4 o[NTD];
+#pragma unroll
+  for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+
+  int k0 = k_begin + w * KT;
+  if (k0 < k_end) load_sub(k0);
+  for (; k0 < k_end; k0 += 4 * KT) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = lane + c * 64;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
+      *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
+    }
+    if (k0 + 4 * KT < k_end) load_sub(k0 + 4 * KT);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    f32x4 s[2];
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
+        s[m] = mfma16(a, qf[kk], s[m]);
+      }
+    }
+    float mx = kNegInf;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * m + 4 * g + r;
+        float v = s[m][r] * p.scale_log2;
+        if (key >= k_end) v = kNegInf;
+        s[m][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = exp2f(s[m][r] - m_new);
+        s[m][r] = e;
+        ls += e;
+      }
+    }
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+    bf16x8 pb;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pb[j] = (short)f2bf(s[0][j]);
+      pb[j + 4] = (short)f2bf(s[1][j]);
+    }
+    const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+      o[t] *= alpha;
+      const int ch = 2 * t + (pp >> 1);
+      const int boff = 8 * (pp & 1);
+      const bf16x4 lo = ds_read_tr16(vs + swz<D>(4 * g + qq, ch) + boff);
+      const bf16x4 hi = ds_read_tr16(vs + swz<D>(16 + 4 * g + qq, ch) + boff);
+      const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      o[t] = mfma16(a, pb, o[t]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // combine the 4 waves of the workgroup through LDS
+  l_run += __shfl_xor(l_run, 16, 64);
+  l_run += __shfl_xor(l_run, 32, 64);
+  __syncthreads();
+  float* ored = reinterpret_cast<float*>(smem);        // [4][16][D]
+  float* mred = ored + 4 * 16 * D;                      // [4][16]
+  float* lred = mred + 4 * 16;                          // [4][16]
+#pragma unroll
+  for (int t = 0; t < NTD; ++t) *reinterpret_cast<f32x4*>(ored + (w * 16 + li) * D + 16 * t + 4 * g) = o[t];
+  if (g == 0) {
+    mred[w * 16 + li] = m_run;
+    lred[w * 16 + li] = l_run;
+  }
+  __syncthreads();
+  const bool direct = p.max_parts == 1;
+  for (int e = tid; e < G * D; e += 256) {
+    const int qh = e / D, d = e % D;
+    float M = -1e30f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, mred[ww * 16 + qh]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = exp2f(mred[ww * 16 + qh] - M);
+      L += f * lred[ww * 16 + qh];
+      O += f * ored[(ww * 16 + qh) * D + d];
+    }
+    const size_t hq = (size_t)b * p.Hq + hk * G + qh;
+    if (direct) {
+      p.out[hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+    } else {
+      const size_t pi = hq * p.max_parts + part;
+      p.part_o[pi * D + d] = O;
+      if (d == 0) {
+        p.part_m[pi] = M;
+        p.part_l[pi] = L;
+      }
+    }
+  }
+}
+
+// out[b, hq, :] = sum_p exp2(m_p - M) o_p / sum_p exp2(m_p - M) l_p over the partitions that hold keys.
+template <int D>
+__global__ __launch_bounds__(D) void decode_reduce_kernel(DecodeParams p) {
+  const int hq = blockIdx.x, b = blockIdx.y;
+  const int ctx = p.ctx_lens[b];
+  const int np = min(p.max_parts, div_up(ctx, p.part_size));
+  const size_t base = ((size_t)b * p.Hq + hq) * p.max_parts;
+  float M = -1e30f;
+  for (int i = 0; i < np; ++i) M = fmaxf(M, p.part_m[base + i]);
+  float L = 0.f, O = 0.f;
+  const int d = threadIdx.x;
+  for (int i = 0; i < np; ++i) {
+    const float f = exp2f(p.part_m[base + i] - M);
+    L += f * p.part_l[base + i];
+    O += f * p.part_o[(base + i) * D + d];
+  }
+  p.out[((size_t)b * p.Hq + hq) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+}
+
+// -----------------------------------------------------------------------------------------------
+
+int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const void* k, const void* v,
+                    long kv_stride_tok, long kv_stride_head, const void* k_cache, const void* v_cache,
+                    const int* block_tables, int max_blocks, int block_size, void* out, long o_stride_tok,
+                    long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
+                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s) {
+  if (batch <= 0 || max_seqlen_q <= 0) return 0;
+  if (Hq % Hkv) return hipErrorInvalidValue;
+  FlashParams prm;
+  prm.q = (const bf16*)q;
+  prm.q_stride_tok = q_stride_tok;
+  prm.q_stride_head = q_stride_head;
+  prm.k = (const bf16*)k;
+  prm.v = (const bf16*)v;
+  prm.kv_stride_tok = kv_stride_tok;
+  prm.kv_stride_head = kv_stride_head;
+  prm.k_cache = (const bf16*)k_cache;
+  prm.v_cache = (const bf16*)v_cache;
+  prm.block_tables = block_tables;
+  prm.max_blocks = max_blocks;
+  prm.block_size = block_size;
+  prm.out = (bf16*)out;
+  prm.o_stride_tok = o_stride_tok;
+  prm.o_stride_head = o_stride_head;
+  prm.cu_q = cu_q;
+  prm.cu_k = cu_k;
+  prm.ctx_k = ctx_k;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid((max_seqlen_q + 63) / 64, Hq, batch);
+#define DAB_FLASH(DD, C, P) hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P>), grid, dim3(256), 0, s, prm)
+#define DAB_FLASH_D(DD)                    \
+  if (paged) {                             \
+    if (causal) DAB_FLASH(DD, true, true); \
+    else DAB_FLASH(DD, false, true);       \
+  } else {                                 \
+    if (causal) DAB_FLASH(DD, true, false); \
+    else DAB_FLASH(DD, false, false);      \
+  }
+  if (D == 128) {
+    DAB_FLASH_D(128)
+  } else if (D == 64) {
+    DAB_FLASH_D(64)
+  } else if (D == 32) {
+    DAB_FLASH_D(32)
+  } else {
+    return hipErrorInvalidValue;
+  }
+#undef DAB_FLASH_D
+#undef DAB_FLASH
+  return hipGetLastError();
+}
+
+int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                           int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
+                           float* part_m, float* part_l, int batch, int Hq, int Hkv, int D, int part_size,
+                           int max_parts, float scale, hipStream_t s) {
+  if (batch <= 0) return 0;
+  if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1) return hipErrorInvalidValue;
+  DecodeParams prm;
+  prm.q = (const bf16*)q;
+  prm.k_cache = (const bf16*)k_cache;
+  prm.v_cache = (const bf16*)v_cache;
+  prm.block_tables = block_tables;
+  prm.max_blocks = max_blocks;
+  prm.block_size = block_size;
+  prm.ctx_lens = ctx_lens;
+  prm.out = (bf16*)out;
+  prm.part_o = part_o;
+  prm.part_m = part_m;
+  prm.part_l = part_l;
+  prm.Hq = Hq;
+  prm.Hkv = Hkv;
+  prm.part_size = part_size;
+  prm.max_parts = max_parts;
+  prm.scale_log2 = scale * 1.4426950408889634f;
+  dim3 grid(max_parts, Hkv, batch);
+  if (D == 128) {
+    hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(256), 0, s, prm);
+    if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, batch), dim3(128), 0, s, prm);
+  } else if (D == 64) {
+    hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(256), 0, s, prm);
+    if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, batch), dim3(64), 0, s, prm);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dab

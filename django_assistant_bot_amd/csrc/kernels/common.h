@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernel library.
+//
+// Conventions used by every kernel in this directory:
+//   * activations / weights are bf16 stored as raw uint16 bits, accumulation is fp32;
+//   * a wavefront is 64 lanes (never 32) and blocks are multiples of 64 threads;
+//   * global loads/stores of bf16 are vectorised to 16 B per lane (8 x bf16);
+//   * MFMA tiles use v_mfma_f32_16x16x32_bf16 whose lane maps are
+//       A: lane l holds A[row l&15][k 8(l>>4)+j], j=0..7
+//       B: lane l holds B[k 8(l>>4)+j][col l&15]
+//       C: lane l holds C[row 4(l>>4)+r][col l&15], r=0..3
+//     (cdna_hip_programming.md section 3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dab {
+
+typedef uint16_t bf16;
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef short bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+// Round-to-nearest-even through the compiler's native conversion (v_cvt_pk_bf16_f32 on gfx950),
+// which keeps NaN a NaN (MI355X_MICROARCH.md, correctness boundaries).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+__device__ __forceinline__ void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(v[i] << 16);
+    f[2 * i + 1] = __uint_as_float(v[i] & 0xffff0000u);
+  }
+}
+
+__device__ __forceinline__ u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = pack2bf(f[2 * i], f[2 * i + 1]);
+  return v;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64 floats.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  __syncthreads();
+  return t;
+}
+
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+// ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q, columns 4p..4p+3
+// of a 4x16 bf16 block; lane i receives column i of the 4 rows (row q in element q).
+__device__ __forceinline__ bf16x4 ds_read_tr16(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(lds_ptr));
+}
+
+__device__ __forceinline__ int div_up(int a, int b) { return (a + b - 1) / b; }
+
+// Orderable unsigned key of a float: larger float -> larger key (used by radix selects).
+__device__ __forceinline__ uint32_t float_key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key_float(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+}  // namespace dab
+
+#define DAB_CHECK_LAUNCH() (hipGetLastError())

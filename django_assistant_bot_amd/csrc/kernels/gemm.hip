@@ -1,0 +1,224 @@
+// bf16 MFMA GEMM  C[M,N] = A[M,K] . B[N,K]^T  with fused epilogues, for gfx950.
+//
+// Used for (a) the encoder projections with their bias / GELU / residual epilogues fused (BERT/bge),
+// (b) the Llama MLP gate|up projection with SwiGLU fused into the epilogue, and (c) the in-HBM
+// cosine index scan (queries x index rows -> fp32 scores with the row-validity / per-query group /
+// allow-bitmask filter applied in the epilogue), which replaces pgvector's CosineDistance ORDER BY
+// (reference rag/services/search_service.py:185-196, storage/models.py:32-58).
+//
+// Structure ("2-phase" of cdna_hip_programming.md section 5.5 T3/T4 minimum form):
+//   * 128x128 block tile, BK = 64, 256 threads = 2x2 waves, 64x64 per wave = 4x4 MFMA 16x16x32 tiles;
+//   * A/B tiles staged global->LDS with global_load_lds_dwordx4 (no VGPR round trip), double-buffered,
+//     next K tile issued before the current tile's MFMAs, one barrier per K step;
+//   * 128-B LDS rows XOR-swizzled on the SOURCE address (LDS-DMA writes lane-linear), the same
+//     involution applied on the ds_read_b128 side -> conflict-free fragment reads;
+//   * operands swapped in the MFMA (B rows feed the A slot) so each lane ends with 4 consecutive
+//     output columns of one row -> 8-B / 16-B epilogue stores;
+//   * bijective XCD-aware block remap (T1) so neighbouring tiles share an XCD's L2.
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+enum EpiMode { EPI_NONE = 0, EPI_GELU = 1, EPI_SWIGLU = 2, EPI_SCORES = 3 };
+
+struct GemmParams {
+  const bf16* A;
+  const bf16* B;
+  void* C;
+  const bf16* bias;
+  const bf16* residual;
+  const int* row_group;   // scores: [N] group id of each index row (<0 = deleted)
+  const int* q_group;     // scores: [M] group each query may see (<0 = any)
+  const uint32_t* allow;  // scores: [M, ceil(N/32)] allow bitmask (optional)
+  int M, N, K;
+  long lda, ldb, ldc, ldr;
+  int allow_words;
+  int out_f32;
+};
+
+__device__ __forceinline__ int gsw(int r) { return 2 * ((r >> 1) & 3); }
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
+  constexpr int BM = 128, BN = 128, BK = 64;
+  constexpr int TILE = BM * BK * 2;  // bytes per operand tile
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][A|B]
+
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  // bijective XCD remap: blocks b and b+8 share an XCD; give each XCD a contiguous id range
+  const int bid = blockIdx.x;
+  const int xcd = bid % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int swz_id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tm = swz_id % tiles_m, tn = swz_id / tiles_m;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int wm = w >> 1, wn = w & 1;
+
+  // staging: wave w, instruction c writes LDS bytes [(c*4+w)*1024, +1024) of a tile = rows 8(c*4+w)..+7
+  auto stage = [&](int buf, int k0) {
+    char* As = smem + buf * 2 * TILE;
+    char* Bs = As + TILE;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int e = (c * 4 + w) * 64 + lane;
+      const int r = e >> 3, pos = e & 7;
+      const int src_chunk = pos ^ gsw(r);
+      const int ra = min(m0 + r, p.M - 1);
+      const int rb = min(n0 + r, p.N - 1);
+      const bf16* ga = p.A + (size_t)ra * p.lda + k0 + src_chunk * 8;
+      const bf16* gb = p.B + (size_t)rb * p.ldb + k0 + src_chunk * 8;
+      __builtin_amdgcn_global_load_lds((const void*)ga, (__attribute__((address_space(3))) void*)(As + (c * 4 + w) * 1024),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)gb, (__attribute__((address_space(3))) void*)(Bs + (c * 4 + w) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.K / BK;
+  stage(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+    const char* As = smem + (kt & 1) * 2 * TILE;
+    const char* Bs = As + TILE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ra = wm * 64 + 16 * i + li;
+        af[i] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + 16 * ((4 * ks + g) ^ gsw(ra)));
+        const int rb = wn * 64 + 16 * i + li;
+        bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + 16 * ((4 * ks + g) ^ gsw(rb)));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni)
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = mfma16(bfr[ni], af[mi], acc[ni][mi]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // epilogue: acc[ni][mi][r] = C[m = m0 + wm*64 + 16 mi + li][n = n0 + wn*64 + 16 ni + 4 g + r]
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int m = m0 + wm * 64 + 16 * mi + li;
+    if (m >= p.M) continue;
+    if (EPI == EPI_SWIGLU) {
+      // weight rows interleaved in 16-row groups [gate 16 | up 16]: ni even = gate, ni odd = up
+#pragma unroll
+      for (int pi = 0; pi < 2; ++pi) {
+        const int ng = n0 + wn * 64 + 32 * pi + 4 * g;  // gate column in the interleaved space
+        if (ng >= p.N) continue;
+        const int oc = (n0 + wn * 64) / 2 + 16 * pi + 4 * g;
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float gt = acc[2 * pi][mi][r], up = acc[2 * pi + 1][mi][r];
+          if (p.bias) {
+            gt += bf2f(p.bias[ng + r]);
+            up += bf2f(p.bias[ng + 16 + r]);
+          }
+          o[r] = gt / (1.f + __expf(-gt)) * up;
+        }
+        u32x2 v;
+        v[0] = pack2bf(o[0], o[1]);
+        v[1] = pack2bf(o[2], o[3]);
+        *reinterpret_cast<u32x2*>((bf16*)p.C + (size_t)m * p.ldc + oc) = v;
+      }
+      continue;
+    }
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int n = n0 + wn * 64 + 16 * ni + 4 * g;
+      if (n >= p.N) continue;  // N % 4 == 0 is required by the launcher
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = acc[ni][mi][r];
+      if (EPI == EPI_SCORES) {
+        const int qg = p.q_group ? p.q_group[m] : -1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          bool ok = true;
+          if (p.row_group) {
+            const int rg = p.row_group[n + r];
+            ok = rg >= 0 && (qg < 0 || rg == qg);
+          }
+          if (p.allow) ok = ok && ((p.allow[(size_t)m * p.allow_words + ((n + r) >> 5)] >> ((n + r) & 31)) & 1u);
+          if (!ok) o[r] = -__builtin_huge_valf();
+        }
+      } else {
+        if (p.bias) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += bf2f(p.bias[n + r]);
+        }
+        if (EPI == EPI_GELU) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = 0.5f * o[r] * (1.f + erff(o[r] * 0.70710678118654752f));
+        }
+        if (p.residual) {
+          const bf16* rr = p.residual + (size_t)m * p.ldr + n;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += bf2f(rr[r]);
+        }
+      }
+      if (p.out_f32) {
+        *reinterpret_cast<f32x4*>((float*)p.C + (size_t)m * p.ldc + n) = f32x4{o[0], o[1], o[2], o[3]};
+      } else {
+        u32x2 v;
+        v[0] = pack2bf(o[0], o[1]);
+        v[1] = pack2bf(o[2], o[3]);
+        *reinterpret_cast<u32x2*>((bf16*)p.C + (size_t)m * p.ldc + n) = v;
+      }
+    }
+  }
+}
+
+int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
+            long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
+            const uint32_t* allow, int allow_words, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 64 || N % 4 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
+  if (epilogue == EPI_SWIGLU && (N % 32 || out_f32)) return hipErrorInvalidValue;
+  GemmParams p;
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.C = C;
+  p.bias = (const bf16*)bias;
+  p.residual = (const bf16*)residual;
+  p.row_group = row_group;
+  p.q_group = q_group;
+  p.allow = allow;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.ldr = ldr;
+  p.allow_words = allow_words;
+  p.out_f32 = out_f32;
+  const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
+  switch (epilogue) {
+    case EPI_NONE: hipLaunchKernelGGL(gemm_bt_kernel<EPI_NONE>, dim3(nwg), dim3(256), 0, s, p); break;
+    case EPI_GELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU>, dim3(nwg), dim3(256), 0, s, p); break;
+    case EPI_SWIGLU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_SWIGLU>, dim3(nwg), dim3(256), 0, s, p); break;
+    case EPI_SCORES: hipLaunchKernelGGL(gemm_bt_kernel<EPI_SCORES>, dim3(nwg), dim3(256), 0, s, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dab

@@ -1,0 +1,53 @@
+// Host-side launchers of the gfx950 kernel library.  Every launcher validates the shape
+// constraints its kernel relies on, enqueues on the given stream (graph-capture safe: no
+// allocation, no synchronisation) and returns a hipError_t value (0 = success).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace dab {
+
+inline int div_up_host(int a, int b) { return (a + b - 1) / b; }
+
+// norm.hip
+int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const void* w, int rows, int cols, float eps,
+            hipStream_t s);
+int layernorm(void* out, const void* x, const void* res_in, const void* gamma, const void* beta, int rows, int cols,
+              float eps, hipStream_t s);
+int bert_embed(void* out, const int* ids, const int* pos_ids, const int* type_ids, const void* word, const void* pos,
+               const void* type, const void* gamma, const void* beta, int rows, int cols, float eps, hipStream_t s);
+int embed_gather(void* out, const int* ids, const void* table, int rows, int cols, hipStream_t s);
+int mean_pool(float* out, void* out_bf16, const void* hidden, const int* cu_seqlens, int batch, int cols,
+              int normalize, hipStream_t s);
+
+// elementwise.hip
+int gelu(void* out, const void* x, const void* bias, size_t rows, int cols, hipStream_t s);
+int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s);
+int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos_sin, void* q_out, void* k_cache,
+                  void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s);
+
+// attention.hip
+int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const void* k, const void* v,
+                    long kv_stride_tok, long kv_stride_head, const void* k_cache, const void* v_cache,
+                    const int* block_tables, int max_blocks, int block_size, void* out, long o_stride_tok,
+                    long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
+                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s);
+int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
+                           int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
+                           float* part_m, float* part_l, int batch, int Hq, int Hkv, int D, int part_size,
+                           int max_parts, float scale, hipStream_t s);
+
+// gemm.hip
+int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
+            long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
+            const uint32_t* allow, int allow_words, hipStream_t s);
+
+// select.hip
+int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
+                  const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
+                  float* out_logprobs, hipStream_t s);
+int topk_rows(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx, int64_t index_base,
+              int64_t* out_idx64, hipStream_t s);
+
+}  // namespace dab

@@ -1,0 +1,307 @@
+// Row-wise normalisation, embedding and pooling kernels (memory-bound; 16-B vectorised rows).
+//
+// Replaces the implicit HF ops of the reference encoder / generator:
+//   * Llama RMSNorm with the residual add fused in           (N7)
+//   * BERT post-LN: residual add + LayerNorm fused          (N3)
+//   * BERT embedding gather + sum + LayerNorm fused          (N2)
+//   * masked mean-pool (+ optional L2 normalise)             (N6; reference embedders/transformers.py:25)
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+// One block per row; each thread owns VPT 8-element vectors kept in registers between the
+// reduction and the scaling pass, so the row is read from HBM exactly once.
+template <int NT, int VPT>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, bf16* __restrict__ res_out,
+                                                     const bf16* __restrict__ x, const bf16* __restrict__ res_in,
+                                                     const bf16* __restrict__ w, int cols, float eps) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  const int nvec = cols >> 3;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + row * cols);
+  const u32x4* rr = reinterpret_cast<const u32x4*>(res_in + row * cols);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      unpack8(xr[i], v[k]);
+      if (res_in) {
+        float r[8];
+        unpack8(rr[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + r[j]));  // residual kept in bf16 like HF
+        reinterpret_cast<u32x4*>(res_out + row * cols)[i] = pack8(v[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
+    }
+  }
+  const float tot = block_sum<NT>(ss, red);
+  const float inv = rsqrtf(tot / (float)cols + eps);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  u32x4* orow = reinterpret_cast<u32x4*>(out + row * cols);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      float g[8], o[8];
+      unpack8(wr[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * inv * g[j];
+      orow[i] = pack8(o);
+    }
+  }
+}
+
+// out = LayerNorm(x + res) * gamma + beta   (BERT post-LN; two-pass mean/var in registers)
+template <int NT, int VPT>
+__global__ __launch_bounds__(NT) void layernorm_kernel(bf16* __restrict__ out, const bf16* __restrict__ x,
+                                                       const bf16* __restrict__ res_in, const bf16* __restrict__ gamma,
+                                                       const bf16* __restrict__ beta, int cols, float eps) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  const int nvec = cols >> 3;
+  const u32x4* xr = reinterpret_cast<const u32x4*>(x + row * cols);
+  const u32x4* rr = reinterpret_cast<const u32x4*>(res_in + row * cols);
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      unpack8(xr[i], v[k]);
+      if (res_in) {
+        float r[8];
+        unpack8(rr[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[k][j];
+    }
+  }
+  const float mean = block_sum<NT>(s, red) / (float)cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[k][j] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum<NT>(sq, red) / (float)cols + eps);
+  const u32x4* gr = reinterpret_cast<const u32x4*>(gamma);
+  const u32x4* br = reinterpret_cast<const u32x4*>(beta);
+  u32x4* orow = reinterpret_cast<u32x4*>(out + row * cols);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      float g[8], b[8], o[8];
+      unpack8(gr[i], g);
+      unpack8(br[i], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * inv * g[j] + b[j];
+      orow[i] = pack8(o);
+    }
+  }
+}
+
+// BERT embeddings: LN(word[id] + pos[pos_id] + type[type_id]) fused; type ids default to 0.
+template <int NT, int VPT>
+__global__ __launch_bounds__(NT) void bert_embed_kernel(bf16* __restrict__ out, const int* __restrict__ ids,
+                                                        const int* __restrict__ pos_ids, const int* __restrict__ type_ids,
+                                                        const bf16* __restrict__ word, const bf16* __restrict__ pos,
+                                                        const bf16* __restrict__ type, const bf16* __restrict__ gamma,
+                                                        const bf16* __restrict__ beta, int cols, float eps) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  const int nvec = cols >> 3;
+  const size_t id = (size_t)ids[row];
+  const size_t pid = (size_t)pos_ids[row];
+  const size_t tid = type_ids ? (size_t)type_ids[row] : 0;
+  const u32x4* wr = reinterpret_cast<const u32x4*>(word + id * cols);
+  const u32x4* pr = reinterpret_cast<const u32x4*>(pos + pid * cols);
+  const u32x4* tr = reinterpret_cast<const u32x4*>(type + tid * cols);
+  float v[VPT][8];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      float a[8], b[8];
+      unpack8(wr[i], v[k]);
+      unpack8(pr[i], a);
+      unpack8(tr[i], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[k][j] += a[j] + b[j];
+        s += v[k][j];
+      }
+    }
+  }
+  const float mean = block_sum<NT>(s, red) / (float)cols;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[k][j] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float inv = rsqrtf(block_sum<NT>(sq, red) / (float)cols + eps);
+  const u32x4* gr = reinterpret_cast<const u32x4*>(gamma);
+  const u32x4* br = reinterpret_cast<const u32x4*>(beta);
+  u32x4* orow = reinterpret_cast<u32x4*>(out + row * cols);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      float g[8], b[8], o[8];
+      unpack8(gr[i], g);
+      unpack8(br[i], b);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * inv * g[j] + b[j];
+      orow[i] = pack8(o);
+    }
+  }
+}
+
+// Row gather (token embedding lookup for the decoder).
+__global__ __launch_bounds__(256) void embed_gather_kernel(bf16* __restrict__ out, const int* __restrict__ ids,
+                                                           const bf16* __restrict__ table, int cols) {
+  const size_t row = blockIdx.y;
+  const int nvec = cols >> 3;
+  const u32x4* src = reinterpret_cast<const u32x4*>(table + (size_t)ids[row] * cols);
+  u32x4* dst = reinterpret_cast<u32x4*>(out + row * cols);
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < nvec; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+// Mean over the tokens of each packed sequence [cu[b], cu[b+1]) (all tokens incl. [CLS]/[SEP], as the
+// reference does), optional L2 normalisation; fp32 output [B, cols] and optional bf16 copy.
+__global__ __launch_bounds__(256) void mean_pool_kernel(float* __restrict__ out, bf16* __restrict__ out_bf16,
+                                                        const bf16* __restrict__ hidden, const int* __restrict__ cu,
+                                                        int cols, int normalize) {
+  __shared__ float red[4];
+  const int b = blockIdx.x;
+  const int start = cu[b], end = cu[b + 1];
+  const int nvec = cols >> 3;
+  const float inv_n = end > start ? 1.f / (float)(end - start) : 0.f;
+  float acc[2][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + k * 256;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[k][j] = 0.f;
+    if (i < nvec) {
+      for (int t = start; t < end; ++t) {
+        float v[8];
+        unpack8(reinterpret_cast<const u32x4*>(hidden + (size_t)t * cols)[i], v);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[k][j] += v[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        acc[k][j] *= inv_n;
+        ss += acc[k][j] * acc[k][j];
+      }
+    }
+  }
+  float scale = 1.f;
+  if (normalize) {
+    const float tot = block_sum<256>(ss, red);
+    scale = tot > 0.f ? rsqrtf(tot) : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int i = threadIdx.x + k * 256;
+    if (i < nvec) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        o[j] = acc[k][j] * scale;
+        out[(size_t)b * cols + i * 8 + j] = o[j];
+      }
+      if (out_bf16) reinterpret_cast<u32x4*>(out_bf16 + (size_t)b * cols)[i] = pack8(o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// launchers
+
+#define DAB_ROW_DISPATCH(KERNEL, ROWS, COLS, STREAM, ...)                                        \
+  do {                                                                                          \
+    const int nvec_ = (COLS) / 8;                                                               \
+    if (nvec_ <= 64)                                                                            \
+      hipLaunchKernelGGL((KERNEL<64, 1>), dim3(ROWS), dim3(64), 0, STREAM, __VA_ARGS__);        \
+    else if (nvec_ <= 128)                                                                      \
+      hipLaunchKernelGGL((KERNEL<128, 1>), dim3(ROWS), dim3(128), 0, STREAM, __VA_ARGS__);      \
+    else if (nvec_ <= 256)                                                                      \
+      hipLaunchKernelGGL((KERNEL<256, 1>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);      \
+    else if (nvec_ <= 512)                                                                      \
+      hipLaunchKernelGGL((KERNEL<256, 2>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);      \
+    else if (nvec_ <= 1024)                                                                     \
+      hipLaunchKernelGGL((KERNEL<256, 4>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);      \
+    else                                                                                        \
+      hipLaunchKernelGGL((KERNEL<256, 8>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);      \
+  } while (0)
+
+int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const void* w, int rows, int cols, float eps,
+            hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8 || cols > 16384) return hipErrorInvalidValue;
+  DAB_ROW_DISPATCH(rmsnorm_kernel, rows, cols, s, (bf16*)out, (bf16*)res_out, (const bf16*)x, (const bf16*)res_in,
+                   (const bf16*)w, cols, eps);
+  return hipGetLastError();
+}
+
+int layernorm(void* out, const void* x, const void* res_in, const void* gamma, const void* beta, int rows, int cols,
+              float eps, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8 || cols > 16384) return hipErrorInvalidValue;
+  DAB_ROW_DISPATCH(layernorm_kernel, rows, cols, s, (bf16*)out, (const bf16*)x, (const bf16*)res_in,
+                   (const bf16*)gamma, (const bf16*)beta, cols, eps);
+  return hipGetLastError();
+}
+
+int bert_embed(void* out, const int* ids, const int* pos_ids, const int* type_ids, const void* word, const void* pos,
+               const void* type, const void* gamma, const void* beta, int rows, int cols, float eps, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8 || cols > 16384) return hipErrorInvalidValue;
+  DAB_ROW_DISPATCH(bert_embed_kernel, rows, cols, s, (bf16*)out, ids, pos_ids, type_ids, (const bf16*)word,
+                   (const bf16*)pos, (const bf16*)type, (const bf16*)gamma, (const bf16*)beta, cols, eps);
+  return hipGetLastError();
+}
+
+int embed_gather(void* out, const int* ids, const void* table, int rows, int cols, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8) return hipErrorInvalidValue;
+  const int nvec = cols / 8;
+  dim3 grid(div_up_host(nvec, 256), rows);
+  hipLaunchKernelGGL(embed_gather_kernel, grid, dim3(256), 0, s, (bf16*)out, ids, (const bf16*)table, cols);
+  return hipGetLastError();
+}
+
+int mean_pool(float* out, void* out_bf16, const void* hidden, const int* cu_seqlens, int batch, int cols,
+              int normalize, hipStream_t s) {
+  if (batch <= 0) return 0;
+  if (cols % 8 || cols > 4096) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mean_pool_kernel, dim3(batch), dim3(256), 0, s, out, (bf16*)out_bf16, (const bf16*)hidden,
+                     cu_seqlens, cols, normalize);
+  return hipGetLastError();
+}
+
+}  // namespace dab

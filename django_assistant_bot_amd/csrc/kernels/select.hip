@@ -1,0 +1,268 @@
+// Per-row selection kernels (one 1024-thread workgroup per row):
+//   sample_tokens : HF-parity sampling  temperature -> top-k -> top-p -> multinomial  (N12;
+//                   reference ai/providers/transformers.py:57-66 do_sample=True, top_k=50, top_p=0.95),
+//                   greedy when temperature <= 0.  Counter-based RNG: graph replays draw fresh numbers.
+//   topk_rows     : exact top-k (k <= 1024) of fp32 score rows, sorted descending, for the in-HBM
+//                   cosine index (N13/N14; replaces pgvector ORDER BY distance LIMIT n).
+//
+// Both use an MSB-first 4 x 8-bit radix select of the k-th largest orderable key.  Histogram
+// increments are wave-aggregated (one LDS atomic per distinct bin per wave) because score /
+// logit keys cluster in a handful of top-byte bins and plain per-lane LDS atomics would serialise.
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+constexpr int SEL_NT = 1024;
+constexpr int SEL_MAXK = 1024;
+
+struct SelShared {
+  uint32_t hist[256];
+  uint32_t bcast[4];
+  uint32_t cnt_gt, cnt_eq;
+  uint32_t cand_key[SEL_MAXK];
+  int cand_idx[SEL_MAXK];
+};
+
+// Appends `pred` lanes with one atomic per wave; returns this lane's slot (or -1).
+__device__ __forceinline__ int wave_append(uint32_t* counter, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (!m) return -1;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const unsigned long long below = lane ? (m & ((1ull << lane) - 1ull)) : 0ull;
+  return pred ? (int)(base + __popcll(below)) : -1;
+}
+
+template <class KeyAt>
+__device__ uint32_t radix_kth(KeyAt key_at, int n, int k, SelShared& sh, uint32_t& ties_needed) {
+  uint32_t prefix = 0, pmask = 0, kk = (uint32_t)k;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += SEL_NT) sh.hist[i] = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += SEL_NT) {
+      const int i = i0 + tid;
+      int bin = -1;
+      if (i < n) {
+        const uint32_t key = key_at(i);
+        if ((key & pmask) == prefix) bin = (int)((key >> shift) & 255u);
+      }
+      unsigned long long active = __ballot(bin >= 0);
+      while (active) {
+        const int leader = __ffsll((long long)active) - 1;
+        const int lb = __shfl(bin, leader, 64);
+        const unsigned long long eq = __ballot(bin == lb);
+        if (lane == leader) atomicAdd(&sh.hist[lb], (uint32_t)__popcll(eq));
+        active &= ~eq;
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      uint32_t c[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        c[j] = sh.hist[255 - 4 * tid - j];
+        sum += c[j];
+      }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += t;
+      }
+      const uint32_t excl = incl - sum;
+      if (excl < kk && kk <= incl) {
+        uint32_t acc = excl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (acc + c[j] >= kk) {
+            sh.bcast[0] = 255u - 4u * tid - j;
+            sh.bcast[1] = kk - acc;
+            break;
+          }
+          acc += c[j];
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t digit = sh.bcast[0];
+    kk = sh.bcast[1];
+    prefix |= digit << shift;
+    pmask |= 255u << shift;
+    __syncthreads();
+  }
+  ties_needed = kk;
+  return prefix;
+}
+
+// Gathers the k largest keys (ties at the k-th key taken in arbitrary order) into sh.cand_*[0..k)
+// and sorts them descending by key (ascending index among equal keys).
+template <class KeyAt>
+__device__ void select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
+  const int tid = threadIdx.x;
+  uint32_t ties;
+  const uint32_t kth = radix_kth(key_at, n, k, sh, ties);
+  if (tid == 0) {
+    sh.cnt_gt = 0;
+    sh.cnt_eq = 0;
+  }
+  __syncthreads();
+  const uint32_t n_gt = (uint32_t)k - ties;
+  for (int i0 = 0; i0 < n; i0 += SEL_NT) {
+    const int i = i0 + tid;
+    uint32_t key = 0;
+    if (i < n) key = key_at(i);
+    const int pg = wave_append(&sh.cnt_gt, i < n && key > kth);
+    if (pg >= 0) {
+      sh.cand_key[pg] = key;
+      sh.cand_idx[pg] = i;
+    }
+    const int pe = wave_append(&sh.cnt_eq, i < n && key == kth);
+    if (pe >= 0 && (uint32_t)pe < ties) {
+      sh.cand_key[n_gt + pe] = key;
+      sh.cand_idx[n_gt + pe] = i;
+    }
+  }
+  __syncthreads();
+  int P = 1;
+  while (P < k) P <<= 1;
+  for (int i = k + tid; i < P; i += SEL_NT) {
+    sh.cand_key[i] = 0u;
+    sh.cand_idx[i] = 0x7fffffff;
+  }
+  __syncthreads();
+  // bitonic sort, descending key, ascending index
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < P; t += SEL_NT) {
+        const int u = t ^ stride;
+        if (u > t) {
+          const bool desc = (t & size) == 0;
+          const uint32_t ka = sh.cand_key[t], kb = sh.cand_key[u];
+          const int ia = sh.cand_idx[t], ib = sh.cand_idx[u];
+          const bool a_first = ka > kb || (ka == kb && ia < ib);
+          if (a_first != desc) {
+            sh.cand_key[t] = kb;
+            sh.cand_key[u] = ka;
+            sh.cand_idx[t] = ib;
+            sh.cand_idx[u] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(SEL_NT) void sample_kernel(const void* __restrict__ logits, int logits_f32, long ld,
+                                                        int vocab, const float* __restrict__ temperature,
+                                                        const int* __restrict__ top_k,
+                                                        const float* __restrict__ top_p, unsigned long long seed,
+                                                        int64_t* __restrict__ counters, int* __restrict__ out_tokens,
+                                                        float* __restrict__ out_logprobs) {
+  __shared__ SelShared sh;
+  __shared__ float probs[SEL_MAXK];
+  const int row = blockIdx.x;
+  const float T = temperature ? temperature[row] : 1.f;
+  int k = (T <= 0.f) ? 1 : (top_k && top_k[row] > 0 ? top_k[row] : SEL_MAXK);
+  if (k > SEL_MAXK) k = SEL_MAXK;
+  if (k > vocab) k = vocab;
+  const float P = top_p ? top_p[row] : 1.f;
+  const bool f32 = logits_f32 != 0;
+  const float* lf = reinterpret_cast<const float*>(logits) + (size_t)row * ld;
+  const bf16* lb = reinterpret_cast<const bf16*>(logits) + (size_t)row * ld;
+  auto key_at = [&](int i) -> uint32_t { return float_key(f32 ? lf[i] : bf2f(lb[i])); };
+  select_topk(key_at, vocab, k, sh);
+  if (threadIdx.x != 0) return;
+  if (T <= 0.f) {
+    out_tokens[row] = sh.cand_idx[0];
+    if (out_logprobs) out_logprobs[row] = 0.f;
+    return;
+  }
+  // softmax over the top-k set (HF: top-k sets the rest to -inf before top-p's softmax)
+  const float x0 = key_float(sh.cand_key[0]) / T;
+  float total = 0.f;
+  for (int i = 0; i < k; ++i) {
+    const float e = __expf(key_float(sh.cand_key[i]) / T - x0);
+    probs[i] = e;
+    total += e;
+  }
+  // HF TopPLogitsWarper: ascending cumsum, drop tokens with cumsum <= 1 - top_p, keep >= 1.
+  int keep = k;
+  if (P < 1.f) {
+    const float thr = (1.f - P) * total;
+    float cum = 0.f;
+    keep = k;
+    for (int i = k - 1; i >= 1; --i) {  // ascending order = reverse of the sorted list
+      cum += probs[i];
+      if (cum <= thr) keep = i;
+      else break;
+    }
+  }
+  float kept = 0.f;
+  for (int i = 0; i < keep; ++i) kept += probs[i];
+  const long long c = counters ? counters[row] : 0;
+  if (counters) counters[row] = c + 1;
+  const unsigned long long r =
+      splitmix64(seed ^ splitmix64((unsigned long long)c * 0x9E3779B97F4A7C15ull + (unsigned long long)row));
+  const float u = (float)(r >> 40) * (1.f / 16777216.f);
+  const float target = u * kept;
+  float acc = 0.f;
+  int pick = keep - 1;
+  for (int i = 0; i < keep; ++i) {
+    acc += probs[i];
+    if (acc > target) {
+      pick = i;
+      break;
+    }
+  }
+  out_tokens[row] = sh.cand_idx[pick];
+  if (out_logprobs) out_logprobs[row] = __logf(probs[pick] / kept);
+}
+
+__global__ __launch_bounds__(SEL_NT) void topk_rows_kernel(const float* __restrict__ scores, long ld, int n, int k,
+                                                           float* __restrict__ out_vals, int* __restrict__ out_idx,
+                                                           int64_t index_base, int64_t* __restrict__ out_idx64) {
+  __shared__ SelShared sh;
+  const int row = blockIdx.x;
+  const float* s = scores + (size_t)row * ld;
+  auto key_at = [&](int i) -> uint32_t { return float_key(s[i]); };
+  select_topk(key_at, n, k, sh);
+  for (int i = threadIdx.x; i < k; i += SEL_NT) {
+    out_vals[(size_t)row * k + i] = key_float(sh.cand_key[i]);
+    if (out_idx) out_idx[(size_t)row * k + i] = sh.cand_idx[i];
+    if (out_idx64) out_idx64[(size_t)row * k + i] = index_base + sh.cand_idx[i];
+  }
+}
+
+int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
+                  const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
+                  float* out_logprobs, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (vocab <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(rows), dim3(SEL_NT), 0, s, logits, logits_f32, ld, vocab, temperature, top_k,
+                     top_p, seed, counters, out_tokens, out_logprobs);
+  return hipGetLastError();
+}
+
+int topk_rows(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx, int64_t index_base,
+              int64_t* out_idx64, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (k < 1 || k > SEL_MAXK || k > n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(topk_rows_kernel, dim3(rows), dim3(SEL_NT), 0, s, scores, ld, n, k, out_vals, out_idx, index_base,
+                     out_idx64);
+  return hipGetLastError();
+}
+
+}  // namespace dab

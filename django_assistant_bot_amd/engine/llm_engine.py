@@ -1,0 +1,467 @@
+"""Continuous-batching generation engine for the Llama decoder (paged KV cache, HIP graphs).
+
+Reference behaviour replaced: ``TransformersProvider.get_response`` (ai/providers/transformers.py:35-94)
+runs ``model.generate`` once per HTTP request (batch 1, fp16, top_k=50 / top_p=0.95 sampling, no
+request batching across callers).  Here every concurrent request shares one batch:
+
+  * admission / prefill: prompts are admitted while KV blocks last (native ``KVBlockManager``, with
+    content-hashed prefix reuse), prompt tokens are packed into chunks of ``max_prefill_tokens``
+    (long prompts are split across steps), the last prompt position is sampled;
+  * decode: all running sequences advance one token per step; the step (forward + LM head + the
+    sampling kernel) is replayed from a HIP graph captured per batch-size bucket, so the ~400 kernel
+    launches of a decode step cost one graph launch;
+  * preemption: if the pool runs dry while decoding, the youngest sequence is freed and re-queued
+    (recompute), so admission can be optimistic.
+
+Sampling parity with HF: temperature -> top-k -> top-p -> multinomial (``sample_tokens`` kernel);
+``max_new_tokens`` bounds the completion (the reference's ``max_length`` counted the prompt too,
+SURVEY.md 7.5; pass ``max_length`` for that behaviour).
+"""
+from __future__ import annotations
+
+import itertools
+import math
+import time
+from collections import deque
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models import AttnMeta, KVCache, LlamaModel, decoder_config, random_decoder_weights
+from ..models.configs import DecoderConfig
+from ..ops._lib import native
+from .tokenizer import Tokenizer
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 1024
+    temperature: float = 1.0
+    top_k: int = 50
+    top_p: float = 0.95
+    ignore_eos: bool = False
+    max_length: int | None = None  # HF-style cap on prompt + completion
+    seed: int | None = None
+    stop_token_ids: tuple = ()
+    do_sample: bool = True
+
+
+@dataclass
+class GenerationOutput:
+    request_id: int
+    prompt_ids: list
+    token_ids: list
+    text: str
+    finish_reason: str
+    usage: dict
+    timings: dict
+
+
+@dataclass
+class _Req:
+    rid: int
+    prompt: list
+    params: SamplingParams
+    arrival: float
+    out: list = field(default_factory=list)
+    computed: int = 0  # prompt tokens whose KV is in the cache
+    admitted: bool = False
+    first_token_t: float = 0.0
+    finish_t: float = 0.0
+    finish_reason: str = ""
+    rng_base: int = 0
+    prefill_s: float = 0.0
+    preempted: int = 0
+
+    @property
+    def seq(self):
+        return self.rid
+
+    def full_prompt(self):
+        return self.prompt + self.out if self.preempted else self.prompt
+
+
+def _bucket_sizes(max_batch):
+    b = [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512]
+    return [x for x in b if x < max_batch] + [max_batch]
+
+
+class LLMEngine:
+    def __init__(self, model: str | DecoderConfig = "llama-3-8b", device=None, weights: dict | None = None,
+                 checkpoint: str | None = None, seed: int = 0, max_batch: int = 256, block_size: int = 64,
+                 max_model_len: int | None = None, kv_cache_gb: float | None = None, num_blocks: int | None = None,
+                 max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
+                 tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = False,
+                 part_size: int = 512, kv_memory_fraction: float = 0.85):
+        self.cfg = decoder_config(model) if isinstance(model, str) else model
+        cfg = self.cfg
+        self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.is_gpu = self.device.type == "cuda"
+        self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank
+        if weights is None:
+            if checkpoint:
+                from ..models import load_decoder_checkpoint
+
+                weights = load_decoder_checkpoint(checkpoint, cfg, tp_rank=tp_rank, tp_size=tp_size,
+                                                  interleave_mlp=interleaved_mlp)
+            else:
+                weights = random_decoder_weights(cfg, self.device, seed=seed, tp_rank=tp_rank, tp_size=tp_size,
+                                                 interleave_mlp=interleaved_mlp)
+        self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
+                                interleaved_mlp=interleaved_mlp)
+        del weights
+        self.tokenizer = Tokenizer.for_decoder(cfg, checkpoint)
+        self.max_batch = max_batch
+        self.block_size = block_size
+        self.max_model_len = min(max_model_len or cfg.max_position, cfg.max_position)
+        self.max_blocks_per_seq = math.ceil(self.max_model_len / block_size)
+        self.max_prefill_tokens = max_prefill_tokens
+        self.part_size = part_size
+        hkv = cfg.kv_heads // tp_size
+        per_block = KVCache.bytes_per_block(cfg.layers, hkv, block_size, cfg.head_dim)
+        if num_blocks is None:
+            if kv_cache_gb:
+                num_blocks = int(kv_cache_gb * (1 << 30) // per_block)
+            elif self.is_gpu:
+                free, _ = torch.cuda.mem_get_info(self.device)
+                num_blocks = int(free * kv_memory_fraction // per_block)
+            else:
+                num_blocks = 4 * self.max_blocks_per_seq
+            num_blocks = max(2, min(num_blocks, max_batch * self.max_blocks_per_seq + 8))
+        self.kv = KVCache(cfg.layers, num_blocks, hkv, block_size, cfg.head_dim, self.device)
+        self.blocks = native().KVBlockManager(num_blocks, block_size, prefix_cache)
+        self.seed = seed
+        self.waiting: deque[_Req] = deque()
+        self.prefilling: list[_Req] = []
+        self.running: list[_Req] = []
+        self.finished: dict[int, _Req] = {}
+        self._ids = itertools.count()
+        self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "decode_steps": 0, "prefill_steps": 0,
+                      "preemptions": 0, "graph_replays": 0}
+        # decode static buffers (graph inputs / outputs)
+        self.use_graphs = use_graphs and self.is_gpu
+        dev = self.device
+        mb = max_batch
+        self._d_ids = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self._d_pos = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self._d_slots = torch.full((mb,), -1, dtype=torch.int64, device=dev)
+        self._d_ctx = torch.ones(mb, dtype=torch.int32, device=dev)
+        self._d_bt = torch.zeros((mb, self.max_blocks_per_seq), dtype=torch.int32, device=dev)
+        self._d_temp = torch.ones(mb, dtype=torch.float32, device=dev)
+        self._d_topk = torch.full((mb,), 50, dtype=torch.int32, device=dev)
+        self._d_topp = torch.ones(mb, dtype=torch.float32, device=dev)
+        self._d_cnt = torch.zeros(mb, dtype=torch.int64, device=dev)
+        self._d_tokens = torch.zeros(mb, dtype=torch.int32, device=dev)
+        pin = self.is_gpu
+        mk = lambda *a, **k: torch.zeros(*a, **k, pin_memory=pin)  # noqa: E731
+        self._h_ids = mk(mb, dtype=torch.int32)
+        self._h_pos = mk(mb, dtype=torch.int32)
+        self._h_slots = mk(mb, dtype=torch.int64)
+        self._h_ctx = mk(mb, dtype=torch.int32)
+        self._h_bt = mk((mb, self.max_blocks_per_seq), dtype=torch.int32)
+        self._h_temp = mk(mb, dtype=torch.float32)
+        self._h_topk = mk(mb, dtype=torch.int32)
+        self._h_topp = mk(mb, dtype=torch.float32)
+        self._h_cnt = mk(mb, dtype=torch.int64)
+        self._h_tokens = mk(mb, dtype=torch.int32)
+        max_parts = math.ceil(self.max_model_len / part_size)
+        self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
+            else None
+        self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._buckets = _bucket_sizes(max_batch)
+        self._graph_pool = None
+
+    # ------------------------------------------------------------------ public API
+    def add_request(self, prompt_ids: list, params: SamplingParams | None = None, request_id: int | None = None) -> int:
+        params = params or SamplingParams()
+        rid = next(self._ids) if request_id is None else request_id
+        prompt = [int(t) for t in prompt_ids]
+        if not prompt:
+            prompt = [self.cfg.bos_id]
+        if len(prompt) >= self.max_model_len:
+            prompt = prompt[-(self.max_model_len - 1):]
+        seed = params.seed if params.seed is not None else self.seed
+        r = _Req(rid, prompt, params, time.perf_counter(), rng_base=((seed * 1000003 + rid) & 0xFFFFFFFF) << 20)
+        self.waiting.append(r)
+        return rid
+
+    def has_unfinished(self) -> bool:
+        return bool(self.waiting or self.prefilling or self.running)
+
+    def generate(self, prompts: list, params: SamplingParams | list | None = None) -> list[GenerationOutput]:
+        """Batch generate: token-id lists or strings -> outputs in input order."""
+        plist = params if isinstance(params, list) else [params or SamplingParams()] * len(prompts)
+        rids = []
+        for p, sp in zip(prompts, plist):
+            ids = self.tokenizer.encode(p) if isinstance(p, str) else p
+            rids.append(self.add_request(ids, sp))
+        while self.has_unfinished():
+            self.step()
+        return [self.pop_output(r) for r in rids]
+
+    def pop_output(self, rid: int) -> GenerationOutput:
+        r = self.finished.pop(rid)
+        n_out = len(r.out)
+        return GenerationOutput(
+            request_id=rid, prompt_ids=r.prompt, token_ids=list(r.out),
+            text=self.tokenizer.decode(r.out), finish_reason=r.finish_reason,
+            usage={"prompt_tokens": len(r.prompt), "completion_tokens": n_out, "total_tokens": len(r.prompt) + n_out},
+            timings={"queue_s": max(0.0, r.first_token_t - r.arrival - r.prefill_s),
+                     "ttft_s": r.first_token_t - r.arrival, "total_s": r.finish_t - r.arrival,
+                     "decode_s": r.finish_t - r.first_token_t, "prefill_s": r.prefill_s},
+        )
+
+    def step(self) -> list[int]:
+        """One scheduler iteration (a prefill chunk batch, else a decode step). Returns finished ids."""
+        done_before = set(self.finished)
+        chunks = self._schedule_prefill()
+        if chunks:
+            self._run_prefill(chunks)
+        elif self.running:
+            self._run_decode()
+        return [k for k in self.finished if k not in done_before]
+
+    # ------------------------------------------------------------------ scheduling
+    def _schedule_prefill(self):
+        budget = self.max_prefill_tokens
+        chunks = []
+        for r in self.prefilling:
+            if budget <= 0:
+                break
+            total = len(r.full_prompt())
+            n = min(total - r.computed, budget)
+            if n > 0:
+                chunks.append((r, r.computed, n))
+                budget -= n
+        while self.waiting and budget > 0 and len(self.running) + len(self.prefilling) < self.max_batch:
+            r = self.waiting[0]
+            toks = r.full_prompt()
+            cached = self.blocks.add_sequence(r.seq, toks, 1)
+            if cached < 0:
+                if not self.running and not self.prefilling:
+                    raise RuntimeError("KV cache too small for a single request")
+                break
+            self.waiting.popleft()
+            r.admitted = True
+            r.computed = cached
+            self.prefilling.append(r)
+            n = min(len(toks) - cached, budget)
+            chunks.append((r, cached, n))
+            budget -= n
+        return chunks
+
+    def _build_block_tables(self, seqs, out_host):
+        self.blocks.block_table_into(seqs, self.max_blocks_per_seq, out_host.data_ptr())
+
+    def _run_prefill(self, chunks):
+        t0 = time.perf_counter()
+        dev = self.device
+        B = len(chunks)
+        T = sum(n for _, _, n in chunks)
+        ids = np.empty(T, dtype=np.int32)
+        pos = np.empty(T, dtype=np.int32)
+        slots = torch.empty(T, dtype=torch.int64)
+        cu = np.zeros(B + 1, dtype=np.int32)
+        ctx = np.empty(B, dtype=np.int32)
+        o = 0
+        for i, (r, s, n) in enumerate(chunks):
+            toks = r.full_prompt()
+            ids[o:o + n] = toks[s:s + n]
+            pos[o:o + n] = np.arange(s, s + n, dtype=np.int32)
+            self.blocks.slot_mapping_into(r.seq, s, n, slots.data_ptr() + 8 * o)
+            o += n
+            cu[i + 1] = o
+            ctx[i] = s + n
+        bt = torch.zeros((B, self.max_blocks_per_seq), dtype=torch.int32)
+        self._build_block_tables([r.seq for r, _, _ in chunks], bt)
+        to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
+        meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
+                        cu_q=to(cu), max_q=max(n for _, _, n in chunks))
+        hidden = self.model.forward(to(ids), meta, self.kv)
+        last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
+        self.stats["prefill_tokens"] += T
+        self.stats["prefill_steps"] += 1
+        if last_rows:
+            sel = torch.as_tensor([int(cu[i + 1]) - 1 for i in last_rows], dtype=torch.long).to(dev)
+            logits = self.model.logits(hidden.index_select(0, sel))
+            reqs = [chunks[i][0] for i in last_rows]
+            toks = self._sample(logits, reqs)
+        for r, s, n in chunks:
+            r.computed = s + n
+        now = time.perf_counter()
+        for r, s, n in chunks:
+            r.prefill_s += now - t0
+        if last_rows:
+            for r, t in zip(reqs, toks):
+                self.blocks.commit_prefix(r.seq, len(r.full_prompt()))
+                self.prefilling.remove(r)
+                r.first_token_t = r.first_token_t or now
+                r.preempted = 0
+                self.running.append(r)
+                self._accept_token(r, int(t), now)
+
+    def _sample(self, logits, reqs):
+        n = len(reqs)
+        temps = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in reqs], dtype=torch.float32)
+        topk = torch.tensor([r.params.top_k for r in reqs], dtype=torch.int32)
+        topp = torch.tensor([r.params.top_p for r in reqs], dtype=torch.float32)
+        cnt = torch.tensor([r.rng_base + len(r.out) for r in reqs], dtype=torch.int64)
+        if self.is_gpu:
+            d = self.device
+            toks = ops.sample_tokens(logits, temps.to(d), topk.to(d), topp.to(d), self.seed, cnt.to(d))
+            toks = self._tp_sync_tokens(toks)
+            return toks.cpu().tolist()
+        g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
+        return ops.sample_tokens(logits, temps, topk, topp, self.seed, cnt, generator=g).tolist()
+
+    def _tp_sync_tokens(self, toks):
+        if self.tp_size > 1:
+            import torch.distributed as dist
+
+            src = dist.get_global_rank(self.tp_group, 0) if self.tp_group is not None else 0
+            dist.broadcast(toks, src=src, group=self.tp_group)
+        return toks
+
+    def _accept_token(self, r: _Req, tok: int, now: float):
+        r.out.append(tok)
+        p = r.params
+        reason = ""
+        if not p.ignore_eos and (tok in self.cfg.eos_ids or tok in p.stop_token_ids):
+            reason = "stop"
+        elif len(r.out) >= p.max_new_tokens:
+            reason = "length"
+        elif p.max_length is not None and len(r.prompt) + len(r.out) >= p.max_length:
+            reason = "length"
+        elif len(r.prompt) + len(r.out) >= self.max_model_len:
+            reason = "length"
+        if reason:
+            r.finish_reason = reason
+            r.finish_t = now
+            self.running.remove(r)
+            self.blocks.free_sequence(r.seq)
+            self.finished[r.rid] = r
+
+    def _preempt_one(self, protect: _Req) -> bool:
+        for victim in reversed(self.running):
+            if victim is protect:
+                continue
+            self.running.remove(victim)
+            self.blocks.free_sequence(victim.seq)
+            victim.preempted = 1
+            victim.computed = 0
+            self.waiting.appendleft(victim)
+            self.stats["preemptions"] += 1
+            return True
+        return False
+
+    # ------------------------------------------------------------------ decode
+    def _run_decode(self):
+        # reserve one slot per running sequence, preempting the youngest when the pool is dry
+        batch = []
+        for r in list(self.running):
+            if r not in self.running:
+                continue
+            while not self.blocks.extend(r.seq, 1):
+                if not self._preempt_one(protect=r):
+                    raise RuntimeError("KV cache exhausted")
+            batch.append(r)
+        batch = [r for r in batch if r in self.running]
+        B = len(batch)
+        if B == 0:
+            return
+        for i, r in enumerate(batch):
+            last = r.out[-1]
+            self.blocks.append_tokens(r.seq, [last])
+            p = self.blocks.num_tokens(r.seq) - 1
+            self._h_ids[i] = last
+            self._h_pos[i] = p
+            self.blocks.slot_mapping_into(r.seq, p, 1, self._h_slots.data_ptr() + 8 * i)
+            self._h_ctx[i] = p + 1
+            self._h_temp[i] = r.params.temperature if r.params.do_sample else 0.0
+            self._h_topk[i] = r.params.top_k
+            self._h_topp[i] = r.params.top_p
+            self._h_cnt[i] = r.rng_base + len(r.out)
+        self._build_block_tables([r.seq for r in batch], self._h_bt[:B])
+        Bp = next(b for b in self._buckets if b >= B) if self.use_graphs else B
+        if Bp > B:  # padding rows: no cache write, attend to one key of block 0, output ignored
+            self._h_ids[B:Bp] = 0
+            self._h_pos[B:Bp] = 0
+            self._h_slots[B:Bp] = -1
+            self._h_ctx[B:Bp] = 1
+            self._h_bt[B:Bp] = 0
+            self._h_temp[B:Bp] = 0.0
+            self._h_topk[B:Bp] = 1
+            self._h_topp[B:Bp] = 1.0
+            self._h_cnt[B:Bp] = 0
+        for d, h in ((self._d_ids, self._h_ids), (self._d_pos, self._h_pos), (self._d_slots, self._h_slots),
+                     (self._d_ctx, self._h_ctx), (self._d_temp, self._h_temp), (self._d_topk, self._h_topk),
+                     (self._d_topp, self._h_topp), (self._d_cnt, self._h_cnt)):
+            d[:Bp].copy_(h[:Bp], non_blocking=True)
+        self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
+        if self.use_graphs:
+            g = self._graphs.get(Bp)
+            if g is None:
+                g = self._capture(Bp)
+            if g is not None:
+                g.replay()
+                self.stats["graph_replays"] += 1
+            else:
+                self._decode_body(Bp)
+        else:
+            self._decode_body(Bp)
+        if self.is_gpu:
+            self._tp_sync_tokens(self._d_tokens[:Bp])
+            self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+        toks = self._h_tokens[:B].tolist()
+        now = time.perf_counter()
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += B
+        for r, t in zip(batch, toks):
+            self._accept_token(r, int(t), now)
+
+    def _decode_body(self, Bp: int):
+        meta = AttnMeta(decode=True, positions=self._d_pos[:Bp], slots=self._d_slots[:Bp],
+                        block_tables=self._d_bt[:Bp], ctx_lens=self._d_ctx[:Bp], workspace=self._workspace,
+                        part_size=self.part_size)
+        h = self.model.forward(self._d_ids[:Bp], meta, self.kv)
+        logits = self.model.logits(h)
+        if self.is_gpu:
+            ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp], self.seed,
+                              self._d_cnt[:Bp], out=self._d_tokens[:Bp])
+        else:
+            g = torch.Generator().manual_seed(int(self.seed * 7919 + int(self._h_cnt[0])))
+            self._d_tokens[:Bp] = ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp],
+                                                    self.seed, self._d_cnt[:Bp], generator=g)
+            self._h_tokens[:Bp] = self._d_tokens[:Bp]
+
+    def _capture(self, Bp: int):
+        try:
+            s = torch.cuda.Stream(self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):
+                self._decode_body(Bp)  # warm-up (allocator, lazy init) outside the graph
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            torch.cuda.synchronize(self.device)
+            self._d_cnt[:Bp].copy_(self._h_cnt[:Bp])  # the warm-up advanced the RNG counters
+            g = torch.cuda.CUDAGraph()
+            if self._graph_pool is None:
+                self._graph_pool = torch.cuda.graph_pool_handle()
+            with torch.cuda.graph(g, pool=self._graph_pool, stream=s):
+                self._decode_body(Bp)
+            torch.cuda.synchronize(self.device)
+            self._graphs[Bp] = g
+            return g
+        except Exception as exc:  # pragma: no cover - depends on the runtime
+            import logging
+
+            logging.getLogger(__name__).warning("HIP graph capture failed (%s); decode runs eagerly", exc)
+            self.use_graphs = False
+            return None
+
+    def capture_all(self, sizes=None):
+        for b in sizes or self._buckets:
+            if b not in self._graphs:
+                self._capture(b)

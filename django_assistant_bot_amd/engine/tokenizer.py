@@ -1,0 +1,94 @@
+"""Tokenizer facade: a local HF ``tokenizer.json`` when one is provided, else the native hash tokenizer.
+
+The reference uses ``AutoTokenizer.from_pretrained(local_files_only=True)`` (ai/embedders/transformers.py:11,
+ai/providers/transformers.py:18).  Here, a directory with ``tokenizer.json`` is loaded through the
+``tokenizers`` library (no hub access); otherwise the native C++ ``HashTokenizer`` (csrc/runtime/tokenizer.cpp)
+provides the same contract with the model's vocabulary size and special ids.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+
+from ..models.configs import DecoderConfig, EncoderConfig
+from ..ops._lib import native
+
+
+class Tokenizer:
+    def __init__(self, impl, kind: str, hf=None, cls_id=None, sep_id=None, bos_id=None, vocab_size=0):
+        self._impl = impl
+        self._hf = hf
+        self.kind = kind
+        self.cls_id, self.sep_id, self.bos_id = cls_id, sep_id, bos_id
+        self.vocab_size = vocab_size
+
+    # ------------------------------------------------------------------ construction
+    @classmethod
+    def for_encoder(cls, cfg: EncoderConfig, path: str | None = None) -> "Tokenizer":
+        hf = _maybe_hf(path)
+        if hf is not None:
+            return cls(None, "encoder", hf=hf, vocab_size=cfg.vocab_size)
+        n = native()
+        c = n.TokenizerConfig()
+        c.vocab_size = cfg.vocab_size
+        c.first_id = 1000 if cfg.vocab_size > 2000 else 200
+        c.last_id = cfg.vocab_size
+        c.pad_id, c.unk_id, c.cls_id, c.sep_id = 0, 100, 101, 102
+        return cls(n.HashTokenizer(c), "encoder", cls_id=101, sep_id=102, vocab_size=cfg.vocab_size)
+
+    @classmethod
+    def for_decoder(cls, cfg: DecoderConfig, path: str | None = None) -> "Tokenizer":
+        hf = _maybe_hf(path)
+        if hf is not None:
+            return cls(None, "decoder", hf=hf, bos_id=cfg.bos_id, vocab_size=cfg.vocab_size)
+        n = native()
+        c = n.TokenizerConfig()
+        c.vocab_size = cfg.vocab_size
+        specials_start = min([cfg.bos_id, *cfg.eos_ids])
+        c.first_id = 0
+        c.last_id = specials_start
+        c.pad_id = cfg.eos_ids[0]
+        c.unk_id = cfg.eos_ids[0]
+        c.cls_id = cfg.bos_id  # BOS
+        c.sep_id = -1
+        return cls(n.HashTokenizer(c), "decoder", bos_id=cfg.bos_id, vocab_size=cfg.vocab_size)
+
+    # ------------------------------------------------------------------ API
+    def encode(self, text: str, add_special: bool = True, max_len: int = 0) -> list[int]:
+        if self._hf is not None:
+            ids = self._hf.encode(text, add_special_tokens=add_special).ids
+            if max_len and len(ids) > max_len:
+                ids = ids[: max_len - 1] + ids[-1:] if self.kind == "encoder" else ids[:max_len]
+            return ids
+        return self._impl.encode(text, add_special, max_len)
+
+    def encode_batch(self, texts: list[str], add_special: bool = True, max_len: int = 0, threads: int = 8):
+        """-> (flat int32 ids, int64 offsets[n+1])"""
+        if self._hf is not None:
+            seqs = [self.encode(t, add_special, max_len) for t in texts]
+            offs = np.zeros(len(seqs) + 1, dtype=np.int64)
+            np.cumsum([len(s) for s in seqs], out=offs[1:])
+            flat = np.fromiter((i for s in seqs for i in s), dtype=np.int32, count=int(offs[-1]))
+            return flat, offs
+        return self._impl.encode_batch(list(texts), add_special, max_len, threads)
+
+    def decode(self, ids, skip_special: bool = True) -> str:
+        ids = [int(i) for i in ids]
+        if self._hf is not None:
+            return self._hf.decode(ids, skip_special_tokens=skip_special)
+        return self._impl.decode(ids, skip_special)
+
+    def count_tokens(self, text: str) -> int:
+        return len(self.encode(text, add_special=False))
+
+
+def _maybe_hf(path):
+    if not path:
+        return None
+    f = os.path.join(path, "tokenizer.json") if os.path.isdir(path) else path
+    if not os.path.exists(f):
+        return None
+    from tokenizers import Tokenizer as HFTokenizer
+
+    return HFTokenizer.from_file(f)

@@ -1,0 +1,184 @@
+"""Exact in-HBM cosine top-k index: the pgvector replacement.
+
+The reference stores 768-d vectors in PostgreSQL (``VectorField`` + HNSW m=16/ef_construction=64,
+storage/models.py:32-58) and searches with ``qs.annotate(distance=CosineDistance(field, q))
+.order_by('distance')[:n]`` (rag/services/search_service.py:185-196) -- approximate, on the CPU, one
+query at a time.  Here rows live L2-normalised in bf16 in HBM (1M x 768 = 1.5 GB, noise next to
+288 GB), every query of a batch is scored against every live row by the MFMA GEMM kernel with the
+filter applied in its epilogue (row tombstones, per-query group = bot, optional allow-bitmask for
+arbitrary QuerySet filters), and the exact top-k is selected by the radix-select kernel.
+Recall is 1.0 by construction.  Distance semantics match pgvector: ``1 - cos``.
+
+The index is a cache of the ORM (source of truth); it supports upsert, delete (tombstone + lazy
+compaction), growth, and safetensors snapshots for warm starts.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+
+
+class VectorIndex:
+    def __init__(self, dim: int, device=None, capacity: int = 4096, dtype=torch.bfloat16):
+        self.dim = dim
+        self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
+        self.dtype = dtype
+        self._cap = 0
+        self.n = 0  # rows in use (live + tombstoned)
+        self.vecs = self.row_ids = self.row_docs = self.row_group = None
+        self._row_of: dict[int, int] = {}
+        self._dead = 0
+        self._grow(max(64, capacity))
+
+    # ------------------------------------------------------------------ storage
+    def _grow(self, cap: int):
+        cap = (cap + 63) // 64 * 64
+        dev = self.device
+        vecs = torch.zeros((cap, self.dim), dtype=self.dtype, device=dev)
+        ids = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+        docs = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+        grp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
+        if self.n:
+            vecs[: self.n] = self.vecs[: self.n]
+            ids[: self.n] = self.row_ids[: self.n]
+            docs[: self.n] = self.row_docs[: self.n]
+            grp[: self.n] = self.row_group[: self.n]
+        self.vecs, self.row_ids, self.row_docs, self.row_group = vecs, ids, docs, grp
+        self._cap = cap
+
+    def __len__(self) -> int:
+        return len(self._row_of)
+
+    def __contains__(self, item_id: int) -> bool:
+        return int(item_id) in self._row_of
+
+    def add(self, ids, vectors, doc_ids=None, groups=None) -> None:
+        """Upsert rows.  ids: int64 [n]; vectors [n, dim] (any float dtype / device); doc_ids int64 [n]
+        (document each row belongs to); groups int32 [n] (e.g. bot id; must be >= 0)."""
+        ids = np.asarray(ids, dtype=np.int64).reshape(-1)
+        n = len(ids)
+        if n == 0:
+            return
+        v = torch.as_tensor(vectors).to(self.device, torch.float32).reshape(n, self.dim)
+        v = F.normalize(v, dim=-1).to(self.dtype)
+        docs = np.full(n, -1, dtype=np.int64) if doc_ids is None else np.asarray(doc_ids, dtype=np.int64)
+        grp = np.zeros(n, dtype=np.int32) if groups is None else np.asarray(groups, dtype=np.int32)
+        if (grp < 0).any():
+            raise ValueError("groups must be >= 0 (negative marks deleted rows)")
+        rows = np.empty(n, dtype=np.int64)
+        fresh = []
+        for i, x in enumerate(ids.tolist()):
+            r = self._row_of.get(x)
+            if r is None:
+                fresh.append(i)
+            else:
+                rows[i] = r
+        if fresh:
+            need = self.n + len(fresh)
+            if need > self._cap:
+                self._grow(max(need, 2 * self._cap))
+            for j, i in enumerate(fresh):
+                rows[i] = self.n + j
+                self._row_of[int(ids[i])] = self.n + j
+            self.n += len(fresh)
+        r = torch.from_numpy(rows).to(self.device)
+        self.vecs[r] = v
+        self.row_ids[r] = torch.from_numpy(ids).to(self.device)
+        self.row_docs[r] = torch.from_numpy(docs).to(self.device)
+        self.row_group[r] = torch.from_numpy(grp).to(self.device)
+
+    def remove(self, ids) -> int:
+        rows = [self._row_of.pop(int(x)) for x in np.asarray(ids).reshape(-1).tolist() if int(x) in self._row_of]
+        if rows:
+            r = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
+            self.row_group[r] = -1
+            self.row_ids[r] = -1
+            self._dead += len(rows)
+            if self._dead > 1024 and self._dead > self.n // 4:
+                self.compact()
+        return len(rows)
+
+    def compact(self) -> None:
+        live = (self.row_group[: self.n] >= 0).nonzero().flatten()
+        m = live.numel()
+        self.vecs[:m] = self.vecs[live]
+        self.row_ids[:m] = self.row_ids[live]
+        self.row_docs[:m] = self.row_docs[live]
+        self.row_group[:m] = self.row_group[live]
+        self.row_group[m: self.n] = -1
+        self.n = m
+        self._dead = 0
+        ids = self.row_ids[:m].cpu().numpy()
+        self._row_of = {int(x): i for i, x in enumerate(ids.tolist())}
+
+    # ------------------------------------------------------------------ search
+    def allow_mask(self, allowed: list) -> torch.Tensor:
+        """Per-query allowed item-id sets -> int32 bitmask [q, ceil(n/32)] over rows."""
+        words = (self.n + 31) // 32
+        m = np.zeros((len(allowed), words * 32), dtype=bool)
+        for qi, ids in enumerate(allowed):
+            rows = [self._row_of[i] for i in ids if i in self._row_of]
+            m[qi, rows] = True
+        bits = m.reshape(len(allowed), words, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)
+        packed = bits.sum(-1).astype(np.uint32).view(np.int32)
+        return torch.from_numpy(np.ascontiguousarray(packed)).to(self.device)
+
+    @torch.inference_mode()
+    def scores(self, queries: torch.Tensor, q_groups=None, allowed=None) -> torch.Tensor:
+        """fp32 cosine similarities [q, n] (-inf for filtered / deleted rows)."""
+        q = F.normalize(torch.as_tensor(queries).to(self.device, torch.float32), dim=-1).to(self.dtype)
+        qg = None if q_groups is None else torch.as_tensor(q_groups, dtype=torch.int32).to(self.device)
+        allow = None if allowed is None else self.allow_mask(allowed)
+        n = max(self.n, 4)
+        n = (n + 3) // 4 * 4
+        return ops.gemm_bt(q, self.vecs[:n], epilogue=ops.EPI_SCORES, out_f32=True, row_group=self.row_group[:n],
+                           q_group=qg, allow=allow)
+
+    @torch.inference_mode()
+    def search(self, queries, k: int, q_groups=None, allowed=None):
+        """-> (similarity [q, k] fp32 desc, item ids [q, k] int64 (-1 = none), doc ids [q, k] int64)."""
+        queries = torch.as_tensor(queries)
+        if queries.ndim == 1:
+            queries = queries[None]
+        nq = queries.shape[0]
+        if self.n == 0 or k <= 0:
+            z = torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=self.device)
+            return torch.full((nq, max(k, 0)), float("-inf"), device=self.device), z, z.clone()
+        s = self.scores(queries, q_groups, allowed)
+        kk = min(k, s.shape[1], 1024)
+        vals, rows = ops.topk_rows(s, kk)
+        rows = rows.long()
+        ids = self.row_ids[rows]
+        docs = self.row_docs[rows]
+        dead = torch.isinf(vals)
+        ids = ids.masked_fill(dead, -1)
+        docs = docs.masked_fill(dead, -1)
+        return vals, ids, docs
+
+    # ------------------------------------------------------------------ persistence
+    def save(self, path: str) -> None:
+        from safetensors.torch import save_file
+
+        n = self.n
+        save_file({"vecs": self.vecs[:n].contiguous().cpu(), "ids": self.row_ids[:n].cpu(),
+                   "docs": self.row_docs[:n].cpu(), "group": self.row_group[:n].cpu()}, path,
+                  metadata={"dim": str(self.dim)})
+
+    @classmethod
+    def load(cls, path: str, device=None) -> "VectorIndex":
+        from safetensors.torch import load_file
+
+        st = load_file(path)
+        idx = cls(st["vecs"].shape[1], device, capacity=max(64, st["vecs"].shape[0]), dtype=st["vecs"].dtype)
+        n = st["vecs"].shape[0]
+        idx.vecs[:n] = st["vecs"].to(idx.device)
+        idx.row_ids[:n] = st["ids"].to(idx.device)
+        idx.row_docs[:n] = st["docs"].to(idx.device)
+        idx.row_group[:n] = st["group"].to(idx.device)
+        idx.n = n
+        idx._row_of = {int(x): i for i, x in enumerate(st["ids"].tolist()) if x >= 0}
+        idx._dead = n - len(idx._row_of)
+        return idx

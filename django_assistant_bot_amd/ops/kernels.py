@@ -1,0 +1,361 @@
+"""Tensor-level wrappers of the gfx950 kernels.
+
+Each function validates shapes / dtypes / devices on the host BEFORE launching (a hand-written
+kernel that is fed a wrong shape faults the GPU), then enqueues on the current HIP stream, which
+makes every op capturable into a HIP graph.  CPU tensors run ``ops.reference``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+
+from . import reference as ref
+from ._lib import expect, expect_bf16_contig, native, ptr, same_device, stream
+
+EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SCORES = ref.EPI_NONE, ref.EPI_GELU, ref.EPI_SWIGLU, ref.EPI_SCORES
+
+
+def _i32(t: torch.Tensor) -> None:
+    if t.dtype != torch.int32 or not t.is_contiguous():
+        raise TypeError("expected a contiguous int32 tensor")
+
+
+# ----------------------------------------------------------------------------------------------
+# normalisation / embeddings / pooling
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None):
+    """RMSNorm over the last dim; with ``residual`` the input is ``x + residual`` and the sum is
+    also returned (fused residual stream).  Returns (out, residual_out)."""
+    if not x.is_cuda:
+        return ref.rmsnorm(x, w, eps, residual)
+    expect_bf16_contig(x, w, residual)
+    same_device(x, w, residual)
+    cols = x.shape[-1]
+    rows = x.numel() // cols
+    expect(w.numel() == cols, "rmsnorm weight size mismatch")
+    expect(residual is None or residual.shape == x.shape, "residual shape mismatch")
+    out = torch.empty_like(x)
+    res_out = torch.empty_like(x) if residual is not None else None
+    native().rmsnorm(ptr(out), ptr(res_out), ptr(x), ptr(residual), ptr(w), rows, cols, float(eps), stream(x))
+    return out, res_out
+
+
+def layernorm(x, gamma, beta, eps, residual=None):
+    if not x.is_cuda:
+        return ref.layernorm(x, gamma, beta, eps, residual)
+    expect_bf16_contig(x, gamma, beta, residual)
+    same_device(x, gamma, beta, residual)
+    cols = x.shape[-1]
+    rows = x.numel() // cols
+    expect(gamma.numel() == cols and beta.numel() == cols, "layernorm affine size mismatch")
+    expect(residual is None or residual.shape == x.shape, "residual shape mismatch")
+    out = torch.empty_like(x)
+    native().layernorm(ptr(out), ptr(x), ptr(residual), ptr(gamma), ptr(beta), rows, cols, float(eps), stream(x))
+    return out
+
+
+def bert_embed(ids, pos_ids, type_ids, word, pos, typ, gamma, beta, eps):
+    if not ids.is_cuda:
+        return ref.bert_embed(ids, pos_ids, type_ids, word, pos, typ, gamma, beta, eps)
+    _i32(ids)
+    _i32(pos_ids)
+    if type_ids is not None:
+        _i32(type_ids)
+    expect_bf16_contig(word, pos, typ, gamma, beta)
+    expect(ids.shape == pos_ids.shape, "ids / position ids mismatch")
+    H = word.shape[1]
+    out = torch.empty((ids.numel(), H), dtype=word.dtype, device=ids.device)
+    native().bert_embed(ptr(out), ptr(ids), ptr(pos_ids), ptr(type_ids), ptr(word), ptr(pos), ptr(typ), ptr(gamma),
+                        ptr(beta), ids.numel(), H, float(eps), stream(ids))
+    return out
+
+
+def embed_gather(ids, table):
+    if not ids.is_cuda:
+        return ref.embed_gather(ids, table)
+    _i32(ids)
+    expect_bf16_contig(table)
+    out = torch.empty((ids.numel(), table.shape[1]), dtype=table.dtype, device=ids.device)
+    native().embed_gather(ptr(out), ptr(ids), ptr(table), ids.numel(), table.shape[1], stream(ids))
+    return out
+
+
+def mean_pool(hidden, cu_seqlens, normalize=False, want_bf16=False):
+    """Mean over each packed sequence (all tokens, as the reference).  Returns fp32 [B, H]
+    (and a bf16 copy when ``want_bf16``)."""
+    if not hidden.is_cuda:
+        out = ref.mean_pool(hidden, cu_seqlens, normalize)
+        return (out, out.to(torch.bfloat16)) if want_bf16 else out
+    expect_bf16_contig(hidden)
+    _i32(cu_seqlens)
+    B = cu_seqlens.numel() - 1
+    H = hidden.shape[1]
+    expect(H <= 4096, "mean_pool supports hidden <= 4096")
+    out = torch.empty((B, H), dtype=torch.float32, device=hidden.device)
+    ob = torch.empty((B, H), dtype=torch.bfloat16, device=hidden.device) if want_bf16 else None
+    native().mean_pool(ptr(out), ptr(ob), ptr(hidden), ptr(cu_seqlens), B, H, int(bool(normalize)), stream(hidden))
+    return (out, ob) if want_bf16 else out
+
+
+# ----------------------------------------------------------------------------------------------
+# element-wise
+
+
+def gelu(x, bias=None, out=None):
+    if not x.is_cuda:
+        return ref.gelu(x, bias)
+    expect_bf16_contig(x, bias)
+    cols = x.shape[-1]
+    out = torch.empty_like(x) if out is None else out
+    native().gelu(ptr(out), ptr(x), ptr(bias), x.numel() // cols, cols, stream(x))
+    return out
+
+
+def silu_mul(x):
+    """x [..., 2F] = [gate | up] -> silu(gate) * up  [..., F]"""
+    if not x.is_cuda:
+        return ref.silu_mul(x)
+    expect_bf16_contig(x)
+    F2 = x.shape[-1]
+    rows = x.numel() // F2
+    out = torch.empty((*x.shape[:-1], F2 // 2), dtype=x.dtype, device=x.device)
+    native().silu_mul(ptr(out), ptr(x), rows, F2 // 2, stream(x))
+    return out
+
+
+def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D):
+    """Applies RoPE to the q/k heads of ``qkv`` [T, (Hq+2Hkv)*D]; writes k, v into the paged caches
+    [num_blocks, Hkv, block_size, D] at ``slots`` (int64, <0 skipped); returns q [T, Hq, D]."""
+    block_size = k_cache.shape[2]
+    if not qkv.is_cuda:
+        return ref.rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, block_size)
+    expect_bf16_contig(qkv, k_cache, v_cache)
+    _i32(positions)
+    expect(slots.dtype == torch.int64 and slots.is_contiguous(), "slots must be contiguous int64")
+    expect(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous(), "cos_sin must be contiguous fp32")
+    T = qkv.shape[0]
+    expect(qkv.shape[1] == (Hq + 2 * Hkv) * D, "qkv width mismatch")
+    expect(positions.numel() == T and slots.numel() == T, "positions / slots length mismatch")
+    expect(tuple(k_cache.shape[1:]) == (Hkv, block_size, D) and k_cache.shape == v_cache.shape, "cache shape mismatch")
+    expect(cos_sin.shape[1] == D // 2, "cos/sin table width mismatch")
+    q = torch.empty((T, Hq, D), dtype=qkv.dtype, device=qkv.device)
+    native().rope_kv_write(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache), ptr(v_cache),
+                           ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv))
+    return q
+
+
+# ----------------------------------------------------------------------------------------------
+# attention
+
+
+def _head_strides(t: torch.Tensor):
+    # t viewed as [tokens, heads, D] with unit stride on D
+    expect(t.stride(-1) == 1, "attention operands need unit stride on the head dim")
+    return t.stride(0), t.stride(1)
+
+
+def flash_attention_packed(q, k, v, cu_q, cu_k, max_seqlen_q, causal=False, scale=None, out=None):
+    """Variable-length attention over packed sequences.  q [Tq, Hq, D], k/v [Tk, Hkv, D] may be
+    strided views of a fused QKV buffer.  Returns [Tq, Hq, D] contiguous."""
+    D = q.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if not q.is_cuda:
+        return ref.flash_attention_packed(q, k, v, cu_q, cu_k, causal, scale)
+    _i32(cu_q)
+    _i32(cu_k)
+    expect(q.dtype == torch.bfloat16 and k.dtype == torch.bfloat16 and v.dtype == torch.bfloat16, "bf16 required")
+    expect(D in (32, 64, 128), "head dim must be 32, 64 or 128")
+    Hq, Hkv = q.shape[1], k.shape[1]
+    expect(Hq % Hkv == 0, "GQA requires Hq % Hkv == 0")
+    expect(k.stride() == v.stride(), "k and v must share strides")
+    qst, qsh = _head_strides(q)
+    kst, ksh = _head_strides(k)
+    for s in (qst, qsh, kst, ksh):
+        expect(s % 8 == 0, "attention strides must be multiples of 8 elements (16 B)")
+    out = torch.empty((q.shape[0], Hq, D), dtype=q.dtype, device=q.device) if out is None else out
+    B = cu_q.numel() - 1
+    native().flash_attention(ptr(q), qst, qsh, ptr(k), ptr(v), kst, ksh, 0, 0, 0, 0, 0, ptr(out), out.stride(0),
+                             out.stride(1), ptr(cu_q), ptr(cu_k), 0, B, int(max_seqlen_q), Hq, Hkv, D,
+                             int(bool(causal)), 0, float(scale), stream(q))
+    return out
+
+
+def flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_seqlen_q, causal=True, scale=None,
+                          out=None):
+    """Prefill attention: q [Tq, Hq, D] packed by cu_q, keys/values of each sequence are its first
+    ctx_lens[b] tokens in the paged caches (the query chunk is the tail of that context)."""
+    D = q.shape[-1]
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if not q.is_cuda:
+        return ref.flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, causal, scale)
+    _i32(cu_q)
+    _i32(ctx_lens)
+    _i32(block_tables)
+    expect_bf16_contig(k_cache, v_cache)
+    expect(D in (32, 64, 128), "head dim must be 32, 64 or 128")
+    Hq, Hkv, bs = q.shape[1], k_cache.shape[1], k_cache.shape[2]
+    qst, qsh = _head_strides(q)
+    out = torch.empty((q.shape[0], Hq, D), dtype=q.dtype, device=q.device) if out is None else out
+    B = cu_q.numel() - 1
+    expect(block_tables.shape[0] >= B and ctx_lens.numel() >= B, "block table / ctx_lens rows < batch")
+    native().flash_attention(ptr(q), qst, qsh, 0, 0, 0, 0, ptr(k_cache), ptr(v_cache), ptr(block_tables),
+                             block_tables.shape[1], bs, ptr(out), out.stride(0), out.stride(1), ptr(cu_q), 0,
+                             ptr(ctx_lens), B, int(max_seqlen_q), Hq, Hkv, D, int(bool(causal)), 1, float(scale),
+                             stream(q))
+    return out
+
+
+class DecodeWorkspace:
+    """Partition buffers of the split-K paged decode; allocated once (graph-capture safe)."""
+
+    def __init__(self, max_batch, Hq, D, max_parts, device):
+        self.max_parts = max_parts
+        self.o = torch.empty((max_batch * Hq * max_parts * D,), dtype=torch.float32, device=device)
+        self.m = torch.empty((max_batch * Hq * max_parts,), dtype=torch.float32, device=device)
+        self.l = torch.empty((max_batch * Hq * max_parts,), dtype=torch.float32, device=device)
+
+
+def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
+                 scale=None, out=None):
+    """q [B, Hq, D] (one new token per sequence) over the paged caches."""
+    B, Hq, D = q.shape
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if not q.is_cuda:
+        return ref.paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, scale)
+    _i32(ctx_lens)
+    _i32(block_tables)
+    expect_bf16_contig(q, k_cache, v_cache)
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    expect(D in (64, 128), "decode head dim must be 64 or 128")
+    expect(Hq % Hkv == 0 and Hq // Hkv <= 16, "GQA group must be <= 16")
+    expect(part_size % 128 == 0, "part_size must be a multiple of 128")
+    expect(block_tables.shape[0] >= B and ctx_lens.numel() >= B, "block table / ctx_lens rows < batch")
+    max_parts = workspace.max_parts if workspace is not None else 1
+    if workspace is None:
+        # single partition covering the longest allowed context
+        part_size = max(part_size, ((block_tables.shape[1] * bs + 127) // 128) * 128)
+        ws_o = ws_m = ws_l = None
+    else:
+        expect(workspace.o.numel() >= B * Hq * max_parts * D, "decode workspace too small")
+        ws_o, ws_m, ws_l = workspace.o, workspace.m, workspace.l
+    out = torch.empty_like(q) if out is None else out
+    native().paged_decode_attention(ptr(q), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
+                                    ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), B, Hq, Hkv, D,
+                                    int(part_size), int(max_parts), float(scale), stream(q))
+    return out
+
+
+# ----------------------------------------------------------------------------------------------
+# GEMM
+
+
+def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, row_group=None, q_group=None,
+            allow=None, out=None):
+    """C = A . B^T (+bias) (+act) (+residual) on MFMA; A [M, K], B [N, K] (K-contiguous rows)."""
+    if not A.is_cuda:
+        return ref.gemm_bt(A, B, bias, residual, epilogue, out_f32, row_group, q_group, allow)
+    expect(A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 operands required")
+    expect(A.stride(-1) == 1 and B.stride(-1) == 1, "operands must be K-contiguous")
+    M, K = A.shape
+    N = B.shape[0]
+    expect(B.shape[1] == K, "inner dims mismatch")
+    expect(K % 64 == 0 and N % 4 == 0, "gemm_bt needs K % 64 == 0 and N % 4 == 0")
+    expect(A.stride(0) % 8 == 0 and B.stride(0) % 8 == 0, "row strides must be multiples of 8")
+    if bias is not None:
+        expect_bf16_contig(bias)
+        expect(bias.numel() == N, "bias size mismatch")
+    n_out = N // 2 if epilogue == EPI_SWIGLU else N
+    if epilogue == EPI_SWIGLU:
+        expect(N % 32 == 0 and not out_f32, "swiglu epilogue needs N % 32 == 0 and bf16 output")
+    if residual is not None:
+        expect(residual.dtype == torch.bfloat16 and residual.stride(-1) == 1, "residual must be bf16 row-major")
+        expect(tuple(residual.shape) == (M, n_out), "residual shape mismatch")
+    allow_words = 0
+    if allow is not None:
+        expect(allow.dtype == torch.int32 and allow.is_contiguous() and allow.shape[0] == M, "allow mask shape")
+        allow_words = allow.shape[1]
+        expect(allow_words * 32 >= N, "allow mask too narrow")
+    if row_group is not None:
+        _i32(row_group)
+        expect(row_group.numel() >= N, "row_group shorter than N")
+    if q_group is not None:
+        _i32(q_group)
+        expect(q_group.numel() >= M, "q_group shorter than M")
+    dtype = torch.float32 if out_f32 else torch.bfloat16
+    if out is None:
+        out = torch.empty((M, n_out), dtype=dtype, device=A.device)
+    expect(out.dtype == dtype and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output buffer")
+    native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
+                     residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), int(out_f32),
+                     ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A))
+    return out
+
+
+def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
+    """[F, H] gate and up weights -> [2F, H] interleaved in 16-row groups [g16 | u16 | g16 | u16 ...]
+    (the layout the SWIGLU epilogue of gemm_bt consumes)."""
+    Fd, H = w_gate.shape
+    assert Fd % 16 == 0
+    g = w_gate.view(Fd // 16, 16, H)
+    u = w_up.view(Fd // 16, 16, H)
+    return torch.stack([g, u], dim=1).reshape(2 * Fd, H).contiguous()
+
+
+# ----------------------------------------------------------------------------------------------
+# selection
+
+
+def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, generator=None, out=None):
+    """temperature / top_k (int32) / top_p per row; counters int64 per row (advanced in-kernel)."""
+    if not logits.is_cuda:
+        return ref.sample_hf(logits, temperature, top_k, top_p, generator)
+    rows, vocab = logits.shape
+    expect(logits.stride(-1) == 1, "logits rows must be contiguous")
+    expect(logits.dtype in (torch.float32, torch.bfloat16), "logits must be fp32 or bf16")
+    expect(temperature.dtype == torch.float32 and temperature.numel() >= rows, "temperature")
+    expect(top_p.dtype == torch.float32 and top_p.numel() >= rows, "top_p")
+    _i32(top_k)
+    expect(counters.dtype == torch.int64 and counters.numel() >= rows, "counters")
+    out = torch.empty((rows,), dtype=torch.int32, device=logits.device) if out is None else out
+    native().sample_tokens(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab,
+                           ptr(temperature), ptr(top_k), ptr(top_p), int(seed) & ((1 << 64) - 1), ptr(counters),
+                           ptr(out), 0, stream(logits))
+    return out
+
+
+def topk_rows(scores, k, index_base=0, want_global=False):
+    """Exact per-row top-k of fp32 scores, sorted descending.  Returns (values, idx int32) or, with
+    ``want_global``, (values, idx + index_base as int64)."""
+    rows, n = scores.shape
+    expect(1 <= k <= min(n, 1024), "1 <= k <= min(n, 1024)")
+    if not scores.is_cuda:
+        v, i = ref.topk_rows(scores, k)
+        return (v, i.long() + index_base) if want_global else (v, i)
+    expect(scores.dtype == torch.float32 and scores.stride(-1) == 1, "scores must be fp32 with contiguous rows")
+    vals = torch.empty((rows, k), dtype=torch.float32, device=scores.device)
+    if want_global:
+        idx = torch.empty((rows, k), dtype=torch.int64, device=scores.device)
+        native().topk_rows(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), 0, int(index_base), ptr(idx),
+                           stream(scores))
+    else:
+        idx = torch.empty((rows, k), dtype=torch.int32, device=scores.device)
+        native().topk_rows(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), ptr(idx), 0, 0, stream(scores))
+    return vals, idx
+
+
+def linear(x, w, b=None, residual=None, act=None, use_native=False):
+    """y = x W^T (+b) (+act) (+residual).  Fused epilogues run on the native MFMA GEMM; a plain
+    projection may run on hipBLASLt through torch (vendor library GEMM)."""
+    if not x.is_cuda:
+        epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]
+        return ref.gemm_bt(x, w, b, residual, epi)
+    if act is None and residual is None and not use_native:
+        return F.linear(x, w, b)
+    epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]
+    x2 = x.reshape(-1, x.shape[-1])
+    r2 = residual.reshape(x2.shape[0], -1) if residual is not None else None
+    y = gemm_bt(x2, w, b, r2, epi)
+    return y.view(*x.shape[:-1], y.shape[-1])

@@ -1,0 +1,94 @@
+"""Process-group bootstrap: one process per GPU, ``torch.distributed`` over RCCL (backend "nccl" on
+ROCm) for GPU collectives on xGMI, gloo for CPU tests.  Reads RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR / MASTER_PORT from the environment (torchrun convention).
+
+The reference has no collective library at all; its fan-out is Celery/HTTP.  The
+engine keeps Celery/HTTP as the control plane and uses these groups for the data plane:
+  * ``world``  -- DP replicas of the RAG pipeline and the sharded vector index (all-gather merge);
+  * ``tp``     -- tensor-parallel generator groups (two all-reduces per layer).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", 0))))
+
+
+def init(backend: str | None = None, device_type: str | None = None, timeout_s: int = 600) -> DistInfo:
+    """Initialise the default group when WORLD_SIZE > 1 (idempotent).  GPU ranks bind cuda:LOCAL_RANK."""
+    rank, world, local = env_world()
+    if device_type is None:
+        device_type = "cuda" if torch.cuda.is_available() else "cpu"
+    if device_type == "cuda":
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if backend is None:
+        backend = "nccl" if device_type == "cuda" else "gloo"
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = device
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s), **kw)
+    return DistInfo(rank, world, local, device, backend if world > 1 else "none")
+
+
+def barrier(info: DistInfo | None = None) -> None:
+    if dist.is_available() and dist.is_initialized():
+        if info is not None and info.backend == "nccl":
+            dist.barrier(device_ids=[info.local_rank])
+        else:
+            dist.barrier()
+
+
+def tp_groups(tp_size: int):
+    """Consecutive ranks form tensor-parallel groups (one xGMI-connected node: any grouping is one hop).
+    Returns (my_group, my_tp_rank, dp_rank)."""
+    rank, world, _ = env_world()
+    if tp_size <= 1:
+        return None, 0, rank
+    assert world % tp_size == 0, "WORLD_SIZE must be a multiple of the TP size"
+    mine = None
+    for start in range(0, world, tp_size):
+        ranks = list(range(start, start + tp_size))
+        g = dist.new_group(ranks)
+        if rank in ranks:
+            mine = g
+    return mine, rank % tp_size, rank // tp_size
+
+
+def max_over_ranks(value: float, device) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown() -> None:
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()

@@ -1,0 +1,231 @@
+"""Numerics of every hand-written gfx950 kernel against the plain-PyTorch fp32 reference of the same op."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from django_assistant_bot_amd import ops  # noqa: E402
+from django_assistant_bot_amd.ops import reference as ref  # noqa: E402
+
+DEV = "cuda"
+
+
+def bf(*shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV) * scale).to(torch.bfloat16)
+
+
+def close(a, b, atol=2e-2, rtol=2e-2):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    assert torch.allclose(a, b, atol=atol, rtol=rtol), f"max abs err {err}"
+
+
+@pytest.fixture(autouse=True)
+def _seed():
+    torch.manual_seed(0)
+
+
+def test_native_loaded():
+    m = ops.native()
+    assert m.__file__.endswith(".so")
+
+
+@pytest.mark.parametrize("cols", [256, 768, 4096, 8192])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_rmsnorm(cols, with_res):
+    x, w = bf(37, cols), bf(cols)
+    r = bf(37, cols) if with_res else None
+    out, res = ops.rmsnorm(x, w, 1e-5, residual=r)
+    eo, er = ref.rmsnorm(x, w, 1e-5, residual=r)
+    close(out, eo)
+    if with_res:
+        assert torch.equal(res, er)
+
+
+@pytest.mark.parametrize("cols", [384, 768, 1024])
+def test_layernorm(cols):
+    x, r, g, b = bf(29, cols), bf(29, cols), bf(cols), bf(cols)
+    close(ops.layernorm(x, g, b, 1e-12, residual=r), ref.layernorm(x, g, b, 1e-12, residual=r))
+    close(ops.layernorm(x, g, b, 1e-12), ref.layernorm(x, g, b, 1e-12))
+
+
+def test_bert_embed_and_pool():
+    V, P, H = 500, 64, 768
+    word, pos, typ, g, b = bf(V, H), bf(P, H), bf(2, H), bf(H), bf(H)
+    ids = torch.randint(0, V, (41,), device=DEV, dtype=torch.int32)
+    pids = torch.randint(0, P, (41,), device=DEV, dtype=torch.int32)
+    close(ops.bert_embed(ids, pids, None, word, pos, typ, g, b, 1e-12),
+          ref.bert_embed(ids, pids, None, word, pos, typ, g, b, 1e-12))
+    h = bf(41, H)
+    cu = torch.tensor([0, 5, 5, 30, 41], dtype=torch.int32, device=DEV)
+    for norm in (False, True):
+        got, gotb = ops.mean_pool(h, cu, normalize=norm, want_bf16=True)
+        exp = ref.mean_pool(h, cu, norm)
+        close(got, exp, atol=1e-3, rtol=1e-3)
+        close(gotb, exp)
+    close(ops.embed_gather(ids, word), word[ids.long()], atol=0, rtol=0)
+
+
+def test_gelu_silu():
+    x, b = bf(33, 3072), bf(3072)
+    close(ops.gelu(x, b), ref.gelu(x, b))
+    y = bf(17, 2 * 1408)
+    close(ops.silu_mul(y), ref.silu_mul(y))
+
+
+def test_rope_kv_write():
+    T, Hq, Hkv, D, bs, nb = 50, 4, 2, 128, 64, 8
+    qkv = bf(T, (Hq + 2 * Hkv) * D)
+    inv = ref.llama3_inv_freq(D, 500000.0, {"factor": 8.0})
+    cs = ref.rope_cos_sin(inv, 4096).to(DEV)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int64)
+    slots[3] = -1
+    kc, vc = torch.zeros(nb, Hkv, bs, D, device=DEV, dtype=torch.bfloat16), torch.zeros(nb, Hkv, bs, D, device=DEV,
+                                                                                          dtype=torch.bfloat16)
+    kr, vr = kc.cpu(), vc.cpu()
+    q = ops.rope_kv_write(qkv, pos, cs, kc, vc, slots, Hq, Hkv, D)
+    qr = ref.rope_kv_write(qkv.cpu(), pos.cpu(), cs.cpu(), kr, vr, slots.cpu(), Hq, Hkv, D, bs)
+    close(q.cpu(), qr)
+    close(kc.cpu(), kr)
+    assert torch.equal(vc.cpu(), vr)
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+@pytest.mark.parametrize("causal", [False, True])
+def test_flash_packed(D, causal):
+    lens = [5, 70, 130, 1]
+    Hq, Hkv = (8, 2) if causal else (4, 4)
+    T = sum(lens)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    qkv = bf(T, (Hq + 2 * Hkv) * D)
+    q = qkv[:, :Hq * D].view(T, Hq, D)
+    k = qkv[:, Hq * D:(Hq + Hkv) * D].view(T, Hkv, D)
+    v = qkv[:, (Hq + Hkv) * D:].view(T, Hkv, D)
+    out = ops.flash_attention_packed(q, k, v, cu, cu, max(lens), causal=causal)
+    exp = ref.flash_attention_packed(q, k, v, cu, cu, causal, 1 / math.sqrt(D))
+    close(out, exp)
+
+
+def _paged_setup(ctx, Hkv, D, bs, nb):
+    kc = bf(nb, Hkv, bs, D)
+    vc = bf(nb, Hkv, bs, D)
+    maxb = max(math.ceil(c / bs) for c in ctx)
+    perm = torch.randperm(nb)
+    bt = torch.zeros(len(ctx), maxb + 2, dtype=torch.int32)
+    o = 0
+    for i, c in enumerate(ctx):
+        n = math.ceil(c / bs)
+        bt[i, :n] = perm[o:o + n].to(torch.int32)
+        o += n
+    return kc, vc, bt.to(DEV)
+
+
+def test_flash_paged_prefill():
+    ctx, qlen = [100, 200, 64, 1000], [30, 64, 64, 257]
+    Hq, Hkv, D, bs = 8, 2, 128, 64
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 64)
+    q = bf(sum(qlen), Hq, D)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(qlen), causal=True)
+    exp = ref.flash_attention_paged(q, kc, vc, bt, cu, ctxt, True, 1 / math.sqrt(D))
+    close(out, exp)
+
+
+@pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
+@pytest.mark.parametrize("split", [False, True])
+def test_paged_decode(Hq, Hkv, split):
+    ctx = [1, 63, 64, 65, 700, 1500, 2049]
+    D, bs = 128, 64
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 128)
+    q = bf(len(ctx), Hq, D)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    ws = ops.DecodeWorkspace(len(ctx), Hq, D, math.ceil(4096 / 512), DEV) if split else None
+    out = ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws)
+    exp = ref.paged_decode(q, kc, vc, bt, ctxt, 1 / math.sqrt(D))
+    close(out, exp)
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 384, 256), (1, 2304, 768), (513, 1000, 64), (128, 128, 4096)])
+def test_gemm_epilogues(M, N, K):
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    bias, res = bf(N), bf(M, N)
+    close(ops.gemm_bt(A, B), ref.gemm_bt(A, B), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, bias, res), ref.gemm_bt(A, B, bias, res), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, bias, None, ops.EPI_GELU), ref.gemm_bt(A, B, bias, None, ops.EPI_GELU), atol=3e-2,
+          rtol=2e-2)
+    close(ops.gemm_bt(A, B, out_f32=True), ref.gemm_bt(A, B, out_f32=True), atol=1e-2, rtol=1e-2)
+
+
+def test_gemm_swiglu():
+    M, F, K = 77, 256, 512
+    x, wg, wu = bf(M, K), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
+    w = ops.interleave_gate_up(wg, wu)
+    got = ops.gemm_bt(x, w, epilogue=ops.EPI_SWIGLU)
+    exp = ref.silu_mul(ref.gemm_bt(x, torch.cat([wg, wu], 0)))
+    close(got, exp, atol=3e-2, rtol=3e-2)
+
+
+def test_gemm_scores_masks():
+    Q, N, K = 5, 3000, 768
+    q = torch.nn.functional.normalize(torch.randn(Q, K, device=DEV), dim=-1).to(torch.bfloat16)
+    x = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
+    qg = torch.tensor([-1, 0, 1, 2, 0], device=DEV, dtype=torch.int32)
+    allow = torch.randint(-2 ** 31, 2 ** 31 - 1, (Q, (N + 31) // 32), device=DEV, dtype=torch.int32)
+    got = ops.gemm_bt(q, x, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg, allow=allow)
+    exp = ref.gemm_bt(q, x, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg, allow=allow)
+    assert torch.equal(torch.isinf(got), torch.isinf(exp))
+    fin = ~torch.isinf(exp)
+    close(got[fin], exp[fin], atol=1e-2, rtol=1e-2)
+
+
+def test_topk_rows():
+    s = torch.randn(7, 100003, device=DEV)
+    s[2, 50:] = float("-inf")
+    for k in (1, 5, 250, 1024):
+        v, i = ops.topk_rows(s, k)
+        ev, _ = torch.topk(s, k, dim=-1)
+        assert torch.equal(v, ev)
+        assert torch.equal(torch.gather(s, 1, i.long()), v)
+    v, i = ops.topk_rows(s, 10, index_base=1000, want_global=True)
+    assert i.dtype == torch.int64 and int(i.min()) >= 1000
+
+
+def test_sampling_greedy_and_support():
+    V, R = 128256, 64
+    logits = torch.randn(R, V, device=DEV).to(torch.bfloat16)
+    temp = torch.zeros(R, device=DEV)
+    topk = torch.full((R,), 50, dtype=torch.int32, device=DEV)
+    topp = torch.full((R,), 0.95, device=DEV)
+    cnt = torch.zeros(R, dtype=torch.int64, device=DEV)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt)
+    assert torch.equal(tok.long(), logits.float().argmax(-1))
+    temp.fill_(1.0)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt)
+    top50 = torch.topk(logits.float(), 50, dim=-1).indices
+    assert bool((top50 == tok.long()[:, None]).any(-1).all())
+    assert int(cnt[0]) == 1  # counters advance in-kernel
+
+
+def test_sampling_distribution():
+    R = 4096
+    base = torch.tensor([3.0, 2.0, 1.0, 0.5, -1.0], device=DEV)
+    logits = torch.full((R, 1000), -30.0, device=DEV)
+    logits[:, :5] = base
+    temp = torch.ones(R, device=DEV)
+    topk = torch.full((R,), 3, dtype=torch.int32, device=DEV)
+    topp = torch.ones(R, device=DEV)
+    cnt = torch.arange(R, dtype=torch.int64, device=DEV)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt).long()
+    assert int(tok.max()) <= 2
+    freq = torch.bincount(tok, minlength=3).float() / R
+    p = torch.softmax(base[:3], 0)
+    assert torch.allclose(freq, p, atol=0.03), (freq, p)
+    # top-p 0.7 on probs [.665,.245,.09] keeps {0,1}: ascending cumsum .09 <= .3 drops token 2
+    topp.fill_(0.7)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt).long()
+    assert int(tok.max()) <= 1
