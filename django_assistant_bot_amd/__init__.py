@@ -8,3 +8,8 @@ Subpackages
   utils/     timing, profiling ranges, memory helpers
 """
 __version__ = "0.1.0"
+
+# The HIP runtime must be the one PyTorch ships (libamdhip64.so.7 from torch/lib): importing torch
+# before the native extension makes the extension bind to that already-loaded runtime instead of
+# pulling /opt/rocm's copy into the process first (two HIP runtime versions in one process fail).
+import torch as _torch  # noqa: E402,F401
