@@ -1,0 +1,60 @@
+"""In-process generator on the MI355X engine (replaces the reference's HF ``TransformersProvider``,
+ai/providers/transformers.py:9-94).
+
+Same contract: prompt rendered as ``"role: content"`` lines (no chat template), sampling with
+top_k=50 / top_p=0.95, JSON mode parses the text and falls back to the raw string, usage reports
+prompt/completion token counts, ``length_limited`` when the completion hit the budget.  Differences:
+requests from all concurrent callers share one continuous batch on the GPU (``LLMWorker``), and
+``max_tokens`` bounds the completion only (the reference's ``max_length`` also counted the prompt).
+"""
+from __future__ import annotations
+
+import json
+import logging
+from typing import List
+
+from assistant.ai.domain import AIResponse, Message
+from assistant.ai.providers.base import AIProvider
+
+logger = logging.getLogger(__name__)
+
+
+def render_prompt(messages: List[Message]) -> str:
+    return "\n".join(f"{m['role']}: {m['content']}" for m in messages)
+
+
+class TransformersProvider(AIProvider):
+    def __init__(self, model_name: str, local_files_only: bool = True, **engine_kwargs):
+        from django_assistant_bot_amd.engine.serving import get_llm_worker
+
+        self._model = model_name
+        self._worker = get_llm_worker(model_name, **engine_kwargs)
+        self._tokenizer = self._worker.engine.tokenizer
+
+    @property
+    def context_size(self) -> int:
+        return self._worker.engine.max_model_len
+
+    def calculate_tokens(self, text: str) -> int:
+        return self._tokenizer.count_tokens(text)
+
+    async def get_response(self, messages: List[Message], max_tokens: int = 1024,
+                           json_format: bool = False) -> AIResponse:
+        from django_assistant_bot_amd.engine.llm_engine import SamplingParams
+
+        prompt = render_prompt(messages)
+        ids = self._tokenizer.encode(prompt, add_special=True, max_len=self._worker.engine.max_model_len - 1)
+        params = SamplingParams(max_new_tokens=max_tokens, temperature=1.0, top_k=50, top_p=0.95)
+        out = await self._worker.generate(ids, params)
+        text = out.text.strip()
+        result = text
+        if json_format:
+            try:
+                result = json.loads(text)
+            except json.JSONDecodeError:
+                logger.warning("generator returned non-JSON text in JSON mode")
+        self._record_attempts(1)
+        return AIResponse(result=result,
+                          usage={"model": self._model, "prompt_tokens": out.usage["prompt_tokens"],
+                                 "completion_tokens": out.usage["completion_tokens"]},
+                          length_limited=out.finish_reason == "length")

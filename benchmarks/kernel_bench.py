@@ -1,0 +1,131 @@
+"""Per-kernel timings on the real model shapes (bf16, random data).
+
+GEMM: native MFMA ``gemm_bt`` vs hipBLASLt (torch.nn.functional.linear) on the Llama-3-8B decode /
+prefill and bge-base encoder projections; attention: flash prefill, paged decode; selection kernels.
+Prints one JSON line per measurement (TFLOP/s and effective GB/s).
+"""
+import json
+import math
+import os
+import sys
+
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from django_assistant_bot_amd import ops  # noqa: E402
+
+
+def timeit(fn, iters=20, warmup=3):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters / 1e3
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def gemm_suite(which):
+    shapes = []
+    for M in (1, 32, 64, 128, 256):
+        shapes += [("llama8b-qkv", M, 6144, 4096), ("llama8b-o", M, 4096, 4096), ("llama8b-gateup", M, 28672, 4096),
+                   ("llama8b-down", M, 4096, 14336)]
+    shapes += [("llama8b-lmhead", 64, 128256, 4096)]
+    for M in (4096, 16384):
+        shapes += [("llama8b-qkv", M, 6144, 4096), ("llama8b-gateup", M, 28672, 4096), ("llama8b-down", M, 4096, 14336)]
+    for M in (2048, 32768):
+        shapes += [("bge-qkv", M, 2304, 768), ("bge-o", M, 768, 768), ("bge-up", M, 3072, 768), ("bge-down", M, 768, 3072)]
+    shapes += [("index-scan", 64, 1_000_000, 768), ("index-scan", 512, 1_000_000, 768)]
+    for name, M, N, K in shapes:
+        if which and which not in name:
+            continue
+        a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        b = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
+        flop = 2.0 * M * N * K
+        byts = 2.0 * (M * K + N * K + M * N)
+        res = {"op": name, "M": M, "N": N, "K": K}
+        if name == "index-scan":
+            t_nat = timeit(lambda: ops.gemm_bt(a, b, epilogue=ops.EPI_SCORES, out_f32=True), iters=5)
+            t_lib = timeit(lambda: torch.mm(a, b.t()).float(), iters=5)
+            byts = 2.0 * (M * K + N * K) + 4.0 * M * N
+        else:
+            t_nat = timeit(lambda: ops.gemm_bt(a, b))
+            t_lib = timeit(lambda: F.linear(a, b))
+        res.update(native_us=round(t_nat * 1e6, 1), hipblaslt_us=round(t_lib * 1e6, 1),
+                   native_tflops=round(flop / t_nat / 1e12, 1), hipblaslt_tflops=round(flop / t_lib / 1e12, 1),
+                   native_gbps=round(byts / t_nat / 1e9), hipblaslt_gbps=round(byts / t_lib / 1e9))
+        emit(**res)
+        del a, b
+
+
+def attn_suite():
+    # prefill: 16 sequences x 1024 tokens, Llama-3-8B heads
+    B, T, Hq, Hkv, D, bs = 16, 1024, 32, 8, 128, 64
+    nb = B * T // bs
+    kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(B, T // bs)
+    q = torch.randn(B * T, Hq, D, device="cuda").to(torch.bfloat16)
+    cu = torch.arange(0, B * T + 1, T, dtype=torch.int32, device="cuda")
+    ctx = torch.full((B,), T, dtype=torch.int32, device="cuda")
+    t = timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True))
+    flop = 4.0 * B * Hq * T * T * D / 2
+    emit(op="flash-prefill-causal", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    # encoder: 256 x 128 tokens, bge-base heads (packed)
+    B2, T2, H2, D2 = 256, 128, 12, 64
+    qkv = torch.randn(B2 * T2, 3 * H2 * D2, device="cuda").to(torch.bfloat16)
+    cu2 = torch.arange(0, B2 * T2 + 1, T2, dtype=torch.int32, device="cuda")
+    qv = qkv[:, :H2 * D2].view(-1, H2, D2)
+    kv = qkv[:, H2 * D2:2 * H2 * D2].view(-1, H2, D2)
+    vv = qkv[:, 2 * H2 * D2:].view(-1, H2, D2)
+    t = timeit(lambda: ops.flash_attention_packed(qv, kv, vv, cu2, cu2, T2))
+    flop = 4.0 * B2 * H2 * T2 * T2 * D2
+    emit(op="flash-encoder", B=B2, T=T2, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    # decode: 64 sequences x 1300 context
+    for Bd, C in ((64, 1300), (256, 1300), (64, 4000)):
+        nbd = Bd * math.ceil(C / bs)
+        kc = torch.randn(nbd, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nbd, dtype=torch.int32, device="cuda").view(Bd, -1)
+        qd = torch.randn(Bd, Hq, D, device="cuda").to(torch.bfloat16)
+        ctx = torch.full((Bd,), C, dtype=torch.int32, device="cuda")
+        ws = ops.DecodeWorkspace(Bd, Hq, D, math.ceil(8192 / 512), "cuda")
+        t = timeit(lambda: ops.paged_decode(qd, kc, vc, bt, ctx, 512, ws))
+        byts = 2.0 * Bd * C * Hkv * D * 2
+        emit(op="paged-decode", B=Bd, ctx=C, us=round(t * 1e6, 1), gbps=round(byts / t / 1e9))
+        del kc, vc
+
+
+def select_suite():
+    logits = torch.randn(64, 128256, device="cuda").to(torch.bfloat16)
+    temp = torch.ones(64, device="cuda")
+    topk = torch.full((64,), 50, dtype=torch.int32, device="cuda")
+    topp = torch.full((64,), 0.95, device="cuda")
+    cnt = torch.zeros(64, dtype=torch.int64, device="cuda")
+    t = timeit(lambda: ops.sample_tokens(logits, temp, topk, topp, 1, cnt))
+    emit(op="sample-topk50-topp95", rows=64, vocab=128256, us=round(t * 1e6, 1))
+    s = torch.randn(64, 1_000_000, device="cuda")
+    t = timeit(lambda: ops.topk_rows(s, 250), iters=5)
+    emit(op="topk-250", rows=64, n=1_000_000, us=round(t * 1e6, 1), gbps=round(4 * 64e6 / t / 1e9))
+    x = torch.randn(64, 4096, device="cuda").to(torch.bfloat16)
+    w = torch.randn(4096, device="cuda").to(torch.bfloat16)
+    t = timeit(lambda: ops.rmsnorm(x, w, 1e-5, residual=x))
+    emit(op="rmsnorm+res", rows=64, cols=4096, us=round(t * 1e6, 1))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which in ("all", "gemm"):
+        gemm_suite(None)
+    if which in ("all", "attn"):
+        attn_suite()
+    if which in ("all", "select"):
+        select_suite()

@@ -101,28 +101,26 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
   const int n_tiles = div_up(n_keys, KT);
 
   u32x4 kreg[CH], vreg[CH];
+  // Branch-free staging: rows past the end are clamped to the last valid key (finite data, masked
+  // to -inf in the scores), and the paged block id is looked up once per tile (wave-uniform) --
+  // per-lane lookups behind a branch made the compiler drain vmcnt(0) per 16-B chunk.
   auto load_tile = [&](int kt) {
+    const int k0 = kt * KT;
+    const int last = kv_len - 1 - k0;
+    size_t base;
+    if (PAGED) {
+      const int blk = p.block_tables[(size_t)b * p.max_blocks + k0 / p.block_size];
+      base = (((size_t)blk * p.Hkv + hk) * p.block_size + (k0 % p.block_size)) * D;
+    } else {
+      base = (size_t)(k_start + k0) * p.kv_stride_tok + (size_t)hk * p.kv_stride_head;
+    }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int idx = tid + c * 256;
-      const int row = idx / CPR, ch = idx % CPR;
-      const int key = kt * KT + row;
-      u32x4 z = {0u, 0u, 0u, 0u};
-      kreg[c] = z;
-      vreg[c] = z;
-      if (key < kv_len) {
-        size_t off;
-        if (PAGED) {
-          const int blk = p.block_tables[(size_t)b * p.max_blocks + key / p.block_size];
-          off = (((size_t)blk * p.Hkv + hk) * p.block_size + (key % p.block_size)) * D;
-          kreg[c] = *reinterpret_cast<const u32x4*>(p.k_cache + off + ch * 8);
-          vreg[c] = *reinterpret_cast<const u32x4*>(p.v_cache + off + ch * 8);
-        } else {
-          off = (size_t)(k_start + key) * p.kv_stride_tok + (size_t)hk * p.kv_stride_head;
-          kreg[c] = *reinterpret_cast<const u32x4*>(p.k + off + ch * 8);
-          vreg[c] = *reinterpret_cast<const u32x4*>(p.v + off + ch * 8);
-        }
-      }
+      const int row = min(idx / CPR, last), ch = idx % CPR;
+      const size_t off = base + (PAGED ? (size_t)row * D : (size_t)row * p.kv_stride_tok) + ch * 8;
+      kreg[c] = *reinterpret_cast<const u32x4*>((PAGED ? p.k_cache : p.k) + off);
+      vreg[c] = *reinterpret_cast<const u32x4*>((PAGED ? p.v_cache : p.v) + off);
     }
   };
   auto store_tile = [&]() {
@@ -247,7 +245,7 @@ struct DecodeParams {
 };
 
 template <int D>
-__global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p) {
+__global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int total_items) {
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
@@ -258,161 +256,166 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p) {
   constexpr int STAGE_BYTES = 4 * 2 * SUB_BYTES;
   __shared__ __attribute__((aligned(16))) char smem[STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES];
 
-  const int part = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
-  const int ctx = p.ctx_lens[b];
-  const int k_begin = part * p.part_size;
-  if (k_begin >= ctx) return;
-  const int k_end = min(ctx, k_begin + p.part_size);
   const int G = p.Hq / p.Hkv;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   char* ks = smem + w * 2 * SUB_BYTES;
   char* vs = ks + SUB_BYTES;
 
-  bf16x8 qf[NKK];
-  {
-    const bool qv = li < G;
-    const bf16* qrow = p.q + ((size_t)b * p.Hq + hk * G + (qv ? li : 0)) * D;
-#pragma unroll
-    for (int kk = 0; kk < NKK; ++kk) {
-      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      qf[kk] = qv ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
-    }
-  }
+  // persistent walk over (sequence, kv head, key partition) items; empty partitions cost a compare
+  for (int item = blockIdx.x; item < total_items; item += gridDim.x) {
+    const int part = item % p.max_parts;
+    const int bh = item / p.max_parts;
+    const int hk = bh % p.Hkv, b = bh / p.Hkv;
+    const int ctx = p.ctx_lens[b];
+    const int k_begin = part * p.part_size;
+    if (k_begin >= ctx) continue;
+    const int k_end = min(ctx, k_begin + p.part_size);
 
-  u32x4 kreg[CH], vreg[CH];
-  auto load_sub = [&](int k0) {
+    bf16x8 qf[NKK];
+    {
+      const bool qv = li < G;
+      const bf16* qrow = p.q + ((size_t)b * p.Hq + hk * G + (qv ? li : 0)) * D;
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = lane + c * 64;
-      const int row = idx / CPR, ch = idx % CPR;
-      const int key = k0 + row;
-      u32x4 z = {0u, 0u, 0u, 0u};
-      kreg[c] = z;
-      vreg[c] = z;
-      if (key < k_end) {
-        const int blk = p.block_tables[(size_t)b * p.max_blocks + key / p.block_size];
-        const size_t off = (((size_t)blk * p.Hkv + hk) * p.block_size + (key % p.block_size)) * D + ch * 8;
+      for (int kk = 0; kk < NKK; ++kk) {
+        bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+        qf[kk] = qv ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
+      }
+    }
+
+    u32x4 kreg[CH], vreg[CH];
+    // a 32-key sub-tile never straddles a cache block (block_size % 32 == 0): one uniform lookup
+    auto load_sub = [&](int k0) {
+      const int blk = p.block_tables[(size_t)b * p.max_blocks + k0 / p.block_size];
+      const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (k0 % p.block_size)) * D;
+      const int last = k_end - 1 - k0;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        const int idx = lane + c * 64;
+        const int row = min(idx / CPR, last), ch = idx % CPR;
+        const size_t off = base + (size_t)row * D + ch * 8;
         kreg[c] = *reinterpret_cast<const u32x4*>(p.k_cache + off);
         vreg[c] = *reinterpret_cast<const u32x4*>(p.v_cache + off);
       }
-    }
-  };
+    };
 
-  f32x4 o[NTD];
+    f32x4 o[NTD];
 #pragma unroll
-  for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f, l_run = 0.f;
+    for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -1e30f, l_run = 0.f;
 
-  int k0 = k_begin + w * KT;
-  if (k0 < k_end) load_sub(k0);
-  for (; k0 < k_end; k0 += 4 * KT) {
+    int k0 = k_begin + w * KT;
+    if (k0 < k_end) load_sub(k0);
+    for (; k0 < k_end; k0 += 4 * KT) {
 #pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int idx = lane + c * 64;
-      const int row = idx / CPR, ch = idx % CPR;
-      *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
-      *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
-    }
-    if (k0 + 4 * KT < k_end) load_sub(k0 + 4 * KT);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
-    __builtin_amdgcn_wave_barrier();
-    f32x4 s[2];
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
-        s[m] = mfma16(a, qf[kk], s[m]);
+      for (int c = 0; c < CH; ++c) {
+        const int idx = lane + c * 64;
+        const int row = idx / CPR, ch = idx % CPR;
+        *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
+        *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
       }
-    }
-    float mx = kNegInf;
+      if (k0 + 4 * KT < k_end) load_sub(k0 + 4 * KT);
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+      __builtin_amdgcn_wave_barrier();
+      f32x4 s[2];
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+      for (int m = 0; m < 2; ++m) {
+        s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + 16 * m + 4 * g + r;
-        float v = s[m][r] * p.scale_log2;
-        if (key >= k_end) v = kNegInf;
-        s[m][r] = v;
-        mx = fmaxf(mx, v);
+        for (int kk = 0; kk < NKK; ++kk) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
+          s[m] = mfma16(a, qf[kk], s[m]);
+        }
       }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
-    float ls = 0.f;
+      float mx = kNegInf;
 #pragma unroll
-    for (int m = 0; m < 2; ++m) {
+      for (int m = 0; m < 2; ++m) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(s[m][r] - m_new);
-        s[m][r] = e;
-        ls += e;
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + 16 * m + 4 * g + r;
+          float v = s[m][r] * p.scale_log2;
+          if (key >= k_end) v = kNegInf;
+          s[m][r] = v;
+          mx = fmaxf(mx, v);
+        }
       }
-    }
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
-    bf16x8 pb;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      float ls = 0.f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      pb[j] = (short)f2bf(s[0][j]);
-      pb[j + 4] = (short)f2bf(s[1][j]);
-    }
-    const int qq = li >> 2, pp = li & 3;
+      for (int m = 0; m < 2; ++m) {
 #pragma unroll
-    for (int t = 0; t < NTD; ++t) {
-      o[t] *= alpha;
-      const int ch = 2 * t + (pp >> 1);
-      const int boff = 8 * (pp & 1);
-      const bf16x4 lo = ds_read_tr16(vs + swz<D>(4 * g + qq, ch) + boff);
-      const bf16x4 hi = ds_read_tr16(vs + swz<D>(16 + 4 * g + qq, ch) + boff);
-      const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      o[t] = mfma16(a, pb, o[t]);
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(s[m][r] - m_new);
+          s[m][r] = e;
+          ls += e;
+        }
+      }
+      l_run = l_run * alpha + ls;
+      m_run = m_new;
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pb[j] = (short)f2bf(s[0][j]);
+        pb[j + 4] = (short)f2bf(s[1][j]);
+      }
+      const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int t = 0; t < NTD; ++t) {
+        o[t] *= alpha;
+        const int ch = 2 * t + (pp >> 1);
+        const int boff = 8 * (pp & 1);
+        const bf16x4 lo = ds_read_tr16(vs + swz<D>(4 * g + qq, ch) + boff);
+        const bf16x4 hi = ds_read_tr16(vs + swz<D>(16 + 4 * g + qq, ch) + boff);
+        const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[t] = mfma16(a, pb, o[t]);
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-  }
 
-  // combine the 4 waves of the workgroup through LDS
-  l_run += __shfl_xor(l_run, 16, 64);
-  l_run += __shfl_xor(l_run, 32, 64);
-  __syncthreads();
-  float* ored = reinterpret_cast<float*>(smem);        // [4][16][D]
-  float* mred = ored + 4 * 16 * D;                      // [4][16]
-  float* lred = mred + 4 * 16;                          // [4][16]
+    // combine the 4 waves of the workgroup through LDS
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+    __syncthreads();
+    float* ored = reinterpret_cast<float*>(smem);  // [4][16][D]
+    float* mred = ored + 4 * 16 * D;               // [4][16]
+    float* lred = mred + 4 * 16;                   // [4][16]
 #pragma unroll
-  for (int t = 0; t < NTD; ++t) *reinterpret_cast<f32x4*>(ored + (w * 16 + li) * D + 16 * t + 4 * g) = o[t];
-  if (g == 0) {
-    mred[w * 16 + li] = m_run;
-    lred[w * 16 + li] = l_run;
-  }
-  __syncthreads();
-  const bool direct = p.max_parts == 1;
-  for (int e = tid; e < G * D; e += 256) {
-    const int qh = e / D, d = e % D;
-    float M = -1e30f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, mred[ww * 16 + qh]);
-    float L = 0.f, O = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
-      const float f = exp2f(mred[ww * 16 + qh] - M);
-      L += f * lred[ww * 16 + qh];
-      O += f * ored[(ww * 16 + qh) * D + d];
+    for (int t = 0; t < NTD; ++t) *reinterpret_cast<f32x4*>(ored + (w * 16 + li) * D + 16 * t + 4 * g) = o[t];
+    if (g == 0) {
+      mred[w * 16 + li] = m_run;
+      lred[w * 16 + li] = l_run;
     }
-    const size_t hq = (size_t)b * p.Hq + hk * G + qh;
-    if (direct) {
-      p.out[hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
-    } else {
-      const size_t pi = hq * p.max_parts + part;
-      p.part_o[pi * D + d] = O;
-      if (d == 0) {
-        p.part_m[pi] = M;
-        p.part_l[pi] = L;
+    __syncthreads();
+    const bool direct = p.max_parts == 1;
+    for (int e = tid; e < G * D; e += 256) {
+      const int qh = e / D, d = e % D;
+      float M = -1e30f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, mred[ww * 16 + qh]);
+      float L = 0.f, O = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) {
+        const float f = exp2f(mred[ww * 16 + qh] - M);
+        L += f * lred[ww * 16 + qh];
+        O += f * ored[(ww * 16 + qh) * D + d];
+      }
+      const size_t hq = (size_t)b * p.Hq + hk * G + qh;
+      if (direct) {
+        p.out[hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
+      } else {
+        const size_t pi = hq * p.max_parts + part;
+        p.part_o[pi * D + d] = O;
+        if (d == 0) {
+          p.part_m[pi] = M;
+          p.part_l[pi] = L;
+        }
       }
     }
+    __syncthreads();  // LDS is restaged by the next item
   }
 }
 
@@ -443,7 +446,7 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
                     int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s) {
   if (batch <= 0 || max_seqlen_q <= 0) return 0;
-  if (Hq % Hkv) return hipErrorInvalidValue;
+  if (Hq % Hkv || (paged && block_size % 64)) return hipErrorInvalidValue;
   FlashParams prm;
   prm.q = (const bf16*)q;
   prm.q_stride_tok = q_stride_tok;
@@ -495,7 +498,7 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
                            float* part_m, float* part_l, int batch, int Hq, int Hkv, int D, int part_size,
                            int max_parts, float scale, hipStream_t s) {
   if (batch <= 0) return 0;
-  if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1) return hipErrorInvalidValue;
+  if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1 || block_size % 32) return hipErrorInvalidValue;
   DecodeParams prm;
   prm.q = (const bf16*)q;
   prm.k_cache = (const bf16*)k_cache;
@@ -513,12 +516,13 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_size = part_size;
   prm.max_parts = max_parts;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid(max_parts, Hkv, batch);
+  const int total_items = max_parts * Hkv * batch;
+  dim3 grid(total_items < 2048 ? total_items : 2048);
   if (D == 128) {
-    hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(256), 0, s, prm);
+    hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(256), 0, s, prm, total_items);
     if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, batch), dim3(128), 0, s, prm);
   } else if (D == 64) {
-    hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(256), 0, s, prm);
+    hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(256), 0, s, prm, total_items);
     if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, batch), dim3(64), 0, s, prm);
   } else {
     return hipErrorInvalidValue;

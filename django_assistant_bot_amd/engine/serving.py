@@ -1,0 +1,206 @@
+"""Async serving front of the engines: cross-request batching for HTTP / asyncio callers.
+
+The reference gpu_service handlers are ``async def`` but call torch synchronously, one request at a
+time per gunicorn worker, each worker holding its own full model copy.  Here one
+process owns the GPU; asyncio callers submit into worker threads that batch across requests:
+
+  * ``LLMWorker``    -- owns an ``LLMEngine`` and runs its continuous-batching step loop; every
+                        awaiting caller is a sequence of the same running batch.
+  * ``EmbedWorker``  -- gathers concurrent embedding requests for up to ``max_wait_s`` (or until
+                        ``max_batch_tokens``) and encodes them in one packed batch.
+
+Engines are created lazily per model name and cached for the process (``get_llm_worker`` /
+``get_embed_worker``); ``engine_metrics()`` feeds gpu_service ``/metrics``.
+"""
+from __future__ import annotations
+
+import asyncio
+import logging
+import queue
+import threading
+import time
+from concurrent.futures import Future
+
+logger = logging.getLogger(__name__)
+
+
+class LLMWorker:
+    def __init__(self, engine):
+        self.engine = engine
+        self._inbox: queue.Queue = queue.Queue()
+        self._futures: dict[int, Future] = {}
+        self._wake = threading.Event()
+        self._stop = False
+        self._lock = threading.Lock()
+        self.requests = 0
+        self._thread = threading.Thread(target=self._run, name="dab-llm-worker", daemon=True)
+        self._thread.start()
+
+    def submit(self, prompt_ids, params) -> Future:
+        fut: Future = Future()
+        self._inbox.put((list(prompt_ids), params, fut))
+        self._wake.set()
+        return fut
+
+    async def generate(self, prompt_ids, params):
+        return await asyncio.wrap_future(self.submit(prompt_ids, params))
+
+    def _drain(self):
+        while True:
+            try:
+                ids, params, fut = self._inbox.get_nowait()
+            except queue.Empty:
+                return
+            try:
+                rid = self.engine.add_request(ids, params)
+                self._futures[rid] = fut
+                self.requests += 1
+            except Exception as exc:  # invalid request: fail only this caller
+                fut.set_exception(exc)
+
+    def _run(self):
+        while not self._stop:
+            self._drain()
+            if not self.engine.has_unfinished():
+                self._wake.wait(0.05)
+                self._wake.clear()
+                continue
+            try:
+                finished = self.engine.step()
+            except Exception as exc:  # engine fault: fail every in-flight request, keep serving
+                logger.exception("engine step failed")
+                for fut in self._futures.values():
+                    if not fut.done():
+                        fut.set_exception(exc)
+                self._futures.clear()
+                self._reset_engine()
+                continue
+            for rid in finished:
+                fut = self._futures.pop(rid, None)
+                out = self.engine.pop_output(rid)
+                if fut is not None and not fut.done():
+                    fut.set_result(out)
+
+    def _reset_engine(self):
+        eng = self.engine
+        for q in (eng.waiting, eng.prefilling, eng.running):
+            for r in list(q):
+                eng.blocks.free_sequence(r.seq)
+        eng.waiting.clear()
+        eng.prefilling.clear()
+        eng.running.clear()
+
+    def stop(self):
+        self._stop = True
+        self._wake.set()
+
+
+class EmbedWorker:
+    def __init__(self, engine, max_wait_s: float = 0.002, max_batch_texts: int = 4096):
+        self.engine = engine
+        self.max_wait_s = max_wait_s
+        self.max_batch_texts = max_batch_texts
+        self._inbox: queue.Queue = queue.Queue()
+        self.requests = 0
+        self._thread = threading.Thread(target=self._run, name="dab-embed-worker", daemon=True)
+        self._thread.start()
+
+    def submit(self, texts, normalize=None) -> Future:
+        fut: Future = Future()
+        self._inbox.put((list(texts), normalize, fut))
+        return fut
+
+    async def embeddings(self, texts, normalize=None):
+        return await asyncio.wrap_future(self.submit(texts, normalize))
+
+    def _run(self):
+        while True:
+            first = self._inbox.get()
+            batch = [first]
+            n = len(first[0])
+            deadline = time.perf_counter() + self.max_wait_s
+            while n < self.max_batch_texts:
+                left = deadline - time.perf_counter()
+                if left <= 0:
+                    break
+                try:
+                    item = self._inbox.get(timeout=left)
+                except queue.Empty:
+                    break
+                batch.append(item)
+                n += len(item[0])
+            groups: dict = {}
+            for texts, norm, fut in batch:
+                groups.setdefault(norm, []).append((texts, fut))
+            for norm, items in groups.items():
+                flat = [t for texts, _ in items for t in texts]
+                try:
+                    vecs = self.engine.embed(flat, normalize=norm).float().cpu().tolist() if flat else []
+                except Exception as exc:
+                    for _, fut in items:
+                        fut.set_exception(exc)
+                    continue
+                o = 0
+                for texts, fut in items:
+                    fut.set_result(vecs[o:o + len(texts)])
+                    o += len(texts)
+                self.requests += len(items)
+
+
+_llm: dict = {}
+_emb: dict = {}
+_lock = threading.Lock()
+
+
+def engine_device():
+    import torch
+
+    return "cuda" if torch.cuda.is_available() else "cpu"
+
+
+def get_llm_worker(model: str, **engine_kwargs) -> LLMWorker:
+    key = model.lower()
+    with _lock:
+        w = _llm.get(key)
+        if w is None:
+            from .llm_engine import LLMEngine
+
+            engine_kwargs.setdefault("device", engine_device())
+            engine_kwargs.setdefault("max_batch", 64 if engine_kwargs["device"] == "cuda" else 4)
+            if engine_kwargs["device"] == "cpu":
+                engine_kwargs.setdefault("max_model_len", 2048)
+            w = _llm[key] = LLMWorker(LLMEngine(model, **engine_kwargs))
+        return w
+
+
+def get_embed_worker(model: str, **engine_kwargs) -> EmbedWorker:
+    key = model.lower()
+    with _lock:
+        w = _emb.get(key)
+        if w is None:
+            from .embedding_engine import EmbeddingEngine
+
+            engine_kwargs.setdefault("device", engine_device())
+            w = _emb[key] = EmbedWorker(EmbeddingEngine(model, **engine_kwargs))
+        return w
+
+
+def loaded_models() -> dict:
+    return {"embedders": sorted(_emb), "providers": sorted(_llm)}
+
+
+def engine_metrics() -> dict:
+    import torch
+
+    m = {"embedders": {}, "providers": {}}
+    for k, w in _emb.items():
+        m["embedders"][k] = {"requests": w.requests, **w.engine.stats, "queue_depth": w._inbox.qsize()}
+    for k, w in _llm.items():
+        e = w.engine
+        m["providers"][k] = {"requests": w.requests, **e.stats, "running": len(e.running), "waiting": len(e.waiting),
+                             "kv_free_blocks": e.blocks.num_free_blocks(), "kv_total_blocks": e.blocks.num_blocks(),
+                             "prefix_hit_tokens": e.blocks.prefix_hits()}
+    if torch.cuda.is_available():
+        free, total = torch.cuda.mem_get_info()
+        m["hbm"] = {"free_gb": round(free / 2 ** 30, 2), "total_gb": round(total / 2 ** 30, 2)}
+    return m

@@ -1,0 +1,145 @@
+"""Model semantics on CPU (reference ops): parity with HF transformers BertModel / LlamaForCausalLM
+built from the same weights -- the reference runs exactly those HF classes (ai/embedders/transformers.py,
+ai/providers/transformers.py)."""
+import math
+
+import pytest
+import torch
+
+from django_assistant_bot_amd.models import (AttnMeta, BertEncoder, KVCache, LlamaModel, decoder_config,
+                                             encoder_config, pack_sequences, random_decoder_weights,
+                                             random_encoder_weights, shard_decoder_weights)
+
+transformers = pytest.importorskip("transformers")
+
+
+def test_bert_matches_hf_mean_pool():
+    cfg = encoder_config("tiny-bert")
+    w = {k: v.float() for k, v in random_encoder_weights(cfg, dtype=torch.float32, seed=3).items()}
+    hf_cfg = transformers.BertConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, num_hidden_layers=cfg.layers,
+                                     num_attention_heads=cfg.heads, intermediate_size=cfg.intermediate,
+                                     max_position_embeddings=cfg.max_position, layer_norm_eps=cfg.eps,
+                                     hidden_act="gelu", attn_implementation="eager")
+    hf = transformers.BertModel(hf_cfg, add_pooling_layer=False).eval()
+    H = cfg.hidden
+    sd = {"embeddings.word_embeddings.weight": w["word_emb"], "embeddings.position_embeddings.weight": w["pos_emb"],
+          "embeddings.token_type_embeddings.weight": w["type_emb"], "embeddings.LayerNorm.weight": w["emb_ln_g"],
+          "embeddings.LayerNorm.bias": w["emb_ln_b"]}
+    for i in range(cfg.layers):
+        p = f"encoder.layer.{i}."
+        for j, n in enumerate(("query", "key", "value")):
+            sd[p + f"attention.self.{n}.weight"] = w[f"l{i}.qkv_w"][j * H:(j + 1) * H]
+            sd[p + f"attention.self.{n}.bias"] = w[f"l{i}.qkv_b"][j * H:(j + 1) * H]
+        sd[p + "attention.output.dense.weight"] = w[f"l{i}.o_w"]
+        sd[p + "attention.output.dense.bias"] = w[f"l{i}.o_b"]
+        sd[p + "attention.output.LayerNorm.weight"] = w[f"l{i}.ln1_g"]
+        sd[p + "attention.output.LayerNorm.bias"] = w[f"l{i}.ln1_b"]
+        sd[p + "intermediate.dense.weight"] = w[f"l{i}.i_w"]
+        sd[p + "intermediate.dense.bias"] = w[f"l{i}.i_b"]
+        sd[p + "output.dense.weight"] = w[f"l{i}.d_w"]
+        sd[p + "output.dense.bias"] = w[f"l{i}.d_b"]
+        sd[p + "output.LayerNorm.weight"] = w[f"l{i}.ln2_g"]
+        sd[p + "output.LayerNorm.bias"] = w[f"l{i}.ln2_b"]
+    missing, unexpected = hf.load_state_dict(sd, strict=False)
+    assert not unexpected and all("position_ids" in m or "token_type" in m for m in missing)
+    enc = BertEncoder(cfg, w, "cpu")
+    seqs = [[101, 5, 6, 7, 102], [101, 900, 102], [101] + list(range(10, 40)) + [102]]
+    ids, pos, cu, mx = pack_sequences(seqs, "cpu")
+    ours = enc.encode(ids, pos, cu, mx)
+    for i, s in enumerate(seqs):
+        with torch.no_grad():
+            ref = hf(input_ids=torch.tensor([s])).last_hidden_state.mean(dim=1)[0]  # the reference's pooling
+        assert torch.allclose(ours[i], ref, atol=2e-4), (ours[i] - ref).abs().max()
+
+
+def _llama_pair(seed=1):
+    cfg = decoder_config("tiny-llama")
+    full = {k: v.float() for k, v in random_decoder_weights(cfg, dtype=torch.float32, seed=seed).items()}
+    return cfg, full
+
+
+def _hf_llama(cfg, full):
+    hc = transformers.LlamaConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, num_hidden_layers=cfg.layers,
+                                  num_attention_heads=cfg.heads, num_key_value_heads=cfg.kv_heads,
+                                  intermediate_size=cfg.intermediate, rms_norm_eps=cfg.eps, rope_theta=cfg.rope_theta,
+                                  max_position_embeddings=cfg.max_position, tie_word_embeddings=False,
+                                  attn_implementation="eager")
+    hf = transformers.LlamaForCausalLM(hc).eval()
+    D, F = cfg.head_dim, cfg.intermediate
+    sd = {"model.embed_tokens.weight": full["embed"], "model.norm.weight": full["final_norm"],
+          "lm_head.weight": full["lm_head"]}
+    qn, kn = cfg.heads * D, cfg.kv_heads * D
+    for i in range(cfg.layers):
+        p = f"model.layers.{i}."
+        qkv = full[f"l{i}.qkv_w"]
+        sd[p + "self_attn.q_proj.weight"] = qkv[:qn]
+        sd[p + "self_attn.k_proj.weight"] = qkv[qn:qn + kn]
+        sd[p + "self_attn.v_proj.weight"] = qkv[qn + kn:]
+        sd[p + "self_attn.o_proj.weight"] = full[f"l{i}.o_w"]
+        sd[p + "mlp.gate_proj.weight"] = full[f"l{i}.gate_up_w"][:F]
+        sd[p + "mlp.up_proj.weight"] = full[f"l{i}.gate_up_w"][F:]
+        sd[p + "mlp.down_proj.weight"] = full[f"l{i}.down_w"]
+        sd[p + "input_layernorm.weight"] = full[f"l{i}.attn_norm"]
+        sd[p + "post_attention_layernorm.weight"] = full[f"l{i}.mlp_norm"]
+    hf.load_state_dict(sd, strict=True)
+    return hf
+
+
+def _prefill(model, cfg, ids, bs=64, nb=8):
+    kv = KVCache(cfg.layers, nb, cfg.kv_heads // model.tp_size, bs, cfg.head_dim, "cpu", dtype=torch.float32)
+    T = len(ids)
+    bt = torch.arange(nb, dtype=torch.int32)[None]
+    meta = AttnMeta(decode=False, positions=torch.arange(T, dtype=torch.int32), slots=torch.arange(T),
+                    block_tables=bt, ctx_lens=torch.tensor([T], dtype=torch.int32),
+                    cu_q=torch.tensor([0, T], dtype=torch.int32), max_q=T)
+    return model.forward(torch.tensor(ids, dtype=torch.int32), meta, kv), kv
+
+
+def test_llama_prefill_matches_hf():
+    cfg, full = _llama_pair()
+    hf = _hf_llama(cfg, full)
+    model = LlamaModel(cfg, full, "cpu")
+    ids = [5, 17, 300, 42, 999, 7, 1, 64, 65, 66]
+    h, _ = _prefill(model, cfg, ids)
+    ours = model.logits(h)
+    with torch.no_grad():
+        ref = hf(torch.tensor([ids])).logits[0]
+    assert torch.allclose(ours, ref, atol=1e-3, rtol=1e-3), (ours - ref).abs().max()
+
+
+def test_llama_decode_consistent_with_prefill():
+    cfg, full = _llama_pair(2)
+    model = LlamaModel(cfg, full, "cpu")
+    ids = list(range(3, 3 + 70))  # crosses a 64-token block
+    h_full, _ = _prefill(model, cfg, ids)
+    h_pre, kv = _prefill(model, cfg, ids[:-1])
+    T = len(ids)
+    meta = AttnMeta(decode=True, positions=torch.tensor([T - 1], dtype=torch.int32), slots=torch.tensor([T - 1]),
+                    block_tables=torch.arange(8, dtype=torch.int32)[None], ctx_lens=torch.tensor([T], dtype=torch.int32))
+    h_dec = model.forward(torch.tensor([ids[-1]], dtype=torch.int32), meta, kv)
+    assert torch.allclose(h_dec[0], h_full[-1], atol=1e-4)
+
+
+def test_tensor_parallel_shards_reconstruct_full_model():
+    """Sum of per-shard row-parallel outputs == unsharded projection (Megatron split used by TP)."""
+    cfg, full = _llama_pair(4)
+    tp = 2
+    shards = [shard_decoder_weights(full, cfg, r, tp) for r in range(tp)]
+    x = torch.randn(3, cfg.hidden)
+    D, F = cfg.head_dim, cfg.intermediate
+    # attention output projection: concatenated head outputs x_heads @ o_w^T == sum over shards
+    heads = torch.randn(3, cfg.heads * D)
+    ref = heads @ full["l0.o_w"].t()
+    hq = cfg.heads // tp
+    got = sum(heads[:, r * hq * D:(r + 1) * hq * D] @ shards[r]["l0.o_w"].t() for r in range(tp))
+    assert torch.allclose(got, ref, atol=1e-5)
+    # MLP: silu(gate) * up, down-projected, summed over shards
+    gu = x @ full["l0.gate_up_w"].t()
+    ref = (torch.nn.functional.silu(gu[:, :F]) * gu[:, F:]) @ full["l0.down_w"].t()
+    got = 0
+    for r in range(tp):
+        g = x @ shards[r]["l0.gate_up_w"].t()
+        f = F // tp
+        got = got + (torch.nn.functional.silu(g[:, :f]) * g[:, f:]) @ shards[r]["l0.down_w"].t()
+    assert torch.allclose(got, ref, atol=1e-4)
+    assert math.isclose(sum(s["l0.qkv_w"].numel() for s in shards), full["l0.qkv_w"].numel())
