@@ -170,6 +170,7 @@ def main():
             pdist.barrier(info)
             if dev.type == "cuda":
                 torch.cuda.synchronize(dev)
+            stats0 = dict(llm.stats)
             t0 = time.perf_counter()
         res = rag.answer(all_q[R][step], params, bot_group=0)
         if step >= args.warmup:
@@ -183,6 +184,8 @@ def main():
     p50 = float(np.median(latencies)) if latencies else float("nan")
     p50 = pdist.max_over_ranks(p50, dev)
     total_q = W * B * args.steps
+    eng = {k: round(v - stats0.get(k, 0), 3) if isinstance(v, float) else v - stats0.get(k, 0)
+           for k, v in llm.stats.items()}
     qps = total_q / elapsed
     out = {
         "metric": METRIC,
@@ -210,6 +213,7 @@ def main():
             "graphs": not args.no_graphs,
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
+            "engine_rank0": eng,
         },
     }
     if R == 0:

@@ -152,6 +152,12 @@ PYBIND11_MODULE(_native, m) {
            [](const dab::KVBlockManager& k, int64_t seq, int start, int n, u out) {
              k.slot_mapping(seq, start, n, (int64_t*)out);
            })
+      .def("prepare_decode_into",
+           [](dab::KVBlockManager& k, const std::vector<int64_t>& seqs, const std::vector<int32_t>& toks,
+              int max_blocks, u ids, u pos, u slots, u ctx, u bt) {
+             return k.prepare_decode(seqs, toks, max_blocks, (int32_t*)ids, (int32_t*)pos, (int64_t*)slots,
+                                     (int32_t*)ctx, (int32_t*)bt);
+           })
       .def("block_table_into", [](const dab::KVBlockManager& k, const std::vector<int64_t>& seqs, int max_blocks,
                                   u out) { k.block_table(seqs, max_blocks, (int32_t*)out); });
 

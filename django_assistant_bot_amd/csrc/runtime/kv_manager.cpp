@@ -170,6 +170,28 @@ void KVBlockManager::slot_mapping(int64_t seq_id, int start, int n, int64_t* out
   }
 }
 
+int KVBlockManager::prepare_decode(const std::vector<int64_t>& seq_ids, const std::vector<int32_t>& tokens,
+                                   int max_blocks, int32_t* ids, int32_t* pos, int64_t* slots, int32_t* ctx,
+                                   int32_t* block_table) {
+  if (seq_ids.size() != tokens.size()) throw std::invalid_argument("seq_ids / tokens length mismatch");
+  for (size_t i = 0; i < seq_ids.size(); ++i)
+    if (!extend(seq_ids[i], 1)) return (int)i;
+  for (size_t i = 0; i < seq_ids.size(); ++i) {
+    Seq& s = seqs_.at(seq_ids[i]);
+    s.tokens.push_back(tokens[i]);
+    const int p = (int)s.tokens.size() - 1;
+    ids[i] = tokens[i];
+    pos[i] = p;
+    slots[i] = (int64_t)s.blocks[p / block_size_] * block_size_ + (p % block_size_);
+    ctx[i] = p + 1;
+    if ((int)s.blocks.size() > max_blocks) throw std::out_of_range("block table wider than max_blocks");
+    int32_t* row = block_table + i * (size_t)max_blocks;
+    std::copy(s.blocks.begin(), s.blocks.end(), row);
+    std::fill(row + s.blocks.size(), row + max_blocks, 0);
+  }
+  return -1;
+}
+
 void KVBlockManager::block_table(const std::vector<int64_t>& seq_ids, int max_blocks, int32_t* out) const {
   for (size_t r = 0; r < seq_ids.size(); ++r) {
     int32_t* row = out + r * max_blocks;

@@ -40,6 +40,11 @@ class KVBlockManager {
   int64_t prefix_hits() const { return prefix_hits_; }
   const std::vector<int32_t>& blocks(int64_t seq_id) const;
 
+  // One decode step for a batch: reserves one slot per sequence (returns the index of the first
+  // sequence that cannot get a block, nothing appended then), else appends each sequence's last
+  // token and fills ids / positions / slots / context lengths / block-table rows; returns -1.
+  int prepare_decode(const std::vector<int64_t>& seq_ids, const std::vector<int32_t>& tokens, int max_blocks,
+                     int32_t* ids, int32_t* pos, int64_t* slots, int32_t* ctx, int32_t* block_table);
   // slot ids (block * block_size + offset) of token positions [start, start + n)
   void slot_mapping(int64_t seq_id, int start, int n, int64_t* out) const;
   // block tables of several sequences into a [len(seq_ids), max_blocks] int32 matrix (-1 padding... 0)

@@ -343,7 +343,7 @@ class LLMEngine:
             self.blocks.free_sequence(r.seq)
             self.finished[r.rid] = r
 
-    def _preempt_one(self, protect: _Req) -> bool:
+    def _preempt_one(self, protect: _Req | None) -> bool:
         for victim in reversed(self.running):
             if victim is protect:
                 continue
@@ -358,32 +358,26 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ decode
     def _run_decode(self):
-        # reserve one slot per running sequence, preempting the youngest when the pool is dry
-        batch = []
-        for r in list(self.running):
-            if r not in self.running:
-                continue
-            while not self.blocks.extend(r.seq, 1):
-                if not self._preempt_one(protect=r):
-                    raise RuntimeError("KV cache exhausted")
-            batch.append(r)
-        batch = [r for r in batch if r in self.running]
-        B = len(batch)
-        if B == 0:
-            return
-        for i, r in enumerate(batch):
-            last = r.out[-1]
-            self.blocks.append_tokens(r.seq, [last])
-            p = self.blocks.num_tokens(r.seq) - 1
-            self._h_ids[i] = last
-            self._h_pos[i] = p
-            self.blocks.slot_mapping_into(r.seq, p, 1, self._h_slots.data_ptr() + 8 * i)
-            self._h_ctx[i] = p + 1
-            self._h_temp[i] = r.params.temperature if r.params.do_sample else 0.0
-            self._h_topk[i] = r.params.top_k
-            self._h_topp[i] = r.params.top_p
-            self._h_cnt[i] = r.rng_base + len(r.out)
-        self._build_block_tables([r.seq for r in batch], self._h_bt[:B])
+        t0 = time.perf_counter()
+        # one native call reserves a slot per sequence and fills ids/positions/slots/ctx/block tables;
+        # when the pool is dry the youngest running sequence is preempted (recompute) and we retry
+        while True:
+            batch = list(self.running)
+            B = len(batch)
+            if B == 0:
+                return
+            fail = self.blocks.prepare_decode_into(
+                [r.seq for r in batch], [r.out[-1] for r in batch], self.max_blocks_per_seq,
+                self._h_ids.data_ptr(), self._h_pos.data_ptr(), self._h_slots.data_ptr(), self._h_ctx.data_ptr(),
+                self._h_bt.data_ptr())
+            if fail < 0:
+                break
+            if not self._preempt_one(protect=None if B == 1 else batch[fail]):
+                raise RuntimeError("KV cache exhausted")
+        self._h_temp[:B] = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in batch])
+        self._h_topk[:B] = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32)
+        self._h_topp[:B] = torch.tensor([r.params.top_p for r in batch])
+        self._h_cnt[:B] = torch.tensor([r.rng_base + len(r.out) for r in batch], dtype=torch.int64)
         Bp = next(b for b in self._buckets if b >= B) if self.use_graphs else B
         if Bp > B:  # padding rows: no cache write, attend to one key of block 0, output ignored
             self._h_ids[B:Bp] = 0
@@ -400,6 +394,7 @@ class LLMEngine:
                      (self._d_topp, self._h_topp), (self._d_cnt, self._h_cnt)):
             d[:Bp].copy_(h[:Bp], non_blocking=True)
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
+        t1 = time.perf_counter()
         if self.use_graphs:
             g = self._graphs.get(Bp)
             if g is None:
@@ -415,12 +410,16 @@ class LLMEngine:
             self._tp_sync_tokens(self._d_tokens[:Bp])
             self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
+        t2 = time.perf_counter()
         toks = self._h_tokens[:B].tolist()
         now = time.perf_counter()
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += B
         for r, t in zip(batch, toks):
             self._accept_token(r, int(t), now)
+        t3 = time.perf_counter()
+        self.stats["decode_host_s"] = self.stats.get("decode_host_s", 0.0) + (t1 - t0) + (t3 - t2)
+        self.stats["decode_gpu_wait_s"] = self.stats.get("decode_gpu_wait_s", 0.0) + (t2 - t1)
 
     def _decode_body(self, Bp: int):
         meta = AttnMeta(decode=True, positions=self._d_pos[:Bp], slots=self._d_slots[:Bp],
