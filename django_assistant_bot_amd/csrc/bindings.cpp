@@ -97,6 +97,20 @@ PYBIND11_MODULE(_native, m) {
           "topk_rows");
   });
 
+  m.def("sample_tokens_2stage", [](u logits, int f32, long ld, int rows, int vocab, u temp, u top_k, u top_p,
+                                   unsigned long long seed, u counters, u out_tokens, u ws, size_t ws_bytes, u s) {
+    check(dab::sample_tokens_2stage(CVP(logits), f32, ld, rows, vocab, (const float*)temp, (const int*)top_k,
+                                    (const float*)top_p, seed, (int64_t*)counters, (int*)out_tokens, VP(ws), ws_bytes,
+                                    ST(s)),
+          "sample_tokens_2stage");
+  });
+  m.def("topk_rows_2stage", [](u scores, long ld, int rows, int n, int k, u out_vals, u out_idx, long long base,
+                               u out_idx64, u ws, size_t ws_bytes, u s) {
+    check(dab::topk_rows_2stage((const float*)scores, ld, rows, n, k, (float*)out_vals, (int*)out_idx, base,
+                                (int64_t*)out_idx64, VP(ws), ws_bytes, ST(s)),
+          "topk_rows_2stage");
+  });
+
   // ---------------- tokenizer ----------------
   py::class_<dab::TokenizerConfig>(m, "TokenizerConfig")
       .def(py::init<>())

@@ -50,4 +50,11 @@ int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int voc
 int topk_rows(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx, int64_t index_base,
               int64_t* out_idx64, hipStream_t s);
 
+// two-stage variants (chunked across workgroups); workspace = rows * candidates * 8 bytes
+int sample_tokens_2stage(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
+                         const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters,
+                         int* out_tokens, void* workspace, size_t workspace_bytes, hipStream_t s);
+int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx,
+                     int64_t index_base, int64_t* out_idx64, void* workspace, size_t workspace_bytes, hipStream_t s);
+
 }  // namespace dab

@@ -246,6 +246,256 @@ __global__ __launch_bounds__(SEL_NT) void topk_rows_kernel(const float* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Two-stage selection for long rows (vocabulary logits, index score rows): stage 1 spreads a row
+// over many workgroups -- each holds a chunk of 256*PT keys in REGISTERS, radix-selects the chunk's
+// top-k with register-resident passes (no global re-reads) and emits exactly k candidates; stage 2
+// merges rows x chunks x kc candidates.  One workgroup per row (the single-stage kernels above)
+// keeps only `rows` CUs busy and re-reads the row 5 times.
+
+constexpr int CH_NT = 256;
+
+template <int PT>
+__global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restrict__ src, int src_bf16, long ld, int n,
+                                                           int k, int kc, uint32_t* __restrict__ cand_key,
+                                                           int* __restrict__ cand_idx) {
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t bc[2];
+  __shared__ uint32_t cnt[2];
+  const int row = blockIdx.y, c = blockIdx.x, nchunks = gridDim.x;
+  const int chunk = CH_NT * PT;
+  const int start = c * chunk;
+  const int len = min(chunk, n - start);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float* sf = reinterpret_cast<const float*>(src) + (size_t)row * ld + start;
+  const bf16* sb = reinterpret_cast<const bf16*>(src) + (size_t)row * ld + start;
+  uint32_t key[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = j * CH_NT + tid;
+    key[j] = i < len ? float_key(src_bf16 ? bf2f(sb[i]) : sf[i]) : 0u;
+  }
+  const int kk = min(k, len);
+  uint32_t prefix = 0, pmask = 0, need = (uint32_t)kk;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += CH_NT) hist[i] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = j * CH_NT + tid;
+      const int bin = (i < len && (key[j] & pmask) == prefix) ? (int)((key[j] >> shift) & 255u) : -1;
+      unsigned long long active = __ballot(bin >= 0);
+      while (active) {
+        const int leader = __ffsll((long long)active) - 1;
+        const int lb = __shfl(bin, leader, 64);
+        const unsigned long long eq = __ballot(bin == lb);
+        if (lane == leader) atomicAdd(&hist[lb], (uint32_t)__popcll(eq));
+        active &= ~eq;
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {
+      uint32_t cc[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cc[j] = hist[255 - 4 * tid - j];
+        sum += cc[j];
+      }
+      uint32_t incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += t;
+      }
+      const uint32_t excl = incl - sum;
+      if (excl < need && need <= incl) {
+        uint32_t acc = excl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (acc + cc[j] >= need) {
+            bc[0] = 255u - 4u * tid - j;
+            bc[1] = need - acc;
+            break;
+          }
+          acc += cc[j];
+        }
+      }
+    }
+    __syncthreads();
+    prefix |= bc[0] << shift;
+    pmask |= 255u << shift;
+    need = bc[1];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    cnt[0] = 0;
+    cnt[1] = 0;
+  }
+  __syncthreads();
+  const uint32_t n_gt = (uint32_t)kk - need;
+  uint32_t* ok = cand_key + ((size_t)row * nchunks + c) * kc;
+  int* oi = cand_idx + ((size_t)row * nchunks + c) * kc;
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int i = j * CH_NT + tid;
+    const bool valid = i < len;
+    const int pg = wave_append(&cnt[0], valid && key[j] > prefix);
+    if (pg >= 0) {
+      ok[pg] = key[j];
+      oi[pg] = start + i;
+    }
+    const int pe = wave_append(&cnt[1], valid && key[j] == prefix);
+    if (pe >= 0 && (uint32_t)pe < need) {
+      ok[n_gt + pe] = key[j];
+      oi[n_gt + pe] = start + i;
+    }
+  }
+  for (int i = kk + tid; i < kc; i += CH_NT) {
+    ok[i] = 0u;
+    oi[i] = -1;
+  }
+}
+
+// Stage 2 of sampling: <= 1024 candidates per row -> sorted top-k -> HF top-p -> multinomial.
+__global__ __launch_bounds__(SEL_NT) void sample_merge_kernel(const uint32_t* __restrict__ cand_key,
+                                                              const int* __restrict__ cand_idx, int ncand,
+                                                              const float* __restrict__ temperature,
+                                                              const int* __restrict__ top_k,
+                                                              const float* __restrict__ top_p, int vocab,
+                                                              unsigned long long seed, int64_t* __restrict__ counters,
+                                                              int* __restrict__ out_tokens) {
+  __shared__ uint32_t skey[SEL_MAXK];
+  __shared__ int sidx[SEL_MAXK];
+  __shared__ float probs[64];
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const float T = temperature ? temperature[row] : 1.f;
+  int k = (T <= 0.f) ? 1 : (top_k && top_k[row] > 0 ? top_k[row] : 64);
+  k = min(k, min(64, vocab));
+  for (int i = tid; i < SEL_MAXK; i += SEL_NT) {
+    skey[i] = i < ncand ? cand_key[(size_t)row * ncand + i] : 0u;
+    sidx[i] = i < ncand ? cand_idx[(size_t)row * ncand + i] : 0x7fffffff;
+  }
+  __syncthreads();
+  for (int size = 2; size <= SEL_MAXK; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = tid; t < SEL_MAXK; t += SEL_NT) {
+        const int u2 = t ^ stride;
+        if (u2 > t) {
+          const bool desc = (t & size) == 0;
+          const uint32_t ka = skey[t], kb = skey[u2];
+          const int ia = sidx[t], ib = sidx[u2];
+          const bool a_first = ka > kb || (ka == kb && ia < ib);
+          if (a_first != desc) {
+            skey[t] = kb;
+            skey[u2] = ka;
+            sidx[t] = ib;
+            sidx[u2] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (tid != 0) return;
+  if (T <= 0.f) {
+    out_tokens[row] = sidx[0];
+    return;
+  }
+  const float P = top_p ? top_p[row] : 1.f;
+  const float x0 = key_float(skey[0]) / T;
+  float total = 0.f;
+  for (int i = 0; i < k; ++i) {
+    const float e = __expf(key_float(skey[i]) / T - x0);
+    probs[i] = e;
+    total += e;
+  }
+  int keep = k;
+  if (P < 1.f) {
+    const float thr = (1.f - P) * total;
+    float cum = 0.f;
+    for (int i = k - 1; i >= 1; --i) {
+      cum += probs[i];
+      if (cum <= thr) keep = i;
+      else break;
+    }
+  }
+  float kept = 0.f;
+  for (int i = 0; i < keep; ++i) kept += probs[i];
+  const long long cval = counters ? counters[row] : 0;
+  if (counters) counters[row] = cval + 1;
+  const unsigned long long r =
+      splitmix64(seed ^ splitmix64((unsigned long long)cval * 0x9E3779B97F4A7C15ull + (unsigned long long)row));
+  const float uu = (float)(r >> 40) * (1.f / 16777216.f);
+  const float target = uu * kept;
+  float acc = 0.f;
+  int pick = keep - 1;
+  for (int i = 0; i < keep; ++i) {
+    acc += probs[i];
+    if (acc > target) {
+      pick = i;
+      break;
+    }
+  }
+  out_tokens[row] = sidx[pick];
+}
+
+// Stage 2 of index top-k: radix select over the candidate keys (L2-resident) + sort + emit.
+__global__ __launch_bounds__(SEL_NT) void topk_merge_kernel(const uint32_t* __restrict__ cand_key,
+                                                            const int* __restrict__ cand_idx, int ncand, int k,
+                                                            float* __restrict__ out_vals, int* __restrict__ out_idx,
+                                                            int64_t index_base, int64_t* __restrict__ out_idx64) {
+  __shared__ SelShared sh;
+  const int row = blockIdx.x;
+  const uint32_t* ck = cand_key + (size_t)row * ncand;
+  const int* ci = cand_idx + (size_t)row * ncand;
+  auto key_at = [&](int i) -> uint32_t { return ck[i]; };
+  select_topk(key_at, ncand, k, sh);
+  for (int i = threadIdx.x; i < k; i += SEL_NT) {
+    const int pos = sh.cand_idx[i];
+    const int idx = (pos >= 0 && pos < ncand) ? ci[pos] : -1;
+    out_vals[(size_t)row * k + i] = key_float(sh.cand_key[i]);
+    if (out_idx) out_idx[(size_t)row * k + i] = idx;
+    if (out_idx64) out_idx64[(size_t)row * k + i] = idx >= 0 ? index_base + idx : -1;
+  }
+}
+
+int sample_tokens_2stage(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
+                         const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters,
+                         int* out_tokens, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (rows <= 0) return 0;
+  constexpr int PT = 32, KC = 64;
+  const int chunk = CH_NT * PT;
+  const int nchunks = (vocab + chunk - 1) / chunk;
+  const int ncand = nchunks * KC;
+  const size_t need = (size_t)rows * ncand * 8;
+  if (ncand > SEL_MAXK || workspace_bytes < need) return hipErrorInvalidValue;
+  uint32_t* ck = reinterpret_cast<uint32_t*>(workspace);
+  int* ci = reinterpret_cast<int*>(ck + (size_t)rows * ncand);
+  hipLaunchKernelGGL(chunk_topk_kernel<PT>, dim3(nchunks, rows), dim3(CH_NT), 0, s, logits, logits_f32 ? 0 : 1, ld,
+                     vocab, KC, KC, ck, ci);
+  hipLaunchKernelGGL(sample_merge_kernel, dim3(rows), dim3(SEL_NT), 0, s, ck, ci, ncand, temperature, top_k, top_p,
+                     vocab, seed, counters, out_tokens);
+  return hipGetLastError();
+}
+
+int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx,
+                     int64_t index_base, int64_t* out_idx64, void* workspace, size_t workspace_bytes, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (k < 1 || k > SEL_MAXK || k > n) return hipErrorInvalidValue;
+  constexpr int PT = 32;
+  const int chunk = CH_NT * PT;
+  const int kc = ((k + 63) / 64) * 64;
+  const int nchunks = (n + chunk - 1) / chunk;
+  const int ncand = nchunks * kc;
+  if (workspace_bytes < (size_t)rows * ncand * 8) return hipErrorInvalidValue;
+  uint32_t* ck = reinterpret_cast<uint32_t*>(workspace);
+  int* ci = reinterpret_cast<int*>(ck + (size_t)rows * ncand);
+  hipLaunchKernelGGL(chunk_topk_kernel<PT>, dim3(nchunks, rows), dim3(CH_NT), 0, s, scores, 0, ld, n, k, kc, ck, ci);
+  hipLaunchKernelGGL(topk_merge_kernel, dim3(rows), dim3(SEL_NT), 0, s, ck, ci, ncand, k, out_vals, out_idx,
+                     index_base, out_idx64);
+  return hipGetLastError();
+}
+
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
                   const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
                   float* out_logprobs, hipStream_t s) {

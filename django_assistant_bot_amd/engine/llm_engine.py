@@ -169,7 +169,8 @@ class LLMEngine:
         max_parts = math.ceil(self.max_model_len / part_size)
         self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
             else None
-        self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._sample_ws = ops.kernels.sample_workspace(mb, cfg.vocab_size, dev) if self.is_gpu else None
+        self._graphs: dict = {}
         self._buckets = _bucket_sizes(max_batch)
         self._graph_pool = None
 
@@ -310,7 +311,9 @@ class LLMEngine:
         cnt = torch.tensor([r.rng_base + len(r.out) for r in reqs], dtype=torch.int64)
         if self.is_gpu:
             d = self.device
-            toks = ops.sample_tokens(logits, temps.to(d), topk.to(d), topp.to(d), self.seed, cnt.to(d))
+            fast = all((0 < r.params.top_k <= ops.kernels.SAMPLE_FAST_MAX_K) or not r.params.do_sample
+                       or r.params.temperature <= 0 for r in reqs)
+            toks = ops.sample_tokens(logits, temps.to(d), topk.to(d), topp.to(d), self.seed, cnt.to(d), fast=fast)
             toks = self._tp_sync_tokens(toks)
             return toks.cpu().tolist()
         g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
@@ -378,6 +381,8 @@ class LLMEngine:
         self._h_topk[:B] = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32)
         self._h_topp[:B] = torch.tensor([r.params.top_p for r in batch])
         self._h_cnt[:B] = torch.tensor([r.rng_base + len(r.out) for r in batch], dtype=torch.int64)
+        self._fast = all((0 < r.params.top_k <= ops.kernels.SAMPLE_FAST_MAX_K) or not r.params.do_sample
+                         or r.params.temperature <= 0 for r in batch)
         Bp = next(b for b in self._buckets if b >= B) if self.use_graphs else B
         if Bp > B:  # padding rows: no cache write, attend to one key of block 0, output ignored
             self._h_ids[B:Bp] = 0
@@ -396,7 +401,7 @@ class LLMEngine:
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
         t1 = time.perf_counter()
         if self.use_graphs:
-            g = self._graphs.get(Bp)
+            g = self._graphs.get((Bp, self._fast))
             if g is None:
                 g = self._capture(Bp)
             if g is not None:
@@ -429,7 +434,8 @@ class LLMEngine:
         logits = self.model.logits(h)
         if self.is_gpu:
             ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp], self.seed,
-                              self._d_cnt[:Bp], out=self._d_tokens[:Bp])
+                              self._d_cnt[:Bp], out=self._d_tokens[:Bp], fast=self._fast,
+                              workspace=self._sample_ws)
         else:
             g = torch.Generator().manual_seed(int(self.seed * 7919 + int(self._h_cnt[0])))
             self._d_tokens[:Bp] = ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp],
@@ -451,7 +457,7 @@ class LLMEngine:
             with torch.cuda.graph(g, pool=self._graph_pool, stream=s):
                 self._decode_body(Bp)
             torch.cuda.synchronize(self.device)
-            self._graphs[Bp] = g
+            self._graphs[(Bp, self._fast)] = g
             return g
         except Exception as exc:  # pragma: no cover - depends on the runtime
             import logging
@@ -461,6 +467,7 @@ class LLMEngine:
             return None
 
     def capture_all(self, sizes=None):
+        self._fast = True
         for b in sizes or self._buckets:
-            if b not in self._graphs:
+            if (b, True) not in self._graphs:
                 self._capture(b)

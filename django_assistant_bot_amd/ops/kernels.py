@@ -308,8 +308,21 @@ def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor
 # selection
 
 
-def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, generator=None, out=None):
-    """temperature / top_k (int32) / top_p per row; counters int64 per row (advanced in-kernel)."""
+SAMPLE_FAST_MAX_K = 64
+_CHUNK = 256 * 32
+
+
+def sample_workspace(rows: int, vocab: int, device) -> torch.Tensor:
+    ncand = -(-vocab // _CHUNK) * SAMPLE_FAST_MAX_K
+    return torch.empty((rows * ncand * 8,), dtype=torch.uint8, device=device)
+
+
+def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, generator=None, out=None,
+                  fast: bool | None = None, workspace: torch.Tensor | None = None):
+    """temperature / top_k (int32) / top_p per row; counters int64 per row (advanced in-kernel).
+
+    ``fast`` (every row has 0 < top_k <= 64, the reference's 50 included) selects the two-stage kernel:
+    per-chunk register-resident top-64 over many workgroups, then a per-row merge + top-p + sample."""
     if not logits.is_cuda:
         return ref.sample_hf(logits, temperature, top_k, top_p, generator)
     rows, vocab = logits.shape
@@ -320,15 +333,25 @@ def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, genera
     _i32(top_k)
     expect(counters.dtype == torch.int64 and counters.numel() >= rows, "counters")
     out = torch.empty((rows,), dtype=torch.int32, device=logits.device) if out is None else out
-    native().sample_tokens(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab,
-                           ptr(temperature), ptr(top_k), ptr(top_p), int(seed) & ((1 << 64) - 1), ptr(counters),
-                           ptr(out), 0, stream(logits))
+    if fast is None:
+        fast = False
+    ncand = -(-vocab // _CHUNK) * SAMPLE_FAST_MAX_K
+    if fast and ncand <= 1024:
+        ws = workspace if workspace is not None else sample_workspace(rows, vocab, logits.device)
+        expect(ws.numel() >= rows * ncand * 8, "sampling workspace too small")
+        native().sample_tokens_2stage(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab,
+                                      ptr(temperature), ptr(top_k), ptr(top_p), int(seed) & ((1 << 64) - 1),
+                                      ptr(counters), ptr(out), ptr(ws), ws.numel(), stream(logits))
+    else:
+        native().sample_tokens(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab,
+                               ptr(temperature), ptr(top_k), ptr(top_p), int(seed) & ((1 << 64) - 1), ptr(counters),
+                               ptr(out), 0, stream(logits))
     return out
 
 
 def topk_rows(scores, k, index_base=0, want_global=False):
     """Exact per-row top-k of fp32 scores, sorted descending.  Returns (values, idx int32) or, with
-    ``want_global``, (values, idx + index_base as int64)."""
+    ``want_global``, (values, idx + index_base as int64).  Long rows use the two-stage kernel."""
     rows, n = scores.shape
     expect(1 <= k <= min(n, 1024), "1 <= k <= min(n, 1024)")
     if not scores.is_cuda:
@@ -338,11 +361,19 @@ def topk_rows(scores, k, index_base=0, want_global=False):
     vals = torch.empty((rows, k), dtype=torch.float32, device=scores.device)
     if want_global:
         idx = torch.empty((rows, k), dtype=torch.int64, device=scores.device)
-        native().topk_rows(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), 0, int(index_base), ptr(idx),
-                           stream(scores))
+        i32, i64 = 0, ptr(idx)
     else:
         idx = torch.empty((rows, k), dtype=torch.int32, device=scores.device)
-        native().topk_rows(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), ptr(idx), 0, 0, stream(scores))
+        i32, i64 = ptr(idx), 0
+    if n >= 4 * _CHUNK:
+        kc = -(-k // 64) * 64
+        ncand = -(-n // _CHUNK) * kc
+        ws = torch.empty((rows * ncand * 8,), dtype=torch.uint8, device=scores.device)
+        native().topk_rows_2stage(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), i32, int(index_base), i64,
+                                  ptr(ws), ws.numel(), stream(scores))
+    else:
+        native().topk_rows(ptr(scores), scores.stride(0), rows, n, k, ptr(vals), i32, int(index_base), i64,
+                           stream(scores))
     return vals, idx
 
 

@@ -183,8 +183,9 @@ def test_gemm_scores_masks():
     close(got[fin], exp[fin], atol=1e-2, rtol=1e-2)
 
 
-def test_topk_rows():
-    s = torch.randn(7, 100003, device=DEV)
+@pytest.mark.parametrize("n", [5000, 100003])
+def test_topk_rows(n):
+    s = torch.randn(7, n, device=DEV)
     s[2, 50:] = float("-inf")
     for k in (1, 5, 250, 1024):
         v, i = ops.topk_rows(s, k)
@@ -195,23 +196,25 @@ def test_topk_rows():
     assert i.dtype == torch.int64 and int(i.min()) >= 1000
 
 
-def test_sampling_greedy_and_support():
+@pytest.mark.parametrize("fast", [False, True])
+def test_sampling_greedy_and_support(fast):
     V, R = 128256, 64
     logits = torch.randn(R, V, device=DEV).to(torch.bfloat16)
     temp = torch.zeros(R, device=DEV)
     topk = torch.full((R,), 50, dtype=torch.int32, device=DEV)
     topp = torch.full((R,), 0.95, device=DEV)
     cnt = torch.zeros(R, dtype=torch.int64, device=DEV)
-    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt, fast=fast)
     assert torch.equal(tok.long(), logits.float().argmax(-1))
     temp.fill_(1.0)
-    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt)
+    tok = ops.sample_tokens(logits, temp, topk, topp, 123, cnt, fast=fast)
     top50 = torch.topk(logits.float(), 50, dim=-1).indices
     assert bool((top50 == tok.long()[:, None]).any(-1).all())
     assert int(cnt[0]) == 1  # counters advance in-kernel
 
 
-def test_sampling_distribution():
+@pytest.mark.parametrize("fast", [False, True])
+def test_sampling_distribution(fast):
     R = 4096
     base = torch.tensor([3.0, 2.0, 1.0, 0.5, -1.0], device=DEV)
     logits = torch.full((R, 1000), -30.0, device=DEV)
@@ -220,12 +223,12 @@ def test_sampling_distribution():
     topk = torch.full((R,), 3, dtype=torch.int32, device=DEV)
     topp = torch.ones(R, device=DEV)
     cnt = torch.arange(R, dtype=torch.int64, device=DEV)
-    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt).long()
+    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt, fast=fast).long()
     assert int(tok.max()) <= 2
     freq = torch.bincount(tok, minlength=3).float() / R
     p = torch.softmax(base[:3], 0)
     assert torch.allclose(freq, p, atol=0.03), (freq, p)
     # top-p 0.7 on probs [.665,.245,.09] keeps {0,1}: ascending cumsum .09 <= .3 drops token 2
     topp.fill_(0.7)
-    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt).long()
+    tok = ops.sample_tokens(logits, temp, topk, topp, 7, cnt, fast=fast).long()
     assert int(tok.max()) <= 1
