@@ -22,6 +22,15 @@ from assistant.ai.domain import AIResponse, Message
 from assistant.ai.providers.base import AIEmbedder, AIProvider
 
 _JSON_BLOCK = re.compile(r"```json\s*(.*?)```", re.S)
+_COMMENT = re.compile(r"//[^\n]*")
+
+
+def parse_example_json(text: str):
+    """Parse a prompt's example schema: strips // comments, '...' lines and trailing commas."""
+    body = _COMMENT.sub("", text)
+    body = "\n".join(line for line in body.splitlines() if line.strip() not in ("...", "..."))
+    body = re.sub(r",(\s*[\]}])", r"\1", body)
+    return json.loads(body)
 
 
 class FakeAIProvider(AIProvider):
@@ -60,7 +69,7 @@ class FakeAIProvider(AIProvider):
                 blocks = _JSON_BLOCK.findall(m.get("content") or "")
                 if blocks:
                     try:
-                        result = json.loads(blocks[0])
+                        result = parse_example_json(blocks[0])
                     except json.JSONDecodeError:
                         pass
                     break

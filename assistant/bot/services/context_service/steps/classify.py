@@ -1,0 +1,68 @@
+"""Topic classification with the fast model (reference steps/classify.py:13-97)."""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+from asgiref.sync import sync_to_async
+
+from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
+from assistant.bot.services.context_service.utils import add_system_message, get_list_str
+from assistant.bot.services.schema_service import json_prompt
+from assistant.utils.fuzzy import extract_bests
+from assistant.utils.repeat_until import repeat_until
+
+SMALL_TALK = "Small talk"
+
+
+class ClassifyStep(ContextProcessingStep):
+    debug_info_key = "classify"
+    _offtopic_examples = [("Hello", SMALL_TALK), ("How are you?", SMALL_TALK),
+                          ("What's the weather in Moscow?", SMALL_TALK)]
+
+    @ai_debugger
+    async def run(self):
+        from assistant.storage.models import WikiDocument, WikiDocumentProcessing
+
+        roots = await sync_to_async(lambda: list(WikiDocument.objects.filter(
+            bot=self._bot, processing__status=WikiDocumentProcessing.Status.COMPLETED, parent=None).distinct()))()
+        topics = [SMALL_TALK] + [w.title for w in roots]
+        examples = self._offtopic_examples + await sync_to_async(self._examples)(roots)
+        messages = add_system_message(self._state.messages, self.prompt(topics, examples, self._state.user_question))
+        response = await repeat_until(self._fast_ai.get_response, messages, max_tokens=256, json_format=True,
+                                      condition=self._condition)
+        topic = response.result["topic"]
+        self._logger.info("classified question as %s", topic)
+        best = extract_bests(topic, topics, limit=1)
+        best_title = best[0][0] if best else SMALL_TALK
+        if best_title == SMALL_TALK:
+            self._debug_info["topic"] = SMALL_TALK
+            return
+        wd = roots[topics.index(best_title) - 1]
+        self._debug_info["topic"] = wd.title
+        self._state.topic = wd
+
+    @staticmethod
+    def prompt(topics, examples, user_question) -> str:
+        return (
+            "Classify the user's question in a way that will help to search answer in the database by sentence "
+            "embeddings.\nDo not answer the question, but just classify to provide the search query.\n\n"
+            f"Possible topics:\n{get_list_str(topics)}\n"
+            f"Examples:\n{get_list_str([f'{chr(34)}{q}{chr(34)} -> {chr(34)}{t}{chr(34)}' for q, t in examples])}\n\n"
+            f"Please, provide the topic name that is relevant to the user question:\n```\n{user_question}\n```\n"
+            "Give only the topic name in the original spelling including language.\n"
+            f"{json_prompt(['classify'])}"
+        )
+
+    def _examples(self, roots, per_topic: int = 2) -> List[Tuple[str, str]]:
+        from assistant.storage.models import Question
+
+        out = []
+        for wiki in roots:
+            qs = Question.objects.filter(document__wiki__tree_id=wiki.tree_id, document__wiki__lft__gt=wiki.lft,
+                                         document__wiki__rght__lt=wiki.rght).order_by("?")[:per_topic]
+            out += [(q.text, wiki.title) for q in qs]
+        return out
+
+    @staticmethod
+    def _condition(response) -> bool:
+        return isinstance(response.result, dict) and isinstance(response.result.get("topic"), str)

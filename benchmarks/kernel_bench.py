@@ -111,7 +111,10 @@ def select_suite():
     topp = torch.full((64,), 0.95, device="cuda")
     cnt = torch.zeros(64, dtype=torch.int64, device="cuda")
     t = timeit(lambda: ops.sample_tokens(logits, temp, topk, topp, 1, cnt))
-    emit(op="sample-topk50-topp95", rows=64, vocab=128256, us=round(t * 1e6, 1))
+    emit(op="sample-topk50-topp95-1stage", rows=64, vocab=128256, us=round(t * 1e6, 1))
+    ws = ops.kernels.sample_workspace(64, 128256, "cuda")
+    t = timeit(lambda: ops.sample_tokens(logits, temp, topk, topp, 1, cnt, fast=True, workspace=ws))
+    emit(op="sample-topk50-topp95-2stage", rows=64, vocab=128256, us=round(t * 1e6, 1))
     s = torch.randn(64, 1_000_000, device="cuda")
     t = timeit(lambda: ops.topk_rows(s, 250), iters=5)
     emit(op="topk-250", rows=64, n=1_000_000, us=round(t * 1e6, 1), gbps=round(4 * 64e6 / t / 1e9))
