@@ -4,7 +4,7 @@ from __future__ import annotations
 
 from typing import List, Optional
 
-from asgiref.sync import sync_to_async
+from assistant.utils.sync import sync_to_async
 
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
 from assistant.bot.services.context_service.utils import add_system_message

@@ -1,11 +1,10 @@
 """Known-question matching with the fast model (reference steps/choose_known_question.py:9-61)."""
 from __future__ import annotations
 
-from asgiref.sync import sync_to_async
-
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
 from assistant.bot.services.context_service.utils import add_system_message, get_numerical_list_str
 from assistant.bot.services.schema_service import json_prompt
+from assistant.rag.knowledge import get_knowledge_base
 from assistant.utils.repeat_until import repeat_until
 
 
@@ -43,7 +42,9 @@ class ChooseKnownQuestionStep(ContextProcessingStep):
         if n and 1 <= n <= len(questions):
             q = questions[n - 1]
             self._debug_info["the_same_question"] = q.text
-            document = await sync_to_async(lambda: q.document)()
+            document = await get_knowledge_base(self._bot).get_document(q.document_id)
+            if document is None:
+                return
             self._debug_info["document"] = f"[{document.id}] {document.name}"
             self._state.documents = [document]
         else:

@@ -1,13 +1,10 @@
 """Topic classification with the fast model (reference steps/classify.py:13-97)."""
 from __future__ import annotations
 
-from typing import List, Tuple
-
-from asgiref.sync import sync_to_async
-
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
 from assistant.bot.services.context_service.utils import add_system_message, get_list_str
 from assistant.bot.services.schema_service import json_prompt
+from assistant.rag.knowledge import get_knowledge_base
 from assistant.utils.fuzzy import extract_bests
 from assistant.utils.repeat_until import repeat_until
 
@@ -21,12 +18,13 @@ class ClassifyStep(ContextProcessingStep):
 
     @ai_debugger
     async def run(self):
-        from assistant.storage.models import WikiDocument, WikiDocumentProcessing
-
-        roots = await sync_to_async(lambda: list(WikiDocument.objects.filter(
-            bot=self._bot, processing__status=WikiDocumentProcessing.Status.COMPLETED, parent=None).distinct()))()
-        topics = [SMALL_TALK] + [w.title for w in roots]
-        examples = self._offtopic_examples + await sync_to_async(self._examples)(roots)
+        kb = get_knowledge_base(self._bot)
+        roots = await kb.topics()
+        if not roots:  # empty knowledge base: nothing to route to, skip the LLM call
+            self._debug_info["topic"] = SMALL_TALK
+            return
+        topics = [SMALL_TALK] + [t.title for t in roots]
+        examples = self._offtopic_examples + [(q, t.title) for t in roots for q in t.examples]
         messages = add_system_message(self._state.messages, self.prompt(topics, examples, self._state.user_question))
         response = await repeat_until(self._fast_ai.get_response, messages, max_tokens=256, json_format=True,
                                       condition=self._condition)
@@ -37,9 +35,9 @@ class ClassifyStep(ContextProcessingStep):
         if best_title == SMALL_TALK:
             self._debug_info["topic"] = SMALL_TALK
             return
-        wd = roots[topics.index(best_title) - 1]
-        self._debug_info["topic"] = wd.title
-        self._state.topic = wd
+        chosen = roots[topics.index(best_title) - 1]
+        self._debug_info["topic"] = chosen.title
+        self._state.topic = chosen
 
     @staticmethod
     def prompt(topics, examples, user_question) -> str:
@@ -52,16 +50,6 @@ class ClassifyStep(ContextProcessingStep):
             "Give only the topic name in the original spelling including language.\n"
             f"{json_prompt(['classify'])}"
         )
-
-    def _examples(self, roots, per_topic: int = 2) -> List[Tuple[str, str]]:
-        from assistant.storage.models import Question
-
-        out = []
-        for wiki in roots:
-            qs = Question.objects.filter(document__wiki__tree_id=wiki.tree_id, document__wiki__lft__gt=wiki.lft,
-                                         document__wiki__rght__lt=wiki.rght).order_by("?")[:per_topic]
-            out += [(q.text, wiki.title) for q in qs]
-        return out
 
     @staticmethod
     def _condition(response) -> bool:

@@ -1,5 +1,5 @@
 """Context assembly within the token budget (reference steps/fill_info.py:6-33)."""
-from asgiref.sync import sync_to_async
+from assistant.utils.sync import sync_to_async
 
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep
 

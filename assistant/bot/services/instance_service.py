@@ -10,7 +10,7 @@ import logging
 import threading
 from contextlib import AbstractAsyncContextManager
 
-from asgiref.sync import sync_to_async
+from assistant.utils.sync import sync_to_async
 from django.db import connection, transaction
 
 logger = logging.getLogger(__name__)

@@ -1,6 +1,7 @@
 """Bot helpers: platform / bot-class resolution (reference bot/utils.py:16-70)."""
 from __future__ import annotations
 
+import importlib
 import logging
 from functools import lru_cache
 
@@ -41,8 +42,6 @@ def get_bot_platform(bot_codename: str, platform_codename: str):
 
 @lru_cache
 def get_bot_class(bot_codename: str):
-    from django.utils.module_loading import import_string
-
     cfg = settings.get("BOTS", {}) or {}
     path = (cfg.get(bot_codename) or {}).get("class")
     if not path:
@@ -50,3 +49,9 @@ def get_bot_class(bot_codename: str):
                                                                                            DEFAULT_BOT_CLASS)
     logger.info("bot class %s for %s", path, bot_codename)
     return import_string(path)
+
+
+def import_string(path: str):
+    """``pkg.module.Name`` -> object (django.utils.module_loading.import_string without Django)."""
+    module_path, _, name = path.rpartition(".")
+    return getattr(importlib.import_module(module_path), name)

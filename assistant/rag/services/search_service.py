@@ -13,7 +13,7 @@ import logging
 from typing import List, Optional, Tuple
 
 import numpy as np
-from asgiref.sync import sync_to_async
+from assistant.utils.sync import sync_to_async
 
 from assistant.ai.services.ai_service import get_ai_embdedder
 from assistant.conf import settings
