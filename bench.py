@@ -90,7 +90,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=64, help="questions per GPU per step")
+    ap.add_argument("--batch", type=int, default=128,
+                    help="questions per GPU per step (128: +24%% QPS over 64 at p50 4.0 s vs 2.5 s, profiles/)")
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--index-rows", type=int, default=1_000_000, help="question rows in the whole (sharded) index")
     ap.add_argument("--rows-per-doc", type=int, default=10)
@@ -140,6 +141,14 @@ def main():
              for _ in range(W)]
     flat_q = [q for r in all_q for s in r for q in s]
     q_emb = torch.nn.functional.normalize(embedder.embed(flat_q).float(), dim=-1)
+    # Random-init encoders embed every question into a narrow cone (pairwise cos ~0.96), so rows
+    # planted at q + noise would also match the OTHER questions and the hit lists would depend on how
+    # many questions were planted (i.e. on --batch).  Planting along each question's own component
+    # off the common direction (q + beta * (q - (q.mu) mu)) keeps its rows ~0.13 closer to it than to
+    # any other question: every query then retrieves its own 3-5 documents at any batch size.
+    mu = torch.nn.functional.normalize(q_emb.mean(0), dim=0)
+    q_own = q_emb - (q_emb @ mu)[:, None] * mu[None]
+    beta = 3.0
     prng = np.random.default_rng(args.seed + 999)
     plant_ids, plant_vecs, plant_docs = [], [], []
     for qi in range(len(flat_q)):
@@ -148,15 +157,15 @@ def main():
         for rank_t, d in enumerate(targets):
             rows = d * args.rows_per_doc + np.arange(min(args.rows_per_doc, 6))
             rows = rows[rows < n_rows]
-            sigma = 0.02 + 0.004 * rank_t  # cos ~0.87..0.80: broad-search path, not the 0.05 shortcut
+            sigma = 0.02 + 0.004 * rank_t  # distance ~0.18: broad-search path, not the 0.05 shortcut
             noise = torch.randn((len(rows), embedder.dim), device=dev, generator=torch.Generator(device=dev)
                                 .manual_seed(qi * 10 + rank_t)) * sigma
             plant_ids.append(rows)
-            plant_vecs.append(q_emb[qi][None] + noise)
+            plant_vecs.append((q_emb[qi] + beta * q_own[qi])[None] + noise)
             plant_docs.append(np.full(len(rows), d, dtype=np.int64))
     index.add(np.concatenate(plant_ids), torch.cat(plant_vecs), doc_ids=np.concatenate(plant_docs),
               groups=np.zeros(sum(len(x) for x in plant_ids), dtype=np.int32))
-    del q_emb
+    del q_emb, q_own
     rag = RAGPipeline(embedder, index, llm, docs, system_text=SYSTEM_TEXT)
     params = SamplingParams(max_new_tokens=args.max_new_tokens, ignore_eos=True, temperature=1.0, top_k=50,
                             top_p=0.95)
@@ -211,6 +220,7 @@ def main():
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
             "graphs": not args.no_graphs,
+            "tuned_gemm_shapes": llm.tuned_gemms,
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
             "engine_rank0": eng,

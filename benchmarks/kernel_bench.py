@@ -52,6 +52,26 @@ def gemm_suite(which):
         flop = 2.0 * M * N * K
         byts = 2.0 * (M * K + N * K + M * N)
         res = {"op": name, "M": M, "N": N, "K": K}
+        if M <= ops.SKINNY_MAX_M and name.startswith("llama8b"):
+            S = ops.skinny_splits(N, K)
+            slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
+            t_sk = timeit(lambda: ops.skinny_gemm(a, b, splits=S, out=slabs))
+            res.update(skinny_splits=S, skinny_us=round(t_sk * 1e6, 1), skinny_gbps=round(byts / t_sk / 1e9))
+            # cold weights (decode streams 16 GB per step, nothing stays in L2/MALL): rotate copies
+            ncopy = max(2, int(2e9 // (N * K * 2)) + 1)
+            ws = [b] + [b.clone() for _ in range(ncopy - 1)]
+            it = [0]
+
+            def nxt():
+                it[0] = (it[0] + 1) % ncopy
+                return ws[it[0]]
+            t_c = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=False), iters=ncopy * 2)
+            t_cn = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=True), iters=ncopy * 2)
+            t_cl = timeit(lambda: F.linear(a, nxt()), iters=ncopy * 2)
+            res.update(cold_skinny_us=round(t_c * 1e6, 1), cold_skinny_nt_us=round(t_cn * 1e6, 1),
+                       cold_hipblaslt_us=round(t_cl * 1e6, 1), cold_skinny_gbps=round(byts / t_c / 1e9),
+                       cold_hipblaslt_gbps=round(byts / t_cl / 1e9))
+            del ws
         if name == "index-scan":
             t_nat = timeit(lambda: ops.gemm_bt(a, b, epilogue=ops.EPI_SCORES, out_f32=True), iters=5)
             t_lib = timeit(lambda: torch.mm(a, b.t()).float(), iters=5)
@@ -127,7 +147,7 @@ def select_suite():
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which in ("all", "gemm"):
-        gemm_suite(None)
+        gemm_suite(sys.argv[2] if len(sys.argv) > 2 else None)
     if which in ("all", "attn"):
         attn_suite()
     if which in ("all", "select"):

@@ -51,14 +51,23 @@ PYBIND11_MODULE(_native, m) {
   m.def("gelu", [](u out, u x, u bias, size_t rows, int cols, u s) {
     check(dab::gelu(VP(out), CVP(x), CVP(bias), rows, cols, ST(s)), "gelu");
   });
-  m.def("silu_mul", [](u out, u x, size_t rows, int F, u s) {
-    check(dab::silu_mul(VP(out), CVP(x), rows, F, ST(s)), "silu_mul");
-  });
+  m.def("silu_mul", [](u out, u x, size_t rows, int F, u s, int interleaved) {
+    check(dab::silu_mul(VP(out), CVP(x), rows, F, ST(s), interleaved), "silu_mul");
+  }, py::arg("out"), py::arg("x"), py::arg("rows"), py::arg("F"), py::arg("s"), py::arg("interleaved") = 0);
   m.def("rope_kv_write", [](u qkv, int ld, u positions, u cos_sin, u q_out, u k_cache, u v_cache, u slots, int T,
-                            int Hq, int Hkv, int D, int block_size, u s) {
+                            int Hq, int Hkv, int D, int block_size, u s, u slabs, int S, long slab_stride) {
     check(dab::rope_kv_write(CVP(qkv), ld, (const int*)positions, CVP(cos_sin), VP(q_out), VP(k_cache), VP(v_cache),
-                             (const int64_t*)slots, T, Hq, Hkv, D, block_size, ST(s)),
+                             (const int64_t*)slots, T, Hq, Hkv, D, block_size, ST(s), (const float*)slabs, S,
+                             slab_stride),
           "rope_kv_write");
+  }, py::arg("qkv"), py::arg("ld"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"),
+     py::arg("v_cache"), py::arg("slots"), py::arg("T"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
+     py::arg("block_size"), py::arg("s"), py::arg("slabs") = 0, py::arg("S") = 0, py::arg("slab_stride") = 0);
+  m.def("rmsnorm_slabs", [](u out, u res_out, u slabs, int S, long slab_stride, u res_in, u w, int rows, int cols,
+                            float eps, u s) {
+    check(dab::rmsnorm_slabs(VP(out), VP(res_out), (const float*)slabs, S, slab_stride, CVP(res_in), CVP(w), rows, cols,
+                             eps, ST(s)),
+          "rmsnorm_slabs");
   });
   m.def("flash_attention",
         [](u q, long qst, long qsh, u k, u v, long kvst, long kvsh, u kc, u vc, u bt, int max_blocks, int bs, u out,
@@ -82,6 +91,16 @@ PYBIND11_MODULE(_native, m) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
                        (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s)),
           "gemm_bt");
+  });
+  m.def("skinny_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
+                          int S, int epilogue, u s, int nt) {
+    check(dab::skinny_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt),
+          "skinny_gemm");
+  }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
+     py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
+     py::arg("nt") = 0);
+  m.def("skinny_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
+    check(dab::skinny_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "skinny_reduce");
   });
   m.def("sample_tokens", [](u logits, int f32, long ld, int rows, int vocab, u temp, u top_k, u top_p,
                             unsigned long long seed, u counters, u out_tokens, u out_logprobs, u s) {

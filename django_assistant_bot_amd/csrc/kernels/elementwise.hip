@@ -25,9 +25,9 @@ __global__ __launch_bounds__(256) void gelu_kernel(bf16* __restrict__ out, const
   }
 }
 
-// x: [rows, 2F] = [gate | up]; out: [rows, F]
+// x: [rows, 2F] = [gate | up] (or, interleaved, 16-column groups [g16 | u16 | g16 | ...]); out: [rows, F]
 __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, const bf16* __restrict__ x,
-                                                       size_t rows, int F) {
+                                                       size_t rows, int F, int interleaved) {
   const int fvec = F >> 3;
   const size_t nvec = rows * fvec;
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (size_t)gridDim.x * 256) {
@@ -35,8 +35,14 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, c
     const int c = (int)(i - r * fvec);
     const u32x4* xr = reinterpret_cast<const u32x4*>(x + r * 2 * F);
     float g[8], u[8], o[8];
-    unpack8(xr[c], g);
-    unpack8(xr[c + fvec], u);
+    if (interleaved) {
+      const int gc = 4 * (c >> 1) + (c & 1);  // 8-col chunk c of the output -> gate chunk in [g16|u16] pairs
+      unpack8(xr[gc], g);
+      unpack8(xr[gc + 2], u);
+    } else {
+      unpack8(xr[c], g);
+      unpack8(xr[c + fvec], u);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
     reinterpret_cast<u32x4*>(out + r * F)[c] = pack8(o);
@@ -53,7 +59,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
                                                       const float2* __restrict__ cos_sin, bf16* __restrict__ q_out,
                                                       bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
                                                       const int64_t* __restrict__ slots, int T, int Hq, int Hkv, int D,
-                                                      int block_size) {
+                                                      int block_size, const float* __restrict__ slabs, int S,
+                                                      long slab_stride) {
   const int per_head = D >> 4;  // threads per head
   const int heads = Hq + 2 * Hkv;
   const size_t total = (size_t)T * heads * per_head;
@@ -64,11 +71,35 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   const int h = (int)(th % heads);
   const int t = (int)(th / heads);
   const int half = D >> 1;
-  const bf16* src = qkv + (size_t)t * ld + (size_t)h * D;
   const int i0 = c * 8;
   float x1[8], x2[8];
-  unpack8(*reinterpret_cast<const u32x4*>(src + i0), x1);
-  unpack8(*reinterpret_cast<const u32x4*>(src + i0 + half), x2);
+  if (slabs) {
+    // split-K slabs of the QKV projection: sum, then round like a bf16 GEMM output
+    const float* src = slabs + (size_t)t * ld + (size_t)h * D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
+    for (int sl = 0; sl < S; ++sl, src += slab_stride) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + i0), a1 = *reinterpret_cast<const f32x4*>(src + i0 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(src + i0 + half);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(src + i0 + half + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x1[j] += a0[j];
+        x1[4 + j] += a1[j];
+        x2[j] += b0[j];
+        x2[4 + j] += b1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x1[j] = bf2f(f2bf(x1[j]));
+      x2[j] = bf2f(f2bf(x2[j]));
+    }
+  } else {
+    const bf16* src = qkv + (size_t)t * ld + (size_t)h * D;
+    unpack8(*reinterpret_cast<const u32x4*>(src + i0), x1);
+    unpack8(*reinterpret_cast<const u32x4*>(src + i0 + half), x2);
+  }
   if (h < Hq + Hkv) {
     const float2* cs = cos_sin + (size_t)positions[t] * half + i0;
     float o1[8], o2[8];
@@ -115,22 +146,24 @@ int gelu(void* out, const void* x, const void* bias, size_t rows, int cols, hipS
   return hipGetLastError();
 }
 
-int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s) {
-  if (F % 8) return hipErrorInvalidValue;
+int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s, int interleaved) {
+  if (F % 8 || (interleaved && F % 16)) return hipErrorInvalidValue;
   const size_t nvec = rows * (size_t)(F / 8);
   if (!nvec) return 0;
-  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(nvec)), dim3(256), 0, s, (bf16*)out, (const bf16*)x, rows, F);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid_for(nvec)), dim3(256), 0, s, (bf16*)out, (const bf16*)x, rows, F,
+                     interleaved);
   return hipGetLastError();
 }
 
 int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos_sin, void* q_out, void* k_cache,
-                  void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s) {
+                  void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s,
+                  const float* slabs, int S, long slab_stride) {
   if (T <= 0) return 0;
-  if (D % 16 || ld % 8) return hipErrorInvalidValue;
+  if (D % 16 || ld % 8 || (slabs && (S < 1 || slab_stride % 4))) return hipErrorInvalidValue;
   const size_t total = (size_t)T * (Hq + 2 * Hkv) * (D / 16);
   hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const bf16*)qkv, ld,
                      positions, (const float2*)cos_sin, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, slots, T, Hq,
-                     Hkv, D, block_size);
+                     Hkv, D, block_size, slabs, S, slab_stride);
   return hipGetLastError();
 }
 

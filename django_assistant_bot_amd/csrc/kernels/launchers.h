@@ -13,6 +13,8 @@ inline int div_up_host(int a, int b) { return (a + b - 1) / b; }
 // norm.hip
 int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const void* w, int rows, int cols, float eps,
             hipStream_t s);
+int rmsnorm_slabs(void* out, void* res_out, const float* slabs, int S, long slab_stride, const void* res_in,
+                  const void* w, int rows, int cols, float eps, hipStream_t s);
 int layernorm(void* out, const void* x, const void* res_in, const void* gamma, const void* beta, int rows, int cols,
               float eps, hipStream_t s);
 int bert_embed(void* out, const int* ids, const int* pos_ids, const int* type_ids, const void* word, const void* pos,
@@ -23,9 +25,10 @@ int mean_pool(float* out, void* out_bf16, const void* hidden, const int* cu_seql
 
 // elementwise.hip
 int gelu(void* out, const void* x, const void* bias, size_t rows, int cols, hipStream_t s);
-int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s);
+int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s, int interleaved = 0);
 int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos_sin, void* q_out, void* k_cache,
-                  void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s);
+                  void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s,
+                  const float* slabs = nullptr, int S = 0, long slab_stride = 0);
 
 // attention.hip
 int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const void* k, const void* v,
@@ -42,6 +45,13 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
             const uint32_t* allow, int allow_words, hipStream_t s);
+
+// skinny_gemm.hip (decode-sized M <= 64; S K-slices: S == 1 -> bf16 out with epilogue, S > 1 -> fp32
+// slabs [S][M][N] reduced by the consumer or by skinny_reduce)
+int skinny_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights = 0);
+int skinny_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
+                  hipStream_t s);
 
 // select.hip
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,

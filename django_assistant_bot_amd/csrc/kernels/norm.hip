@@ -56,6 +56,64 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, bf1
   }
 }
 
+// Same as rmsnorm_kernel but x arrives as S fp32 split-K slabs of the producing projection:
+// x = bf16(sum_s slabs[s]) (the rounding a bf16 GEMM output would have had).
+template <int NT, int VPT>
+__global__ __launch_bounds__(NT) void rmsnorm_slab_kernel(bf16* __restrict__ out, bf16* __restrict__ res_out,
+                                                          const float* __restrict__ slabs, int S, long slab_stride,
+                                                          const bf16* __restrict__ res_in, const bf16* __restrict__ w,
+                                                          int cols, float eps) {
+  __shared__ float red[NT / 64];
+  const size_t row = blockIdx.x;
+  const int nvec = cols >> 3;
+  const u32x4* rr = reinterpret_cast<const u32x4*>(res_in + row * cols);
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+      const float* src = slabs + row * cols + (size_t)i * 8;
+      for (int sl = 0; sl < S; ++sl, src += slab_stride) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[k][j] += a[j];
+          v[k][4 + j] += b[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j]));
+      if (res_in) {
+        float r[8];
+        unpack8(rr[i], r);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + r[j]));
+        reinterpret_cast<u32x4*>(res_out + row * cols)[i] = pack8(v[k]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
+    }
+  }
+  const float tot = block_sum<NT>(ss, red);
+  const float inv = rsqrtf(tot / (float)cols + eps);
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  u32x4* orow = reinterpret_cast<u32x4*>(out + row * cols);
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const int i = threadIdx.x + k * NT;
+    if (i < nvec) {
+      float g[8], o[8];
+      unpack8(wr[i], g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * inv * g[j];
+      orow[i] = pack8(o);
+    }
+  }
+}
+
 // out = LayerNorm(x + res) * gamma + beta   (BERT post-LN; two-pass mean/var in registers)
 template <int NT, int VPT>
 __global__ __launch_bounds__(NT) void layernorm_kernel(bf16* __restrict__ out, const bf16* __restrict__ x,
@@ -265,6 +323,15 @@ int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const v
   if (cols % 8 || cols > 16384) return hipErrorInvalidValue;
   DAB_ROW_DISPATCH(rmsnorm_kernel, rows, cols, s, (bf16*)out, (bf16*)res_out, (const bf16*)x, (const bf16*)res_in,
                    (const bf16*)w, cols, eps);
+  return hipGetLastError();
+}
+
+int rmsnorm_slabs(void* out, void* res_out, const float* slabs, int S, long slab_stride, const void* res_in,
+                  const void* w, int rows, int cols, float eps, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (cols % 8 || cols > 16384 || S < 1 || slab_stride % 4) return hipErrorInvalidValue;
+  DAB_ROW_DISPATCH(rmsnorm_slab_kernel, rows, cols, s, (bf16*)out, (bf16*)res_out, slabs, S, slab_stride,
+                   (const bf16*)res_in, (const bf16*)w, cols, eps);
   return hipGetLastError();
 }
 

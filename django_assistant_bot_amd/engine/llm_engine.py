@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import itertools
 import math
+import os
 import time
 from collections import deque
 from dataclasses import dataclass, field
@@ -93,7 +94,7 @@ class LLMEngine:
                  checkpoint: str | None = None, seed: int = 0, max_batch: int = 256, block_size: int = 64,
                  max_model_len: int | None = None, kv_cache_gb: float | None = None, num_blocks: int | None = None,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
-                 tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = False,
+                 tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
                  part_size: int = 512, kv_memory_fraction: float = 0.85):
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
@@ -112,6 +113,12 @@ class LLMEngine:
         self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
                                 interleaved_mlp=interleaved_mlp)
         del weights
+        self.tuned_gemms = 0
+        if self.device.type == "cuda" and os.environ.get("DAB_GEMM_TUNING", "1") != "0":
+            from ..ops import tuning
+
+            arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
+            self.tuned_gemms = tuning.load(tuning.tuning_file(cfg.name, tp_size, arch))
         self.tokenizer = Tokenizer.for_decoder(cfg, checkpoint)
         self.max_batch = max_batch
         self.block_size = block_size

@@ -15,12 +15,14 @@ columns (Megatron split); the two all-reduces per layer run on the RCCL process 
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import torch
 
 from .. import ops
 from ..ops import reference as ref
+from ..ops import tuning
 from .configs import DecoderConfig
 
 
@@ -79,6 +81,14 @@ class LlamaModel:
             DecoderLayer(*(w[f"l{i}.{n}"] for n in ("attn_norm", "qkv_w", "o_w", "mlp_norm", "gate_up_w", "down_w")))
             for i in range(cfg.layers)
         ]
+        # decode projections on the weight-streaming kernel: "all", "none", or a comma list of
+        # qkv,o,gate_up,down,lm_head (the kernel beats hipBLASLt on the narrow-N projections)
+        sel = os.environ.get("DAB_SKINNY", "none")  # measured: ties hipBLASLt at M=64 (profiles/)
+        sel = {"1": "all", "0": "none"}.get(sel, sel)
+        names = ("qkv", "o", "gate_up", "down", "lm_head")
+        self.skinny_for = set(names) if sel == "all" else set() if sel == "none" else set(sel.split(","))
+        self.use_skinny = bool(self.skinny_for)
+        self._split_cache: dict = {}
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -93,12 +103,33 @@ class LlamaModel:
             dist.all_reduce(x, group=self.tp_group)
         return x
 
+    def _splits(self, w: torch.Tensor) -> int:
+        key = id(w)
+        s = self._split_cache.get(key)
+        if s is None:
+            s = self._split_cache[key] = ops.skinny_splits(w.shape[0], w.shape[1])
+        return s
+
+    def _proj(self, x, w, sk: bool, allow_slabs: bool = True, name: str = ""):
+        """Projection of the decode (``sk``: weight-streaming kernel, fp32 split-K slabs when the
+        consumer can sum them) or prefill path (hipBLASLt)."""
+        if not sk or name not in self.skinny_for:
+            return tuning.linear(x, w) if x.is_cuda else ops.linear(x, w)
+        s = self._splits(w)
+        if s > 1 and not allow_slabs:
+            return ops.skinny_reduce(ops.skinny_gemm(x, w, splits=s))
+        return ops.skinny_gemm(x, w, splits=s)
+
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: KVCache) -> torch.Tensor:
         """ids int32 [T] -> final hidden states [T, H] (after the last RMSNorm)."""
         cfg = self.cfg
         D = cfg.head_dim
         T = ids.numel()
         x = ops.embed_gather(ids, self.embed)
+        # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
+        # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
+        sk = self.use_skinny and meta.decode and T <= ops.SKINNY_MAX_M and x.is_cuda
+        slabs_ok = self.tp_size == 1  # under TP the partial sums go through the all-reduce as bf16
         residual = None
         for li, L in enumerate(self.layers):
             if residual is None:
@@ -106,7 +137,7 @@ class LlamaModel:
                 residual = x
             else:
                 h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
-            qkv = ops.linear(h, L.qkv_w)
+            qkv = self._proj(h, L.qkv_w, sk, name="qkv")
             q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv,
                                   D)
             if meta.decode:
@@ -115,16 +146,20 @@ class LlamaModel:
             else:
                 a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                               meta.max_q, causal=True)
-            o = self._all_reduce(ops.linear(a.view(T, self.hq * D), L.o_w))
+            o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o"))
             h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
-            if self.interleaved_mlp:
-                act = ops.linear(h, L.gate_up_w, act="swiglu")
+            if sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
+                act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
             else:
-                act = ops.silu_mul(ops.linear(h, L.gate_up_w))
-            x = self._all_reduce(ops.linear(act, L.down_w))
+                gu = tuning.linear(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
+                act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
+            x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
         out, _ = ops.rmsnorm(x, self.final_norm, cfg.eps, residual=residual)
         return out
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """[n, H] -> [n, V] logits (bf16 GEMM; the sampler reads bf16 or fp32)."""
-        return ops.linear(h, self.lm_head)
+        if ("lm_head" in self.skinny_for and h.is_cuda and h.shape[0] <= ops.SKINNY_MAX_M
+                and self.lm_head.shape[0] % 64 == 0):
+            return ops.skinny_gemm(h, self.lm_head)
+        return tuning.linear(h, self.lm_head) if h.is_cuda else ops.linear(h, self.lm_head)

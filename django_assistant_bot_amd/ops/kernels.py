@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -28,18 +30,35 @@ def _i32(t: torch.Tensor) -> None:
 
 def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor | None = None):
     """RMSNorm over the last dim; with ``residual`` the input is ``x + residual`` and the sum is
-    also returned (fused residual stream).  Returns (out, residual_out)."""
+    also returned (fused residual stream).  Returns (out, residual_out).
+
+    ``x`` may also be fp32 split-K slabs [S, rows, cols] of the producing projection
+    (``skinny_gemm(..., splits=S)``): they are summed (and rounded to bf16) inside the kernel."""
+    slabs = x.dtype == torch.float32 and x.dim() == 3
     if not x.is_cuda:
+        if slabs:
+            x = x.sum(0).to(torch.bfloat16)
         return ref.rmsnorm(x, w, eps, residual)
-    expect_bf16_contig(x, w, residual)
+    expect_bf16_contig(w, residual)
     same_device(x, w, residual)
     cols = x.shape[-1]
-    rows = x.numel() // cols
     expect(w.numel() == cols, "rmsnorm weight size mismatch")
-    expect(residual is None or residual.shape == x.shape, "residual shape mismatch")
-    out = torch.empty_like(x)
-    res_out = torch.empty_like(x) if residual is not None else None
-    native().rmsnorm(ptr(out), ptr(res_out), ptr(x), ptr(residual), ptr(w), rows, cols, float(eps), stream(x))
+    if slabs:
+        expect(x.is_contiguous(), "slabs must be contiguous")
+        S, rows = x.shape[0], x.shape[1]
+        shape = (rows, cols)
+    else:
+        expect_bf16_contig(x)
+        rows = x.numel() // cols
+        shape = tuple(x.shape)
+    expect(residual is None or tuple(residual.shape) == shape, "residual shape mismatch")
+    out = torch.empty(shape, dtype=torch.bfloat16, device=x.device)
+    res_out = torch.empty(shape, dtype=torch.bfloat16, device=x.device) if residual is not None else None
+    if slabs:
+        native().rmsnorm_slabs(ptr(out), ptr(res_out), ptr(x), S, rows * cols, ptr(residual), ptr(w), rows, cols,
+                               float(eps), stream(x))
+    else:
+        native().rmsnorm(ptr(out), ptr(res_out), ptr(x), ptr(residual), ptr(w), rows, cols, float(eps), stream(x))
     return out, res_out
 
 
@@ -114,36 +133,52 @@ def gelu(x, bias=None, out=None):
     return out
 
 
-def silu_mul(x):
-    """x [..., 2F] = [gate | up] -> silu(gate) * up  [..., F]"""
+def silu_mul(x, interleaved=False):
+    """x [..., 2F] = [gate | up] -> silu(gate) * up  [..., F].  ``interleaved``: x columns are
+    16-wide [gate | up] groups (the projection of ``interleave_gate_up`` weights)."""
     if not x.is_cuda:
+        if interleaved:
+            F2 = x.shape[-1]
+            v = x.reshape(*x.shape[:-1], F2 // 32, 2, 16)
+            x = torch.cat([v[..., 0, :].reshape(*x.shape[:-1], F2 // 2), v[..., 1, :].reshape(*x.shape[:-1], F2 // 2)], -1)
         return ref.silu_mul(x)
     expect_bf16_contig(x)
     F2 = x.shape[-1]
     rows = x.numel() // F2
     out = torch.empty((*x.shape[:-1], F2 // 2), dtype=x.dtype, device=x.device)
-    native().silu_mul(ptr(out), ptr(x), rows, F2 // 2, stream(x))
+    native().silu_mul(ptr(out), ptr(x), rows, F2 // 2, stream(x), int(interleaved))
     return out
 
 
 def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D):
     """Applies RoPE to the q/k heads of ``qkv`` [T, (Hq+2Hkv)*D]; writes k, v into the paged caches
-    [num_blocks, Hkv, block_size, D] at ``slots`` (int64, <0 skipped); returns q [T, Hq, D]."""
+    [num_blocks, Hkv, block_size, D] at ``slots`` (int64, <0 skipped); returns q [T, Hq, D].
+    ``qkv`` may also be fp32 split-K slabs [S, T, (Hq+2Hkv)*D], summed inside the kernel."""
     block_size = k_cache.shape[2]
+    slabs = qkv.dtype == torch.float32 and qkv.dim() == 3
     if not qkv.is_cuda:
+        if slabs:
+            qkv = qkv.sum(0).to(torch.bfloat16)
         return ref.rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, block_size)
-    expect_bf16_contig(qkv, k_cache, v_cache)
+    expect_bf16_contig(k_cache, v_cache)
     _i32(positions)
     expect(slots.dtype == torch.int64 and slots.is_contiguous(), "slots must be contiguous int64")
     expect(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous(), "cos_sin must be contiguous fp32")
-    T = qkv.shape[0]
-    expect(qkv.shape[1] == (Hq + 2 * Hkv) * D, "qkv width mismatch")
+    T = qkv.shape[-2]
+    expect(qkv.shape[-1] == (Hq + 2 * Hkv) * D, "qkv width mismatch")
     expect(positions.numel() == T and slots.numel() == T, "positions / slots length mismatch")
     expect(tuple(k_cache.shape[1:]) == (Hkv, block_size, D) and k_cache.shape == v_cache.shape, "cache shape mismatch")
     expect(cos_sin.shape[1] == D // 2, "cos/sin table width mismatch")
-    q = torch.empty((T, Hq, D), dtype=qkv.dtype, device=qkv.device)
-    native().rope_kv_write(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache), ptr(v_cache),
-                           ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv))
+    q = torch.empty((T, Hq, D), dtype=torch.bfloat16, device=qkv.device)
+    if slabs:
+        expect(qkv.is_contiguous(), "slabs must be contiguous")
+        native().rope_kv_write(0, qkv.shape[-1], ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache), ptr(v_cache),
+                               ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv), ptr(qkv), qkv.shape[0],
+                               T * qkv.shape[-1])
+    else:
+        expect_bf16_contig(qkv)
+        native().rope_kv_write(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache),
+                               ptr(v_cache), ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv))
     return q
 
 
@@ -291,6 +326,83 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
                      residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), int(out_f32),
                      ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A))
+    return out
+
+
+SKINNY_MAX_M = 64
+_SK_KSTAGE = 256
+
+
+def skinny_splits(N: int, K: int, target_wgs: int = 384, max_splits: int = 16) -> int:
+    """K-slices for the weight-streaming GEMM: the fewest that give ~target_wgs workgroups (each
+    workgroup streams 64 weight rows of one slice)."""
+    tiles = N // 64
+    best = 1
+    for s in range(1, max_splits + 1):
+        if K % (s * _SK_KSTAGE):
+            continue
+        best = s
+        if tiles * s >= target_wgs:
+            break
+    return best
+
+
+SKINNY_NT_WEIGHTS = os.environ.get("DAB_SKINNY_NT", "0") == "1"
+
+
+def skinny_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=None):
+    """Decode GEMM y = x w^T for M <= 64 rows on the weight-streaming MFMA kernel.
+
+    splits == 1 -> bf16 [M, N] (or [M, N/2] with EPI_SWIGLU on 16-row interleaved gate|up weights),
+    optional fused residual add.  splits > 1 -> fp32 K-slice slabs [splits, M, N] (sum them with
+    ``skinny_reduce`` or hand them to a slab-aware consumer)."""
+    if not x.is_cuda:
+        y = ref.gemm_bt(x, w, None, None, epilogue, out_f32=splits > 1)
+        if splits > 1:
+            return torch.cat([y[None], torch.zeros((splits - 1,) + tuple(y.shape), dtype=y.dtype)], 0)
+        return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
+    expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
+    expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
+    M, K = x.shape
+    N = w.shape[0]
+    expect(w.shape[1] == K and M <= SKINNY_MAX_M, "skinny_gemm: inner dims mismatch or M > 64")
+    expect(N % 64 == 0 and K % (splits * _SK_KSTAGE) == 0, "skinny_gemm needs N % 64 == 0 and K % (256*splits) == 0")
+    expect(x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0, "row strides must be multiples of 8")
+    if splits > 1:
+        expect(epilogue == EPI_NONE and residual is None, "split-K writes raw slabs")
+        if out is None:
+            out = torch.empty((splits, M, N), dtype=torch.float32, device=x.device)
+        expect(out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
+        ldo = N
+    else:
+        n_out = N // 2 if epilogue == EPI_SWIGLU else N
+        if residual is not None:
+            expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
+                   and tuple(residual.shape) == (M, N), "residual must be bf16 [M, N]")
+        if out is None:
+            out = torch.empty((M, n_out), dtype=torch.bfloat16, device=x.device)
+        expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
+        ldo = out.stride(0)
+    native().skinny_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
+                         residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
+                         int(SKINNY_NT_WEIGHTS if nt is None else nt))
+    return out
+
+
+def skinny_reduce(slabs, residual=None, out=None):
+    """fp32 slabs [S, M, N] -> bf16 [M, N] (sum rounded to bf16, then + residual)."""
+    if not slabs.is_cuda:
+        y = slabs.sum(0).to(torch.bfloat16)
+        return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
+    S, M, N = slabs.shape
+    expect(slabs.dtype == torch.float32 and slabs.is_contiguous() and N % 8 == 0, "bad slabs")
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.bfloat16, device=slabs.device)
+    if residual is not None:
+        expect(residual.dtype == torch.bfloat16 and tuple(residual.shape) == (M, N) and residual.stride(-1) == 1,
+               "residual must be bf16 [M, N]")
+    native().skinny_reduce(ptr(out), out.stride(0), ptr(slabs), S, M, N, ptr(residual),
+                           residual.stride(0) if residual is not None else 0, stream(slabs))
     return out
 
 

@@ -15,11 +15,26 @@ def main():
     lines = [f"# rocprofv3 kernel stats: {prefix}", "", f"total kernel time: {tot / 1e6:.1f} ms", ""]
     tpath = os.path.join(d, f"{prefix}_kernel_trace.csv")
     if os.path.exists(tpath):
-        iv = []
+        iv, named = [], []
         with open(tpath) as f:
             for r in csv.DictReader(f):
                 iv.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+                named.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Kernel_Name", "")))
         iv.sort()
+        named.sort()
+        # decode window: after the last prefill attention kernel, from the first to the last paged
+        # decode kernel -> GPU busy share and inter-kernel gaps inside the graph replays
+        last_pf = max((i for i, k in enumerate(named) if "flash_fwd" in k[2]), default=-1)
+        dec = [k for k in named[last_pf + 1:]]
+        di = [i for i, k in enumerate(dec) if "paged_decode" in k[2]]
+        if di:
+            win = dec[di[0]:di[-1] + 1]
+            wbusy = sum(e - s for s, e, _ in win)
+            wspan = win[-1][1] - win[0][0]
+            gaps = [max(0, win[i + 1][0] - win[i][1]) for i in range(len(win) - 1)]
+            lines += [f"decode window (last step): {len(win)} kernels, busy {wbusy / 1e6:.2f} ms of "
+                      f"{wspan / 1e6:.2f} ms ({100.0 * wbusy / max(wspan, 1):.1f} %), mean gap "
+                      f"{(sum(gaps) / max(1, len(gaps))) / 1e3:.2f} us, {len(di)} paged-decode launches", ""]
         busy, cur_s, cur_e = 0, None, None
         for s, e in iv:
             if cur_e is None or s > cur_e:

@@ -73,6 +73,21 @@ def test_gelu_silu():
     close(ops.gelu(x, b), ref.gelu(x, b))
     y = bf(17, 2 * 1408)
     close(ops.silu_mul(y), ref.silu_mul(y))
+    # 16-column interleaved [g16 | u16] layout == the projection of interleave_gate_up weights
+    g, u = bf(17, 1408), bf(17, 1408)
+    yi = ops.interleave_gate_up(g.t().contiguous(), u.t().contiguous()).t().contiguous()
+    close(ops.silu_mul(yi, interleaved=True), ref.silu_mul(torch.cat([g, u], -1)))
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_rmsnorm_slabs(S):
+    rows, cols = 21, 4096
+    slabs = torch.randn(S, rows, cols, device=DEV)
+    w, r = bf(cols), bf(rows, cols)
+    out, res = ops.rmsnorm(slabs, w, 1e-5, residual=r)
+    eo, er = ref.rmsnorm(slabs.sum(0).to(torch.bfloat16), w, 1e-5, residual=r)
+    close(out, eo)
+    assert torch.equal(res, er)
 
 
 def test_rope_kv_write():
@@ -91,6 +106,16 @@ def test_rope_kv_write():
     close(q.cpu(), qr)
     close(kc.cpu(), kr)
     assert torch.equal(vc.cpu(), vr)
+    # the same through fp32 split-K slabs
+    slabs = torch.randn(3, T, (Hq + 2 * Hkv) * D, device=DEV)
+    kc2, vc2 = torch.zeros_like(kc), torch.zeros_like(vc)
+    kr2, vr2 = kc2.cpu(), vc2.cpu()
+    q2 = ops.rope_kv_write(slabs, pos, cs, kc2, vc2, slots, Hq, Hkv, D)
+    qr2 = ref.rope_kv_write(slabs.sum(0).to(torch.bfloat16).cpu(), pos.cpu(), cs.cpu(), kr2, vr2, slots.cpu(), Hq,
+                            Hkv, D, bs)
+    close(q2.cpu(), qr2)
+    close(kc2.cpu(), kr2)
+    assert torch.equal(vc2.cpu(), vr2)
 
 
 @pytest.mark.parametrize("D", [32, 64, 128])
@@ -166,6 +191,34 @@ def test_gemm_swiglu():
     w = ops.interleave_gate_up(wg, wu)
     got = ops.gemm_bt(x, w, epilogue=ops.EPI_SWIGLU)
     exp = ref.silu_mul(ref.gemm_bt(x, torch.cat([wg, wu], 0)))
+    close(got, exp, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (192, 1792, 7), (128, 4096, 16)])
+def test_skinny_gemm(M, N, K, S):
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    exp = ref.gemm_bt(x, w, out_f32=True)
+    if S == 1:
+        close(ops.skinny_gemm(x, w), exp.to(torch.bfloat16), atol=3e-2, rtol=2e-2)
+        res = bf(M, N)
+        close(ops.skinny_gemm(x, w, residual=res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
+    else:
+        slabs = ops.skinny_gemm(x, w, splits=S)
+        assert slabs.shape == (S, M, N)
+        close(slabs.sum(0), exp, atol=1e-2, rtol=1e-2)
+        res = bf(M, N)
+        close(ops.skinny_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [3, 64])
+def test_skinny_swiglu_and_strided_x(M):
+    F, K = 512, 1024
+    xs, wg, wu = bf(M, K + 64), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
+    x = xs[:, :K]  # row stride K + 64
+    w = ops.interleave_gate_up(wg, wu)
+    got = ops.skinny_gemm(x, w, epilogue=ops.EPI_SWIGLU)
+    exp = ref.silu_mul(ref.gemm_bt(x.contiguous(), torch.cat([wg, wu], 0)))
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 

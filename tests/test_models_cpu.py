@@ -143,3 +143,19 @@ def test_tensor_parallel_shards_reconstruct_full_model():
         got = got + (torch.nn.functional.silu(g[:, :f]) * g[:, f:]) @ shards[r]["l0.down_w"].t()
     assert torch.allclose(got, ref, atol=1e-4)
     assert math.isclose(sum(s["l0.qkv_w"].numel() for s in shards), full["l0.qkv_w"].numel())
+
+
+def test_llama_interleaved_mlp_layout_matches():
+    """16-row interleaved gate|up weights (fused SwiGLU layout) give the same model."""
+    from django_assistant_bot_amd.models.weights import _interleave16
+
+    cfg, full = _llama_pair(3)
+    inter = dict(full)
+    F = cfg.intermediate
+    for i in range(cfg.layers):
+        gu = full[f"l{i}.gate_up_w"]
+        inter[f"l{i}.gate_up_w"] = _interleave16(gu[:F], gu[F:])
+    ids = list(range(5, 40))
+    h_a, _ = _prefill(LlamaModel(cfg, full, "cpu"), cfg, ids)
+    h_b, _ = _prefill(LlamaModel(cfg, inter, "cpu", interleaved_mlp=True), cfg, ids)
+    assert torch.allclose(h_a, h_b, atol=1e-5)
