@@ -37,3 +37,5 @@ if "assistant.storage" in settings.INSTALLED_APPS:
     urlpatterns.append(path("api/v1/", include("assistant.storage.urls")))
 if "assistant.bot" in settings.INSTALLED_APPS:
     urlpatterns.append(path("api/v1/", include("assistant.bot.urls")))
+if "assistant.rag" in settings.INSTALLED_APPS:
+    urlpatterns.append(path("api/v1/", include("assistant.rag.urls")))

@@ -1,0 +1,213 @@
+"""gpu_service: embeddings, dialog, vector index and metrics over HTTP (reference gpu_service/main.py).
+
+Endpoints (request/response shapes of the reference where it had them):
+  POST /embeddings/             {model, texts}                         -> {embeddings: [[float]]}
+  POST /dialog/                 {model, messages, max_tokens, json_format} -> {response: AIResponse}
+  POST /index/{name}/upsert     {ids, vectors, doc_ids?, groups?}      -> {count}
+  POST /index/{name}/delete     {ids}                                  -> {removed}
+  POST /index/{name}/search     {queries, k, groups?, allowed?}        -> {ids, distances, doc_ids}
+  GET  /health                  loaded models, device
+  GET  /metrics                 Prometheus text (engine counters, queue depths, HBM use)
+
+Requests from all concurrent callers share the engine's batches (EmbedWorker / LLMWorker), so the
+service is one process per GPU (gunicorn_conf.py maps worker i -> device i).  Model names are
+case-insensitive; unknown model -> 400; engine errors -> 500.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import sys
+import threading
+from contextlib import asynccontextmanager
+from dataclasses import asdict
+from typing import Dict, List, Optional
+
+from fastapi import FastAPI, HTTPException
+from fastapi.responses import PlainTextResponse
+from pydantic import BaseModel
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+logging.basicConfig(level=os.environ.get("GPU_SERVICE_LOG_LEVEL", "INFO"),
+                    format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
+logger = logging.getLogger("gpu_service")
+
+
+class EmbeddingRequest(BaseModel):
+    model: str
+    texts: List[str]
+
+
+class Message(BaseModel):
+    role: str
+    content: str
+
+
+class DialogRequest(BaseModel):
+    model: str
+    messages: List[Message]
+    max_tokens: int = 1024
+    json_format: bool = False
+
+
+class UpsertRequest(BaseModel):
+    ids: List[int]
+    vectors: List[List[float]]
+    doc_ids: Optional[List[int]] = None
+    groups: Optional[List[int]] = None
+
+
+class DeleteRequest(BaseModel):
+    ids: List[int]
+
+
+class SearchRequest(BaseModel):
+    queries: List[List[float]]
+    k: int = 10
+    groups: Optional[List[int]] = None
+    allowed: Optional[List[List[int]]] = None
+
+
+embedders: Dict[str, object] = {}
+providers: Dict[str, object] = {}
+indexes: Dict[str, object] = {}
+_index_lock = threading.Lock()
+
+
+def load_models(embedder_names, provider_names):
+    from assistant.ai.embedders.transformers import TransformersEmbedder
+    from assistant.ai.providers.transformers import TransformersProvider
+
+    for name in embedder_names:
+        try:
+            embedders[name.lower()] = TransformersEmbedder(name)
+        except Exception:
+            logger.exception("failed to load embedder %s", name)
+    for name in provider_names:
+        try:
+            providers[name.lower()] = TransformersProvider(name)
+        except Exception:
+            logger.exception("failed to load provider %s", name)
+    logger.info("serving embedders=%s providers=%s", sorted(embedders), sorted(providers))
+
+
+@asynccontextmanager
+async def lifespan(app: FastAPI):
+    from gpu_service.models import embedder_models, provider_models
+
+    load_models(embedder_models, provider_models)
+    yield
+
+
+app = FastAPI(title="gpu_service", lifespan=lifespan)
+
+
+@app.post("/embeddings/")
+async def get_embeddings(request: EmbeddingRequest):
+    embedder = embedders.get(request.model.lower())
+    if embedder is None:
+        raise HTTPException(status_code=400, detail="Model is not supported")
+    try:
+        return {"embeddings": await embedder.embeddings(request.texts)}
+    except Exception as e:
+        logger.exception("embeddings failed")
+        raise HTTPException(status_code=500, detail=str(e))
+
+
+@app.post("/dialog/")
+async def get_response(request: DialogRequest):
+    provider = providers.get(request.model.lower())
+    if provider is None:
+        raise HTTPException(status_code=400, detail="Model is not supported")
+    try:
+        resp = await provider.get_response([{"role": m.role, "content": m.content} for m in request.messages],
+                                           max_tokens=request.max_tokens, json_format=request.json_format)
+        return {"response": asdict(resp)}
+    except Exception as e:
+        logger.exception("dialog failed")
+        raise HTTPException(status_code=500, detail=str(e))
+
+
+def _index(name: str, dim: Optional[int] = None, create: bool = False):
+    with _index_lock:
+        idx = indexes.get(name)
+        if idx is None and create:
+            from django_assistant_bot_amd.engine.serving import engine_device
+            from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+            idx = indexes[name] = VectorIndex(dim, device=engine_device())
+        return idx
+
+
+@app.post("/index/{name}/upsert")
+async def index_upsert(name: str, request: UpsertRequest):
+    if len(request.ids) != len(request.vectors):
+        raise HTTPException(status_code=400, detail="ids and vectors differ in length")
+    if not request.ids:
+        return {"count": len(indexes[name]) if name in indexes else 0}
+    idx = _index(name, dim=len(request.vectors[0]), create=True)
+    if len(request.vectors[0]) != idx.dim:
+        raise HTTPException(status_code=400, detail=f"index {name} has dim {idx.dim}")
+    with _index_lock:
+        idx.add(request.ids, request.vectors, doc_ids=request.doc_ids, groups=request.groups)
+        return {"count": len(idx)}
+
+
+@app.post("/index/{name}/delete")
+async def index_delete(name: str, request: DeleteRequest):
+    idx = _index(name)
+    if idx is None:
+        return {"removed": 0}
+    with _index_lock:
+        return {"removed": idx.remove(request.ids)}
+
+
+@app.post("/index/{name}/search")
+async def index_search(name: str, request: SearchRequest):
+    idx = _index(name)
+    nq = len(request.queries)
+    if idx is None or len(idx) == 0 or nq == 0:
+        return {"ids": [[] for _ in range(nq)], "distances": [[] for _ in range(nq)],
+                "doc_ids": [[] for _ in range(nq)]}
+    with _index_lock:
+        sims, ids, docs = idx.search(request.queries, request.k, q_groups=request.groups, allowed=request.allowed)
+    out_ids, out_d, out_docs = [], [], []
+    for s, i, d in zip(sims.tolist(), ids.tolist(), docs.tolist()):
+        keep = [j for j, x in enumerate(i) if x >= 0]
+        out_ids.append([i[j] for j in keep])
+        out_d.append([1.0 - s[j] for j in keep])
+        out_docs.append([d[j] for j in keep])
+    return {"ids": out_ids, "distances": out_d, "doc_ids": out_docs}
+
+
+@app.get("/health")
+async def health():
+    from django_assistant_bot_amd.engine.serving import engine_device
+
+    return {"status": "ok", "device": str(engine_device()), "embedders": sorted(embedders),
+            "providers": sorted(providers), "indexes": {k: len(v) for k, v in indexes.items()}}
+
+
+def _flatten(prefix: str, obj, out: list, labels: str = ""):
+    if isinstance(obj, dict):
+        for k, v in obj.items():
+            if isinstance(v, dict) and k in ("embedders", "providers"):
+                for model, stats in v.items():
+                    _flatten(f"{prefix}_{k[:-1]}", stats, out, f'model="{model}"')
+            else:
+                _flatten(f"{prefix}_{k}", v, out, labels)
+    elif isinstance(obj, (int, float)) and not isinstance(obj, bool):
+        out.append(f"{prefix}{{{labels}}} {float(obj)}" if labels else f"{prefix} {float(obj)}")
+
+
+@app.get("/metrics", response_class=PlainTextResponse)
+async def metrics():
+    from django_assistant_bot_amd.engine.serving import engine_metrics
+
+    lines: list = []
+    _flatten("dab", engine_metrics(), lines)
+    lines += [f'dab_index_rows{{index="{k}"}} {float(len(v))}' for k, v in indexes.items()]
+    return "\n".join(lines) + "\n"

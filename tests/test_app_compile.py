@@ -7,7 +7,7 @@ import py_compile
 import pytest
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
-APP_FILES = sorted(p for p in (ROOT / "assistant").rglob("*.py"))
+APP_FILES = sorted(p for d in ("assistant", "gpu_service", "example") for p in (ROOT / d).rglob("*.py"))
 
 
 @pytest.mark.parametrize("path", APP_FILES, ids=lambda p: str(p.relative_to(ROOT)))
@@ -22,7 +22,9 @@ DJANGO_FREE = [
     "assistant.bot.selfplay", "assistant.bot.tasks", "assistant.bot.services.answer_service",
     "assistant.bot.platforms.telegram.platform", "assistant.bot.platforms.console", "assistant.bot.platforms.api",
     "assistant.bot.chat_completion", "assistant.rag.knowledge", "assistant.rag.aggregation",
-    "assistant.assistant.queue",
+    "assistant.assistant.queue", "assistant.processing.utils", "assistant.processing.repository",
+    "assistant.processing.wiki", "assistant.processing.documents.processor", "assistant.broadcasting.core",
+    "assistant.loading.csv_loader", "assistant.loading.csv", "gpu_service.main", "gpu_service.models",
 ]
 
 

@@ -1,0 +1,62 @@
+"""gpu_service HTTP API on CPU with the tiny engine presets (FastAPI TestClient): embeddings, dialog,
+vector-index upsert/search/delete, health and Prometheus metrics; error codes of the reference
+(400 unknown model)."""
+import pytest
+
+fastapi = pytest.importorskip("fastapi")
+from fastapi.testclient import TestClient  # noqa: E402
+
+from gpu_service import main as svc  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def client():
+    svc.embedders.clear()
+    svc.providers.clear()
+    svc.indexes.clear()
+    svc.load_models(["tiny-bert"], ["tiny-llama"])
+    app = svc.FastAPI()  # no lifespan: models loaded above
+    for r in svc.app.routes:
+        app.router.routes.append(r)
+    return TestClient(app)
+
+
+def test_embeddings(client):
+    r = client.post("/embeddings/", json={"model": "TINY-BERT", "texts": ["hello world", "привет мир"]})
+    assert r.status_code == 200
+    e = r.json()["embeddings"]
+    assert len(e) == 2 and len(e[0]) == 128
+    assert client.post("/embeddings/", json={"model": "nope", "texts": ["x"]}).status_code == 400
+
+
+def test_dialog(client):
+    r = client.post("/dialog/", json={"model": "tiny-llama", "messages": [{"role": "user", "content": "hi"}],
+                                      "max_tokens": 5})
+    assert r.status_code == 200
+    resp = r.json()["response"]
+    assert resp["usage"]["completion_tokens"] <= 5 and isinstance(resp["result"], str)
+    assert resp["length_limited"] in (True, False)
+    assert client.post("/dialog/", json={"model": "x", "messages": []}).status_code == 400
+
+
+def test_index_roundtrip(client):
+    vecs = [[1.0, 0.0, 0.0, 0.0], [0.0, 1.0, 0.0, 0.0], [0.7, 0.7, 0.0, 0.0]]
+    r = client.post("/index/q/upsert", json={"ids": [10, 11, 12], "vectors": vecs, "doc_ids": [1, 2, 3]})
+    assert r.json() == {"count": 3}
+    r = client.post("/index/q/search", json={"queries": [[1.0, 0.1, 0.0, 0.0]], "k": 2}).json()
+    assert r["ids"][0] == [10, 12] and r["doc_ids"][0] == [1, 3]
+    assert r["distances"][0][0] < r["distances"][0][1]
+    r = client.post("/index/q/search", json={"queries": [[1.0, 0.1, 0.0, 0.0]], "k": 3, "allowed": [[11, 12]]}).json()
+    assert r["ids"][0] == [12, 11]
+    assert client.post("/index/q/delete", json={"ids": [12]}).json() == {"removed": 1}
+    r = client.post("/index/q/search", json={"queries": [[1.0, 0.1, 0.0, 0.0]], "k": 3}).json()
+    assert r["ids"][0] == [10, 11]
+    assert client.post("/index/none/search", json={"queries": [[1, 0, 0, 0]], "k": 3}).json()["ids"] == [[]]
+
+
+def test_health_and_metrics(client):
+    h = client.get("/health").json()
+    assert h["status"] == "ok" and "tiny-bert" in h["embedders"] and "tiny-llama" in h["providers"]
+    m = client.get("/metrics").text
+    assert 'dab_embedder_requests{model="tiny-bert"}' in m
+    assert 'dab_provider_requests{model="tiny-llama"}' in m
