@@ -101,6 +101,7 @@ def main():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--kv-gb", type=float, default=None)
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size (groups of consecutive ranks)")
     args = ap.parse_args()
 
     from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
@@ -112,6 +113,10 @@ def main():
     info = pdist.init()
     dev = info.device
     W, R = info.world_size, info.rank
+    tp_group, tp_rank, rep = pdist.tp_groups(args.tp)
+    if args.tp > 1:
+        rep = R // args.tp  # DP replica index (consecutive ranks form a TP group)
+    n_rep = W // max(1, args.tp)
     if W != args.gpus and R == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={W}", file=sys.stderr)
     torch.manual_seed(args.seed + R)
@@ -120,9 +125,9 @@ def main():
 
     t_setup = time.perf_counter()
     embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
-    llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * R, max_batch=B, max_model_len=4096,
+    llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
                     use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb,
-                    max_prefill_tokens=32768)
+                    max_prefill_tokens=32768, tp_group=tp_group, tp_size=args.tp, tp_rank=tp_rank)
     # ---- synthetic corpus: index rows (questions) grouped into documents
     n_rows = args.index_rows
     n_docs = max(1, n_rows // args.rows_per_doc)
@@ -138,7 +143,7 @@ def main():
     # ---- questions of every rank / step (deterministic), embedded once to plant relevant rows
     qrng = np.random.default_rng(args.seed + 12345)
     all_q = [[[synth_text(qrng, int(qrng.integers(8, 16))) + "?" for _ in range(B)] for _ in range(n_steps)]
-             for _ in range(W)]
+             for _ in range(n_rep)]
     flat_q = [q for r in all_q for s in r for q in s]
     q_emb = torch.nn.functional.normalize(embedder.embed(flat_q).float(), dim=-1)
     # Random-init encoders embed every question into a narrow cone (pairwise cos ~0.96), so rows
@@ -181,7 +186,7 @@ def main():
                 torch.cuda.synchronize(dev)
             stats0 = dict(llm.stats)
             t0 = time.perf_counter()
-        res = rag.answer(all_q[R][step], params, bot_group=0)
+        res = rag.answer(all_q[rep][step], params, bot_group=0)
         if step >= args.warmup:
             latencies += [r.latency_s for r in res]
             prompt_lens += [r.usage["prompt_tokens"] for r in res]
@@ -192,7 +197,7 @@ def main():
     elapsed = pdist.max_over_ranks(time.perf_counter() - t0, dev)
     p50 = float(np.median(latencies)) if latencies else float("nan")
     p50 = pdist.max_over_ranks(p50, dev)
-    total_q = W * B * args.steps
+    total_q = n_rep * B * args.steps
     eng = {k: round(v - stats0.get(k, 0), 3) if isinstance(v, float) else v - stats0.get(k, 0)
            for k, v in llm.stats.items()}
     qps = total_q / elapsed
@@ -212,10 +217,10 @@ def main():
         "p50_latency_ms": round(1000 * p50, 1),
         "config": {
             "model": f"{args.embed_model} + {args.llm_model}",
-            "global_batch": W * B,
+            "global_batch": n_rep * B,
             "seq_len": int(np.mean(prompt_lens)) if prompt_lens else 0,
             "max_new_tokens": args.max_new_tokens,
-            "parallelism": f"dp{W}",
+            "parallelism": f"dp{n_rep}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
             "index_rows": n_rows,
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",

@@ -1,0 +1,121 @@
+"""Multi-process (gloo, world_size 2, CPU) checks of the distributed paths: tensor-parallel Llama
+forward == the unsharded model, ShardedIndex search == a single index, DP corpus embedding == a
+single-rank embedding.  The same code runs over RCCL on GPUs (backend chosen by parallel.dist.init)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+WORLD = 2
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, *args):
+    port = _free_port()
+    mp.spawn(_entry, args=(fn, port) + args, nprocs=WORLD, join=True)
+
+
+def _entry(rank, fn, port, *args):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from django_assistant_bot_amd.parallel import dist as pdist
+
+    info = pdist.init(backend="gloo", device_type="cpu")
+    try:
+        fn(info, *args)
+    finally:
+        pdist.shutdown()
+
+
+def _tp_body(info, out_path):
+    from django_assistant_bot_amd.models.configs import decoder_config
+    from django_assistant_bot_amd.models.llama import AttnMeta, KVCache, LlamaModel
+    from django_assistant_bot_amd.models.weights import random_decoder_weights, shard_decoder_weights
+    from django_assistant_bot_amd.parallel import dist as pdist
+
+    cfg = decoder_config("tiny-llama")
+    full = random_decoder_weights(cfg, dtype=torch.float32, seed=11)
+    group, tp_rank, _ = pdist.tp_groups(WORLD)
+    shard = shard_decoder_weights(full, cfg, tp_rank, WORLD)
+    model = LlamaModel(cfg, shard, "cpu", tp_group=group, tp_size=WORLD)
+    ids = torch.arange(5, 45, dtype=torch.int32)
+    T = ids.numel()
+    kv = KVCache(cfg.layers, 4, cfg.kv_heads // WORLD, 64, cfg.head_dim, "cpu", dtype=torch.float32)
+    meta = AttnMeta(decode=False, positions=torch.arange(T, dtype=torch.int32), slots=torch.arange(T),
+                    block_tables=torch.arange(4, dtype=torch.int32)[None], ctx_lens=torch.tensor([T], dtype=torch.int32),
+                    cu_q=torch.tensor([0, T], dtype=torch.int32), max_q=T)
+    h = model.forward(ids, meta, kv)
+    if info.rank == 0:
+        ref_model = LlamaModel(cfg, full, "cpu")
+        kv2 = KVCache(cfg.layers, 4, cfg.kv_heads, 64, cfg.head_dim, "cpu", dtype=torch.float32)
+        ref = ref_model.forward(ids, meta, kv2)
+        torch.save({"err": (h - ref).abs().max().item()}, out_path)
+
+
+def test_tensor_parallel_forward_matches_full_model(tmp_path):
+    out = str(tmp_path / "tp.pt")
+    _run(_tp_body, out)
+    assert torch.load(out, weights_only=True)["err"] < 1e-4
+
+
+def _index_body(info, out_path):
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    g = torch.Generator().manual_seed(3)
+    n, dim = 3000, 32
+    vecs = torch.randn(n, dim, generator=g)
+    ids = np.arange(100, 100 + n)
+    docs = ids // 7
+    idx = ShardedIndex(dim, "cpu")
+    idx.add(ids, vecs, doc_ids=docs)
+    assert len(idx) == n
+    q = torch.randn(3 + info.rank, dim, generator=torch.Generator().manual_seed(50 + info.rank))
+    sims, got_ids, got_docs = idx.search(q, 25)
+    single = VectorIndex(dim, "cpu")
+    single.add(ids, vecs, doc_ids=docs)
+    es, eids, edocs = single.search(q, 25)
+    res = {"ids_equal": bool(torch.equal(got_ids, eids)), "docs_equal": bool(torch.equal(got_docs, edocs)),
+           "sims_err": float((sims - es).abs().max())}
+    torch.save(res, out_path + f".{info.rank}")
+
+
+def test_sharded_index_matches_single_index(tmp_path):
+    out = str(tmp_path / "idx.pt")
+    _run(_index_body, out)
+    for r in range(WORLD):
+        res = torch.load(out + f".{r}", weights_only=True)
+        assert res["ids_equal"] and res["docs_equal"] and res["sims_err"] < 1e-5
+
+
+def _dp_embed_body(info, out_path):
+    from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
+    from django_assistant_bot_amd.parallel.dp_embed import embed_corpus
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    eng = EmbeddingEngine("tiny-bert", "cpu", seed=2)
+    texts = [f"document number {i} about topic {i % 7}" for i in range(37)]
+    idx = ShardedIndex(eng.dim, "cpu")
+    ids, full, total = embed_corpus(eng, lambda i: texts[i], len(texts), info.rank, info.world_size, index=idx,
+                                    gather=True)
+    assert total == 37 and len(idx) == 37 and len(idx.local) == len(ids)
+    if info.rank == 0:
+        ref = EmbeddingEngine("tiny-bert", "cpu", seed=2).embed(texts)
+        torch.save({"err": float((full - ref).abs().max())}, out_path)
+
+
+def test_dp_corpus_embedding_matches_single_rank(tmp_path):
+    out = str(tmp_path / "dp.pt")
+    _run(_dp_embed_body, out)
+    assert torch.load(out, weights_only=True)["err"] < 1e-5
