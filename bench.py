@@ -179,6 +179,7 @@ def main():
     setup_s = time.perf_counter() - t_setup
 
     latencies, prompt_lens, n_docs_used = [], [], []
+    phases = {"retrieve_s": [], "prompt_s": [], "generate_s": []}
     for step in range(n_steps):
         if step == args.warmup:
             pdist.barrier(info)
@@ -191,6 +192,9 @@ def main():
             latencies += [r.latency_s for r in res]
             prompt_lens += [r.usage["prompt_tokens"] for r in res]
             n_docs_used += [len(r.documents) for r in res]
+            phases["retrieve_s"].append(res[0].debug_info["took"])
+            phases["prompt_s"].append(res[0].debug_info["prompt"]["took"])
+            phases["generate_s"].append(max(r.debug_info["final"]["took"] for r in res))
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     pdist.barrier(info)
@@ -229,6 +233,7 @@ def main():
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
             "engine_rank0": eng,
+            "phases_rank0_s": {k: round(float(np.mean(v)), 4) for k, v in phases.items() if v},
         },
     }
     if R == 0:

@@ -46,13 +46,17 @@ def main():
 
     # warm-up (kernels, allocator) on a disjoint id range
     embed_corpus(eng, text_of, args.warmup_chunks, info.rank, info.world_size, first_id=10**9)
+    # synthetic corpus materialised before timing (generating random text is not ingest work;
+    # tokenisation is, and stays inside the timed region)
+    from django_assistant_bot_amd.parallel.dp_embed import owned_ids
+    corpus = {int(i): text_of(int(i)) for i in owned_ids(args.chunks, info.rank, info.world_size)}
     index = ShardedIndex(eng.dim, info.device, capacity=args.chunks // max(1, info.world_size) + 1024)
     pdist.barrier(info)
     if info.device.type == "cuda":
         torch.cuda.synchronize()
     tok0 = eng.stats["tokens"]
     t0 = time.perf_counter()
-    _, _, total = embed_corpus(eng, text_of, args.chunks, info.rank, info.world_size, index=index,
+    _, _, total = embed_corpus(eng, corpus.__getitem__, args.chunks, info.rank, info.world_size, index=index,
                                doc_of=lambda ids: ids // 10)
     if info.device.type == "cuda":
         torch.cuda.synchronize()

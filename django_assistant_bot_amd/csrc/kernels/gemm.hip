@@ -39,11 +39,14 @@ struct GemmParams {
 
 __device__ __forceinline__ int gsw(int r) { return 2 * ((r >> 1) & 3); }
 
-template <int EPI>
-__global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
-  constexpr int BM = 128, BN = 128, BK = 64;
-  constexpr int TILE = BM * BK * 2;  // bytes per operand tile
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE];  // [buf][A|B]
+template <int EPI, int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
+  constexpr int BK = 64;
+  constexpr int NW = WGM * WGN;            // waves
+  constexpr int TM = BM / WGM, TN = BN / WGN;  // per-wave tile
+  constexpr int MI = TM / 16, NI = TN / 16;    // MFMA tiles per wave
+  constexpr int TILE_A = BM * BK * 2, TILE_B = BN * BK * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (TILE_A + TILE_B)];  // [buf][A|B]
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
@@ -56,33 +59,37 @@ __global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WGN, wn = w % WGN;
 
-  // staging: wave w, instruction c writes LDS bytes [(c*4+w)*1024, +1024) of a tile = rows 8(c*4+w)..+7
+  // staging: instruction c of wave w writes LDS bytes [(c*NW+w)*1024, +1024) of a tile = rows 8(c*NW+w)..+7
   auto stage = [&](int buf, int k0) {
-    char* As = smem + buf * 2 * TILE;
-    char* Bs = As + TILE;
+    char* As = smem + buf * (TILE_A + TILE_B);
+    char* Bs = As + TILE_A;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const int e = (c * 4 + w) * 64 + lane;
+    for (int c = 0; c < BM / (8 * NW); ++c) {
+      const int e = (c * NW + w) * 64 + lane;
       const int r = e >> 3, pos = e & 7;
-      const int src_chunk = pos ^ gsw(r);
       const int ra = min(m0 + r, p.M - 1);
+      const bf16* ga = p.A + (size_t)ra * p.lda + k0 + (pos ^ gsw(r)) * 8;
+      __builtin_amdgcn_global_load_lds((const void*)ga,
+                                       (__attribute__((address_space(3))) void*)(As + (c * NW + w) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int c = 0; c < BN / (8 * NW); ++c) {
+      const int e = (c * NW + w) * 64 + lane;
+      const int r = e >> 3, pos = e & 7;
       const int rb = min(n0 + r, p.N - 1);
-      const bf16* ga = p.A + (size_t)ra * p.lda + k0 + src_chunk * 8;
-      const bf16* gb = p.B + (size_t)rb * p.ldb + k0 + src_chunk * 8;
-      __builtin_amdgcn_global_load_lds((const void*)ga, (__attribute__((address_space(3))) void*)(As + (c * 4 + w) * 1024),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const void*)gb, (__attribute__((address_space(3))) void*)(Bs + (c * 4 + w) * 1024),
-                                       16, 0, 0);
+      const bf16* gb = p.B + (size_t)rb * p.ldb + k0 + (pos ^ gsw(r)) * 8;
+      __builtin_amdgcn_global_load_lds((const void*)gb,
+                                       (__attribute__((address_space(3))) void*)(Bs + (c * NW + w) * 1024), 16, 0, 0);
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[NI][MI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < MI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = p.K / BK;
   stage(0, 0);
@@ -90,39 +97,42 @@ __global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
-    const char* As = smem + (kt & 1) * 2 * TILE;
-    const char* Bs = As + TILE;
+    const char* As = smem + (kt & 1) * (TILE_A + TILE_B);
+    const char* Bs = As + TILE_A;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[MI], bfr[NI];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ra = wm * 64 + 16 * i + li;
+      for (int i = 0; i < MI; ++i) {
+        const int ra = wm * TM + 16 * i + li;
         af[i] = *reinterpret_cast<const bf16x8*>(As + ra * 128 + 16 * ((4 * ks + g) ^ gsw(ra)));
-        const int rb = wn * 64 + 16 * i + li;
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int rb = wn * TN + 16 * i + li;
         bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + 16 * ((4 * ks + g) ^ gsw(rb)));
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni)
+      for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
-        for (int mi = 0; mi < 4; ++mi) acc[ni][mi] = mfma16(bfr[ni], af[mi], acc[ni][mi]);
+        for (int mi = 0; mi < MI; ++mi) acc[ni][mi] = mfma16(bfr[ni], af[mi], acc[ni][mi]);
       __builtin_amdgcn_s_setprio(0);
     }
   }
 
-  // epilogue: acc[ni][mi][r] = C[m = m0 + wm*64 + 16 mi + li][n = n0 + wn*64 + 16 ni + 4 g + r]
+  // epilogue: acc[ni][mi][r] = C[m = m0 + wm*TM + 16 mi + li][n = n0 + wn*TN + 16 ni + 4 g + r]
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
-    const int m = m0 + wm * 64 + 16 * mi + li;
+  for (int mi = 0; mi < MI; ++mi) {
+    const int m = m0 + wm * TM + 16 * mi + li;
     if (m >= p.M) continue;
     if (EPI == EPI_SWIGLU) {
       // weight rows interleaved in 16-row groups [gate 16 | up 16]: ni even = gate, ni odd = up
 #pragma unroll
-      for (int pi = 0; pi < 2; ++pi) {
-        const int ng = n0 + wn * 64 + 32 * pi + 4 * g;  // gate column in the interleaved space
+      for (int pi = 0; pi < NI / 2; ++pi) {
+        const int ng = n0 + wn * TN + 32 * pi + 4 * g;  // gate column in the interleaved space
         if (ng >= p.N) continue;
-        const int oc = (n0 + wn * 64) / 2 + 16 * pi + 4 * g;
+        const int oc = (n0 + wn * TN) / 2 + 16 * pi + 4 * g;
         float o[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -141,8 +151,8 @@ __global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
       continue;
     }
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) {
-      const int n = n0 + wn * 64 + 16 * ni + 4 * g;
+    for (int ni = 0; ni < NI; ++ni) {
+      const int n = n0 + wn * TN + 16 * ni + 4 * g;
       if (n >= p.N) continue;  // N % 4 == 0 is required by the launcher
       float o[4];
 #pragma unroll
@@ -186,6 +196,18 @@ __global__ __launch_bounds__(256) void gemm_bt_kernel(GemmParams p) {
   }
 }
 
+template <int EPI>
+static int launch_gemm(const GemmParams& p, bool big, hipStream_t s) {
+  if (big) {
+    const int nwg = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 256, 256, 2, 4>), dim3(nwg), dim3(512), 0, s, p);
+  } else {
+    const int nwg = ((p.M + 127) / 128) * ((p.N + 127) / 128);
+    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 128, 128, 2, 2>), dim3(nwg), dim3(256), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
             const uint32_t* allow, int allow_words, hipStream_t s) {
@@ -210,15 +232,16 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   p.ldr = ldr;
   p.allow_words = allow_words;
   p.out_f32 = out_f32;
-  const int nwg = ((M + 127) / 128) * ((N + 127) / 128);
+  // large problems: 256x256 tiles, 8 waves of 128x64 (half the LDS fragment traffic per MFMA of the
+  // 64x64 wave tile); small M or N: 128x128 tiles, 4 waves (less padding, more workgroups)
+  const bool big = M >= 2048 && N >= 512 && ((long)((M + 255) / 256) * ((N + 255) / 256)) >= 160;
   switch (epilogue) {
-    case EPI_NONE: hipLaunchKernelGGL(gemm_bt_kernel<EPI_NONE>, dim3(nwg), dim3(256), 0, s, p); break;
-    case EPI_GELU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_GELU>, dim3(nwg), dim3(256), 0, s, p); break;
-    case EPI_SWIGLU: hipLaunchKernelGGL(gemm_bt_kernel<EPI_SWIGLU>, dim3(nwg), dim3(256), 0, s, p); break;
-    case EPI_SCORES: hipLaunchKernelGGL(gemm_bt_kernel<EPI_SCORES>, dim3(nwg), dim3(256), 0, s, p); break;
+    case EPI_NONE: return launch_gemm<EPI_NONE>(p, big, s);
+    case EPI_GELU: return launch_gemm<EPI_GELU>(p, big, s);
+    case EPI_SWIGLU: return launch_gemm<EPI_SWIGLU>(p, big, s);
+    case EPI_SCORES: return launch_gemm<EPI_SCORES>(p, big, s);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 }  // namespace dab

@@ -62,16 +62,19 @@ class BertEncoder:
         T = ids.numel()
         x = ops.bert_embed(ids, pos_ids, None, self.word, self.pos, self.typ, self.eln_g, self.eln_b, cfg.eps)
         for L in self.layers:
-            qkv = ops.linear(x, L.qkv_w, L.qkv_b, use_native=True)
+            # plain projections on hipBLASLt (bias in its epilogue); residual adds fused into the native
+            # LayerNorm; the up projection keeps bias+GELU(erf) fused in the native MFMA GEMM
+            # (measured per shape at 32k tokens: benchmarks/kernel_bench.py, profiles/)
+            qkv = ops.linear(x, L.qkv_w, L.qkv_b)
             q = qkv[:, :H].view(T, nh, D)
             k = qkv[:, H:2 * H].view(T, nh, D)
             v = qkv[:, 2 * H:].view(T, nh, D)
             a = ops.flash_attention_packed(q, k, v, cu_seqlens, cu_seqlens, max_seqlen, causal=False)
-            h = ops.linear(a.view(T, H), L.o_w, L.o_b, residual=x)
-            x = ops.layernorm(h, L.ln1_g, L.ln1_b, cfg.eps)
+            h = ops.linear(a.view(T, H), L.o_w, L.o_b)
+            x = ops.layernorm(h, L.ln1_g, L.ln1_b, cfg.eps, residual=x)
             f = ops.linear(x, L.i_w, L.i_b, act="gelu")
-            h = ops.linear(f, L.d_w, L.d_b, residual=x)
-            x = ops.layernorm(h, L.ln2_g, L.ln2_b, cfg.eps)
+            h = ops.linear(f, L.d_w, L.d_b)
+            x = ops.layernorm(h, L.ln2_g, L.ln2_b, cfg.eps, residual=x)
         return x
 
     def encode(self, ids, pos_ids, cu_seqlens, max_seqlen, normalize=None, want_bf16=False):

@@ -185,6 +185,20 @@ def test_gemm_epilogues(M, N, K):
     close(ops.gemm_bt(A, B, out_f32=True), ref.gemm_bt(A, B, out_f32=True), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(4100, 3136, 768), (8192, 2304, 256)])
+def test_gemm_big_tiles(M, N, K):
+    """256x256 / 8-wave path (large M and N), incl. ragged edges."""
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    bias, res = bf(N), bf(M, N)
+    close(ops.gemm_bt(A, B, bias, res), ref.gemm_bt(A, B, bias, res), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, bias, None, ops.EPI_GELU), ref.gemm_bt(A, B, bias, None, ops.EPI_GELU), atol=3e-2,
+          rtol=2e-2)
+    x, wg, wu = bf(M, K), bf(N // 2 // 16 * 16, K, scale=0.05), bf(N // 2 // 16 * 16, K, scale=0.05)
+    w = ops.interleave_gate_up(wg, wu)
+    close(ops.gemm_bt(x, w, epilogue=ops.EPI_SWIGLU), ref.silu_mul(ref.gemm_bt(x, torch.cat([wg, wu], 0))),
+          atol=3e-2, rtol=3e-2)
+
+
 def test_gemm_swiglu():
     M, F, K = 77, 256, 512
     x, wg, wu = bf(M, K), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
@@ -222,12 +236,13 @@ def test_skinny_swiglu_and_strided_x(M):
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 
-def test_gemm_scores_masks():
-    Q, N, K = 5, 3000, 768
+@pytest.mark.parametrize("Q,N", [(5, 3000), (2048, 100004)])
+def test_gemm_scores_masks(Q, N):
+    K = 768
     q = torch.nn.functional.normalize(torch.randn(Q, K, device=DEV), dim=-1).to(torch.bfloat16)
     x = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
     rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
-    qg = torch.tensor([-1, 0, 1, 2, 0], device=DEV, dtype=torch.int32)
+    qg = torch.tensor([-1, 0, 1, 2, 0] * (Q // 5) + [-1] * (Q % 5), device=DEV, dtype=torch.int32)
     allow = torch.randint(-2 ** 31, 2 ** 31 - 1, (Q, (N + 31) // 32), device=DEV, dtype=torch.int32)
     got = ops.gemm_bt(q, x, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg, allow=allow)
     exp = ref.gemm_bt(q, x, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg, allow=allow)
