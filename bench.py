@@ -1,22 +1,31 @@
 #!/usr/bin/env python
 """Headline benchmark: RAG queries/sec + p50 end-to-end latency, bge-base + Llama-3-8B (BASELINE.json).
 
-One "step" = a batch of B user questions per GPU answered end to end through the engine's RAG path
-(``django_assistant_bot_amd.engine.rag.RAGPipeline``, the batched mirror of the reference's
-ContextService -> ChatCompletion chain):
+Every question goes through the engine's RAG path (``django_assistant_bot_amd.engine.rag.RAGPipeline``,
+the batched mirror of the reference's ContextService -> ChatCompletion chain):
 
     bge-base query embedding (native encoder kernels)
-    -> exact top-250 question search over a 1M-row in-HBM index (fused MFMA score GEMM + radix top-k;
-       sharded across the ranks with all-gather merge when N > 1)
+    -> exact top-250 question search over a 1M-row in-HBM index (fused MFMA score GEMM + radix top-k)
     -> per-document aggregation (max_scores_n=5, top_n=5) -> FillInfo (<= 3 docs, 15 % of 8000)
     -> FinalPrompt -> Llama-3-8B generation of a fixed number of tokens (ignore_eos) with the
        reference's sampling (temperature 1, top_k 50, top_p 0.95), continuous batching + paged KV +
        HIP-graph decode.
 
+Two load shapes (``--mode``):
+
+  * ``serve`` (default) -- a bot's real traffic: questions keep arriving.  Closed loop at a fixed
+    concurrency C (= ``--batch``) per GPU: whenever ``--admit-group`` slots are free, that many new
+    questions are retrieved and queued; their prompt chunks ride along inside the running decode
+    steps (``LLMEngine`` mixed steps).  Arrivals are staggered over the first generation length so
+    the load is in steady state; one "step" = C completed questions (warmup steps are not timed).
+    The index is replicated per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
+  * ``batch`` -- one step = a batch of C questions answered together (retrieve all, prefill all,
+    decode all); the index is sharded across the ranks with an all-gather merge.
+
 Weights are random-init with the real architectures; corpus / questions are synthetic: each
 question has planted "paraphrase" rows near its embedding in 3-5 target documents so retrieval
-returns real documents and prompts have realistic length (~1k tokens).  Every rank uses TP=1
-(DP replicas; "scaling": weak -- per-GPU batch fixed).
+returns real documents and prompts have realistic length (~1k tokens).  Every rank runs TP=1 by
+default (DP replicas; "scaling": weak -- per-GPU load fixed).
 
     python bench.py --gpus N --steps K --warmup W      (N > 1 under torch.distributed.run)
 """
@@ -90,8 +99,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--mode", choices=("serve", "batch"), default="serve")
     ap.add_argument("--batch", type=int, default=128,
-                    help="questions per GPU per step (128: +24%% QPS over 64 at p50 4.0 s vs 2.5 s, profiles/)")
+                    help="questions in flight per GPU (serve) / per batch (batch); one step = this many answers")
+    ap.add_argument("--admit-group", type=int, default=16, help="serve: questions retrieved + queued together")
+    ap.add_argument("--mixed-tokens", type=int, default=2048,
+                    help="serve: prompt tokens mixed into one decode step (0: separate prefill steps)")
     ap.add_argument("--max-new-tokens", type=int, default=256)
     ap.add_argument("--index-rows", type=int, default=1_000_000, help="question rows in the whole (sharded) index")
     ap.add_argument("--rows-per-doc", type=int, default=10)
@@ -107,6 +120,7 @@ def main():
     from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
     from django_assistant_bot_amd.engine.rag import RAGPipeline
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
     from django_assistant_bot_amd.parallel import dist as pdist
     from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
 
@@ -123,29 +137,43 @@ def main():
     B = args.batch
     n_steps = args.warmup + args.steps
 
+    serve = args.mode == "serve"
+    G = max(1, min(args.admit_group, B))
+    if serve:
+        # questions answered in the timed window + the ones still in flight at both ends
+        n_questions = n_steps * B + 2 * B
+    else:
+        n_questions = n_steps * B
+
     t_setup = time.perf_counter()
     embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
     llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
-                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb,
-                    max_prefill_tokens=32768, tp_group=tp_group, tp_size=args.tp, tp_rank=tp_rank)
+                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb, max_prefill_tokens=32768,
+                    mixed_prefill_tokens=args.mixed_tokens if serve else 0, tp_group=tp_group, tp_size=args.tp,
+                    tp_rank=tp_rank)
     # ---- synthetic corpus: index rows (questions) grouped into documents
     n_rows = args.index_rows
     n_docs = max(1, n_rows // args.rows_per_doc)
     docs = SyntheticDocuments(n_docs, args.seed)
-    index = ShardedIndex(embedder.dim, dev)
-    gen = torch.Generator(device=dev).manual_seed(args.seed * 31 + R)
+    if serve:  # replicated: every rank holds all rows (identical generator), no collective per search
+        index = VectorIndex(embedder.dim, dev)
+        gen = torch.Generator(device=dev).manual_seed(args.seed * 31)
+        my_ids = np.arange(n_rows, dtype=np.int64)
+    else:
+        index = ShardedIndex(embedder.dim, dev)
+        gen = torch.Generator(device=dev).manual_seed(args.seed * 31 + R)
+        my_ids = np.arange(R, n_rows, W, dtype=np.int64)
     chunk = 1 << 18
-    my_ids = np.arange(R, n_rows, W, dtype=np.int64)
     for s in range(0, len(my_ids), chunk):
         ids = my_ids[s:s + chunk]
         v = torch.randn((len(ids), embedder.dim), device=dev, generator=gen)
         index.add(ids, v, doc_ids=ids // args.rows_per_doc, groups=np.zeros(len(ids), dtype=np.int32))
-    # ---- questions of every rank / step (deterministic), embedded once to plant relevant rows
+    # ---- questions of every replica (deterministic), embedded once to plant relevant rows
     qrng = np.random.default_rng(args.seed + 12345)
-    all_q = [[[synth_text(qrng, int(qrng.integers(8, 16))) + "?" for _ in range(B)] for _ in range(n_steps)]
-             for _ in range(n_rep)]
-    flat_q = [q for r in all_q for s in r for q in s]
-    q_emb = torch.nn.functional.normalize(embedder.embed(flat_q).float(), dim=-1)
+    all_q = [[synth_text(qrng, int(qrng.integers(8, 16))) + "?" for _ in range(n_questions)] for _ in range(n_rep)]
+    flat_q = [q for r in all_q for q in r]
+    q_emb = torch.cat([embedder.embed(flat_q[i:i + 4096]).float() for i in range(0, len(flat_q), 4096)])
+    q_emb = torch.nn.functional.normalize(q_emb, dim=-1)
     # Random-init encoders embed every question into a narrow cone (pairwise cos ~0.96), so rows
     # planted at q + noise would also match the OTHER questions and the hit lists would depend on how
     # many questions were planted (i.e. on --batch).  Planting along each question's own component
@@ -178,29 +206,62 @@ def main():
         torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
 
+    def sync_start():
+        pdist.barrier(info)
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        return dict(llm.stats), time.perf_counter()
+
     latencies, prompt_lens, n_docs_used = [], [], []
     phases = {"retrieve_s": [], "prompt_s": [], "generate_s": []}
-    for step in range(n_steps):
-        if step == args.warmup:
-            pdist.barrier(info)
-            if dev.type == "cuda":
-                torch.cuda.synchronize(dev)
-            stats0 = dict(llm.stats)
-            t0 = time.perf_counter()
-        res = rag.answer(all_q[rep][step], params, bot_group=0)
-        if step >= args.warmup:
-            latencies += [r.latency_s for r in res]
-            prompt_lens += [r.usage["prompt_tokens"] for r in res]
-            n_docs_used += [len(r.documents) for r in res]
-            phases["retrieve_s"].append(res[0].debug_info["took"])
-            phases["prompt_s"].append(res[0].debug_info["prompt"]["took"])
-            phases["generate_s"].append(max(r.debug_info["final"]["took"] for r in res))
+    my_q = all_q[rep]
+    if serve:
+        # closed loop at concurrency B; during the ramp one group is admitted every
+        # max_new_tokens * G / B decode steps so completions are spread evenly from then on
+        pace = max(1, args.max_new_tokens * G // B)
+        next_q, next_admit, admitted, done = 0, 0, 0, 0
+        warm_n, total_n = args.warmup * B, n_steps * B
+        t0 = None
+        stats0, t0 = (sync_start() if warm_n == 0 else (None, None))
+        while done < total_n:
+            while (rag.in_flight + G <= B and next_q + G <= len(my_q)
+                   and (admitted >= B or llm.stats["decode_steps"] >= next_admit)):
+                rag.submit(my_q[next_q:next_q + G], params, bot_group=0)
+                next_q += G
+                admitted += G
+                next_admit += pace
+            for _, r in rag.poll():
+                done += 1
+                if t0 is not None:
+                    latencies.append(r.latency_s)
+                    prompt_lens.append(r.usage["prompt_tokens"])
+                    n_docs_used.append(len(r.documents))
+                    phases["retrieve_s"].append(r.debug_info["took"])
+                    phases["prompt_s"].append(r.debug_info["prompt"]["took"])
+                    phases["generate_s"].append(r.debug_info["final"]["took"])
+                if done == warm_n and t0 is None:
+                    stats0, t0 = sync_start()
+                if done == total_n:
+                    break
+    else:
+        for step in range(n_steps):
+            if step == args.warmup:
+                stats0, t0 = sync_start()
+            res = rag.answer(my_q[step * B:(step + 1) * B], params, bot_group=0)
+            if step >= args.warmup:
+                latencies += [r.latency_s for r in res]
+                prompt_lens += [r.usage["prompt_tokens"] for r in res]
+                n_docs_used += [len(r.documents) for r in res]
+                phases["retrieve_s"].append(res[0].debug_info["took"])
+                phases["prompt_s"].append(res[0].debug_info["prompt"]["took"])
+                phases["generate_s"].append(max(r.debug_info["final"]["took"] for r in res))
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     pdist.barrier(info)
     elapsed = pdist.max_over_ranks(time.perf_counter() - t0, dev)
     p50 = float(np.median(latencies)) if latencies else float("nan")
     p50 = pdist.max_over_ranks(p50, dev)
+    p90 = pdist.max_over_ranks(float(np.percentile(latencies, 90)) if latencies else float("nan"), dev)
     total_q = n_rep * B * args.steps
     eng = {k: round(v - stats0.get(k, 0), 3) if isinstance(v, float) else v - stats0.get(k, 0)
            for k, v in llm.stats.items()}
@@ -219,16 +280,20 @@ def main():
         "dtype": "bf16",
         "data": "synthetic (random-init weights; synthetic corpus/questions)",
         "p50_latency_ms": round(1000 * p50, 1),
+        "p90_latency_ms": round(1000 * p90, 1),
         "config": {
             "model": f"{args.embed_model} + {args.llm_model}",
             "global_batch": n_rep * B,
             "seq_len": int(np.mean(prompt_lens)) if prompt_lens else 0,
             "max_new_tokens": args.max_new_tokens,
             "parallelism": f"dp{n_rep}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
+            "mode": (f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"
+                     if serve else "batch"),
             "index_rows": n_rows,
+            "index": "replicated per GPU" if serve else "sharded (all-gather merge)",
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
-            "graphs": not args.no_graphs,
+            "graphs": llm.use_graphs,
             "tuned_gemm_shapes": llm.tuned_gemms,
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),

@@ -95,7 +95,7 @@ class LLMEngine:
                  max_model_len: int | None = None, kv_cache_gb: float | None = None, num_blocks: int | None = None,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
                  tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
-                 part_size: int = 512, kv_memory_fraction: float = 0.85):
+                 part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0):
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -125,6 +125,7 @@ class LLMEngine:
         self.max_model_len = min(max_model_len or cfg.max_position, cfg.max_position)
         self.max_blocks_per_seq = math.ceil(self.max_model_len / block_size)
         self.max_prefill_tokens = max_prefill_tokens
+        self.mixed_prefill_tokens = mixed_prefill_tokens
         self.part_size = part_size
         hkv = cfg.kv_heads // tp_size
         per_block = KVCache.bytes_per_block(cfg.layers, hkv, block_size, cfg.head_dim)
@@ -146,7 +147,7 @@ class LLMEngine:
         self.finished: dict[int, _Req] = {}
         self._ids = itertools.count()
         self.stats = {"prefill_tokens": 0, "decode_tokens": 0, "decode_steps": 0, "prefill_steps": 0,
-                      "preemptions": 0, "graph_replays": 0}
+                      "preemptions": 0, "graph_replays": 0, "mixed_steps": 0}
         # decode static buffers (graph inputs / outputs)
         self.use_graphs = use_graphs and self.is_gpu
         dev = self.device
@@ -222,18 +223,39 @@ class LLMEngine:
         )
 
     def step(self) -> list[int]:
-        """One scheduler iteration (a prefill chunk batch, else a decode step). Returns finished ids."""
+        """One scheduler iteration. Returns the ids finished by it.
+
+        * nothing running: a prefill step (chunks of up to ``max_prefill_tokens``);
+        * running sequences and pending prompts with ``mixed_prefill_tokens`` > 0: ONE mixed forward
+          -- every running sequence decodes a token and up to ``mixed_prefill_tokens`` prompt tokens
+          ride along in the same GEMMs (a decode-sized GEMM is weight-read bound, so the first few
+          hundred extra rows are nearly free and the rest run at prefill efficiency), instead of
+          stalling all decodes for a whole prefill step;
+        * otherwise a decode step (HIP-graph replay).
+        """
         done_before = set(self.finished)
-        chunks = self._schedule_prefill()
-        if chunks:
-            self._run_prefill(chunks)
-        elif self.running:
-            self._run_decode()
+        if self.running and self.mixed_prefill_tokens > 0 and (self.waiting or self.prefilling):
+            batch = self._reserve_decode()
+            chunks = self._schedule_prefill(self.mixed_prefill_tokens) if batch else self._schedule_prefill()
+            if chunks and batch:
+                self._run_mixed(batch, chunks)
+            elif chunks:
+                self._run_prefill(chunks)
+            elif batch:
+                self._run_decode(batch)
+        else:
+            chunks = self._schedule_prefill()
+            if chunks:
+                self._run_prefill(chunks)
+            elif self.running:
+                batch = self._reserve_decode()
+                if batch:
+                    self._run_decode(batch)
         return [k for k in self.finished if k not in done_before]
 
     # ------------------------------------------------------------------ scheduling
-    def _schedule_prefill(self):
-        budget = self.max_prefill_tokens
+    def _schedule_prefill(self, budget: int | None = None):
+        budget = self.max_prefill_tokens if budget is None else budget
         chunks = []
         for r in self.prefilling:
             if budget <= 0:
@@ -310,6 +332,76 @@ class LLMEngine:
                 self.running.append(r)
                 self._accept_token(r, int(t), now)
 
+    def _run_mixed(self, batch: list, chunks):
+        """Prefill chunks + one decode token per running sequence in one forward (see ``step``)."""
+        t0 = time.perf_counter()
+        dev = self.device
+        B = len(batch)
+        P = len(chunks)
+        Tp = sum(n for _, _, n in chunks)
+        # pad the decode rows (slot -1, one key of block 0, output ignored) so the GEMM M is a
+        # multiple of 64: fewer distinct shapes for the vendor GEMM heuristics, full MFMA tiles
+        Bp = B + (-(Tp + B)) % 64 if self.is_gpu else B
+        Bp = min(Bp, self.max_batch)
+        T = Tp + Bp
+        ids = torch.empty(T, dtype=torch.int32, pin_memory=self.is_gpu)
+        pos = torch.empty(T, dtype=torch.int32, pin_memory=self.is_gpu)
+        slots = torch.empty(T, dtype=torch.int64, pin_memory=self.is_gpu)
+        cu = np.zeros(P + 1, dtype=np.int32)
+        ctx = np.empty(P, dtype=np.int32)
+        ids_np, pos_np = ids.numpy(), pos.numpy()
+        o = 0
+        for i, (r, s, n) in enumerate(chunks):
+            toks = r.full_prompt()
+            ids_np[o:o + n] = toks[s:s + n]
+            pos_np[o:o + n] = np.arange(s, s + n, dtype=np.int32)
+            self.blocks.slot_mapping_into(r.seq, s, n, slots.data_ptr() + 8 * o)
+            o += n
+            cu[i + 1] = o
+            ctx[i] = s + n
+        if Bp > B:
+            self._h_ids[B:Bp] = 0
+            self._h_pos[B:Bp] = 0
+            self._h_slots[B:Bp] = -1
+            self._h_ctx[B:Bp] = 1
+            self._h_bt[B:Bp] = 0
+        ids[Tp:] = self._h_ids[:Bp]
+        pos[Tp:] = self._h_pos[:Bp]
+        slots[Tp:] = self._h_slots[:Bp]
+        bt = torch.zeros((P, self.max_blocks_per_seq), dtype=torch.int32)
+        self._build_block_tables([r.seq for r, _, _ in chunks], bt)
+        to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
+        self._d_ctx[:Bp].copy_(self._h_ctx[:Bp], non_blocking=True)
+        self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
+        meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
+                        cu_q=to(cu), max_q=max(n for _, _, n in chunks), workspace=self._workspace,
+                        part_size=self.part_size, n_decode=Bp, dec_block_tables=self._d_bt[:Bp],
+                        dec_ctx_lens=self._d_ctx[:Bp])
+        hidden = self.model.forward(to(ids), meta, self.kv)
+        last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
+        sel = [int(cu[i + 1]) - 1 for i in last_rows] + list(range(Tp, Tp + B))
+        sel_d = torch.as_tensor(sel, dtype=torch.long).to(dev, non_blocking=True)
+        logits = self.model.logits(hidden.index_select(0, sel_d))
+        preqs = [chunks[i][0] for i in last_rows]
+        toks = self._sample(logits, preqs + batch)
+        now = time.perf_counter()
+        self.stats["prefill_tokens"] += Tp
+        self.stats["decode_tokens"] += B
+        self.stats["decode_steps"] += 1
+        self.stats["mixed_steps"] += 1
+        for r, s, n in chunks:
+            r.computed = s + n
+            r.prefill_s += now - t0
+        for r, t in zip(batch, toks[len(preqs):]):
+            self._accept_token(r, int(t), now)
+        for r, t in zip(preqs, toks[:len(preqs)]):
+            self.blocks.commit_prefix(r.seq, len(r.full_prompt()))
+            self.prefilling.remove(r)
+            r.first_token_t = r.first_token_t or now
+            r.preempted = 0
+            self.running.append(r)
+            self._accept_token(r, int(t), now)
+
     def _sample(self, logits, reqs):
         n = len(reqs)
         temps = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in reqs], dtype=torch.float32)
@@ -367,23 +459,27 @@ class LLMEngine:
         return False
 
     # ------------------------------------------------------------------ decode
-    def _run_decode(self):
-        t0 = time.perf_counter()
-        # one native call reserves a slot per sequence and fills ids/positions/slots/ctx/block tables;
-        # when the pool is dry the youngest running sequence is preempted (recompute) and we retry
+    def _reserve_decode(self) -> list:
+        """Reserve one cache slot per running sequence and fill the host decode buffers (ids, positions,
+        slots, context lengths, block tables) in one native call; when the pool is dry the youngest
+        running sequence is preempted (recompute) and the call retried.  -> the decode batch."""
         while True:
             batch = list(self.running)
             B = len(batch)
             if B == 0:
-                return
+                return batch
             fail = self.blocks.prepare_decode_into(
                 [r.seq for r in batch], [r.out[-1] for r in batch], self.max_blocks_per_seq,
                 self._h_ids.data_ptr(), self._h_pos.data_ptr(), self._h_slots.data_ptr(), self._h_ctx.data_ptr(),
                 self._h_bt.data_ptr())
             if fail < 0:
-                break
+                return batch
             if not self._preempt_one(protect=None if B == 1 else batch[fail]):
                 raise RuntimeError("KV cache exhausted")
+
+    def _run_decode(self, batch: list):
+        t0 = time.perf_counter()
+        B = len(batch)
         self._h_temp[:B] = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in batch])
         self._h_topk[:B] = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32)
         self._h_topp[:B] = torch.tensor([r.params.top_p for r in batch])

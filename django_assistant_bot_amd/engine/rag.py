@@ -110,6 +110,7 @@ class RAGPipeline:
         self.same_question_distance = same_question_distance
         self.max_documents, self.max_tokens_share = max_documents, max_tokens_share
         self._native = native()
+        self._inflight: dict = {}
 
     def retrieve(self, questions: list[str], bot_group: int | None = None):
         """-> per question (documents list, debug dict); one embed + one search for the whole batch."""
@@ -163,29 +164,53 @@ class RAGPipeline:
         token_lists = [flat[offs[i]:offs[i + 1]].tolist() for i in range(len(prompts))]
         return token_lists, used_docs
 
-    def answer(self, questions: list[str], params: SamplingParams | None = None, bot_group: int | None = None,
-               now: datetime | None = None) -> list[RAGResult]:
+    # -------------------------------------------------------------- serving (continuous arrival)
+    def submit(self, questions: list[str], params: SamplingParams | None = None, bot_group: int | None = None,
+               now: datetime | None = None) -> list[int]:
+        """Retrieve + build prompts for newly arrived questions and queue their generations; answers
+        come back from ``poll`` while earlier questions are still decoding (the engine mixes their
+        prompt chunks into the running decode steps)."""
         params = params or SamplingParams(max_new_tokens=1024)
         t0 = time.perf_counter()
         retrieved = self.retrieve(questions, bot_group)
         t_ret = time.perf_counter()
         token_lists, used_docs = self.build_prompts(questions, retrieved, now)
         t_prompt = time.perf_counter()
-        rids = [self.llm.add_request(toks, params) for toks in token_lists]
-        pending = set(rids)
-        done_at = {}
-        while pending:
-            for rid in self.llm.step():
-                if rid in pending:
-                    pending.discard(rid)
-                    done_at[rid] = time.perf_counter()
-        results = []
-        for q, rid, (docs_q, dbg), used in zip(questions, rids, retrieved, used_docs):
+        rids = []
+        for q, toks, ret, used in zip(questions, token_lists, retrieved, used_docs):
+            rid = self.llm.add_request(toks, params)
+            self._inflight[rid] = (q, ret, used, t0, t_ret, t_prompt)
+            rids.append(rid)
+        return rids
+
+    def poll(self) -> list[tuple[int, RAGResult]]:
+        """One engine step -> (request id, result) of every question it completed."""
+        out = []
+        for rid in self.llm.step():
+            if rid not in self._inflight:
+                continue
+            done = time.perf_counter()
+            q, (docs_q, dbg), used, t0, t_ret, t_prompt = self._inflight.pop(rid)
             o = self.llm.pop_output(rid)
             dbg = dict(dbg)
-            dbg["final"] = {"took": done_at[rid] - t_prompt, **o.timings}
+            dbg["final"] = {"took": done - t_prompt, **o.timings}
             dbg["prompt"] = {"took": t_prompt - t_ret}
-            dbg["total"] = {"took": done_at[rid] - t0}
-            results.append(RAGResult(q, o.text, [d.id for d in used], o.usage, o.finish_reason, done_at[rid] - t0,
-                                     dbg))
-        return results
+            dbg["total"] = {"took": done - t0}
+            out.append((rid, RAGResult(q, o.text, [d.id for d in used], o.usage, o.finish_reason, done - t0, dbg)))
+        return out
+
+    @property
+    def in_flight(self) -> int:
+        return len(self._inflight)
+
+    def answer(self, questions: list[str], params: SamplingParams | None = None, bot_group: int | None = None,
+               now: datetime | None = None) -> list[RAGResult]:
+        """Batch mode: answer a batch of questions end to end (submit + poll until all are done)."""
+        rids = self.submit(questions, params, bot_group, now)
+        pending = set(rids)
+        got = {}
+        while pending:
+            for rid, res in self.poll():
+                got[rid] = res
+                pending.discard(rid)
+        return [got[r] for r in rids]

@@ -49,6 +49,11 @@ class AttnMeta:
     max_q: int = 1
     workspace: ops.DecodeWorkspace | None = None
     part_size: int = 512
+    # mixed step: the LAST n_decode tokens are single-token decode rows (one per sequence) with their
+    # own block tables / context lengths; the tokens before them are prefill chunks described above
+    n_decode: int = 0
+    dec_block_tables: torch.Tensor | None = None
+    dec_ctx_lens: torch.Tensor | None = None
 
 
 class KVCache:
@@ -143,6 +148,8 @@ class LlamaModel:
             if meta.decode:
                 a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
                                      meta.workspace)
+            elif meta.n_decode:
+                a = self._mixed_attention(q, kv, li, meta)
             else:
                 a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                               meta.max_q, causal=True)
@@ -156,6 +163,28 @@ class LlamaModel:
             x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
         out, _ = ops.rmsnorm(x, self.final_norm, cfg.eps, residual=residual)
         return out
+
+    @staticmethod
+    def _mixed_attention(q, kv: KVCache, li: int, meta: AttnMeta) -> torch.Tensor:
+        """Prefill rows through flash attention, decode rows through the split-K paged decode kernel
+        (flash's 64-query tiles would be 1/64 full for them and re-read the KV per query head); both
+        write disjoint row ranges of one output, so the projections around stay single GEMMs."""
+        Tp = q.shape[0] - meta.n_decode
+        if not q.is_cuda:
+            parts = []
+            if Tp:
+                parts.append(ops.flash_attention_paged(q[:Tp], kv.k[li], kv.v[li], meta.block_tables, meta.cu_q,
+                                                       meta.ctx_lens, meta.max_q, causal=True))
+            parts.append(ops.paged_decode(q[Tp:], kv.k[li], kv.v[li], meta.dec_block_tables, meta.dec_ctx_lens,
+                                          meta.part_size, meta.workspace))
+            return torch.cat(parts)
+        a = torch.empty_like(q)
+        if Tp:
+            ops.flash_attention_paged(q[:Tp], kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                      meta.max_q, causal=True, out=a[:Tp])
+        ops.paged_decode(q[Tp:], kv.k[li], kv.v[li], meta.dec_block_tables, meta.dec_ctx_lens, meta.part_size,
+                         meta.workspace, out=a[Tp:])
+        return a
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """[n, H] -> [n, V] logits (bf16 GEMM; the sampler reads bf16 or fp32)."""

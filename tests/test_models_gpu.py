@@ -54,3 +54,79 @@ def test_decode_skinny_matches_library_path_and_reference(B):
     h_ref, _ = _run(m_ref, cfg, prompts, "cpu", torch.float32)
     err = (h_sk.float().cpu() - h_ref).abs().max().item()
     assert err < 0.15, err
+
+
+def test_mixed_forward_matches_separate_prefill_and_decode():
+    """One mixed forward (prefill chunks + decode rows, padded decode rows included) == the prefill
+    forward and the decode forward run separately."""
+    cfg = decoder_config("tiny-llama")
+    w = {k: v.to(torch.bfloat16) for k, v in
+         random_decoder_weights(cfg, dtype=torch.float32, seed=9, interleave_mlp=True).items()}
+    model = LlamaModel(cfg, w, DEV, interleaved_mlp=True)
+    bs, nbp = 64, 4
+    gen = torch.Generator().manual_seed(0)
+    dec_prompts = [torch.randint(0, 900, (int(n),), generator=gen).tolist() for n in (40, 130, 77)]
+    pre_prompts = [torch.randint(0, 900, (int(n),), generator=gen).tolist() for n in (90, 33)]
+    nd, npf = len(dec_prompts), len(pre_prompts)
+    i32 = dict(dtype=torch.int32, device=DEV)
+
+    def fresh_cache():
+        kv = KVCache(cfg.layers, (nd + npf + 1) * nbp, cfg.kv_heads, bs, cfg.head_dim, DEV)
+        for b, ids in enumerate(dec_prompts):  # decode sequences: everything but the last token cached
+            T = len(ids) - 1
+            bt = torch.arange(b * nbp, (b + 1) * nbp, **i32)[None]
+            meta = AttnMeta(decode=False, positions=torch.arange(T, **i32), slots=bt[0, 0].long() * bs +
+                            torch.arange(T, device=DEV), block_tables=bt, ctx_lens=torch.tensor([T], **i32),
+                            cu_q=torch.tensor([0, T], **i32), max_q=T)
+            model.forward(torch.tensor(ids[:-1], **i32), meta, kv)
+        return kv
+
+    dbt = torch.arange(nd * nbp, **i32).view(nd, nbp)
+    dpos = torch.tensor([len(p) - 1 for p in dec_prompts], **i32)
+    dslots = dbt[:, 0].long() * bs + dpos.long()
+    dids = torch.tensor([p[-1] for p in dec_prompts], **i32)
+    pbt = torch.arange(nd * nbp, (nd + npf) * nbp, **i32).view(npf, nbp)
+    pids = torch.tensor([t for p in pre_prompts for t in p], **i32)
+    ppos = torch.cat([torch.arange(len(p), **i32) for p in pre_prompts])
+    pslots = torch.cat([pbt[i, 0].long() * bs + torch.arange(len(p), device=DEV) for i, p in enumerate(pre_prompts)])
+    cu = torch.tensor([0, len(pre_prompts[0]), len(pre_prompts[0]) + len(pre_prompts[1])], **i32)
+    pctx = torch.tensor([len(p) for p in pre_prompts], **i32)
+    ws = ops.DecodeWorkspace(8, cfg.heads, cfg.head_dim, nbp * bs // 512 + 1, DEV)
+    # separate
+    kv = fresh_cache()
+    h_pre = model.forward(pids, AttnMeta(decode=False, positions=ppos, slots=pslots, block_tables=pbt,
+                                         ctx_lens=pctx, cu_q=cu, max_q=90), kv)
+    h_dec = model.forward(dids, AttnMeta(decode=True, positions=dpos, slots=dslots, block_tables=dbt,
+                                         ctx_lens=dpos + 1, workspace=ws), kv)
+    # mixed, with two padding decode rows (slot -1, one key of block 0)
+    kv = fresh_cache()
+    pad = 2
+    mbt = torch.cat([dbt, torch.zeros((pad, nbp), **i32)])
+    mctx = torch.cat([dpos + 1, torch.ones(pad, **i32)])
+    ids = torch.cat([pids, dids, torch.zeros(pad, **i32)])
+    pos = torch.cat([ppos, dpos, torch.zeros(pad, **i32)])
+    slots = torch.cat([pslots, dslots, torch.full((pad,), -1, dtype=torch.int64, device=DEV)])
+    meta = AttnMeta(decode=False, positions=pos, slots=slots, block_tables=pbt, ctx_lens=pctx, cu_q=cu, max_q=90,
+                    workspace=ws, n_decode=nd + pad, dec_block_tables=mbt, dec_ctx_lens=mctx)
+    h_mix = model.forward(ids, meta, kv)
+    Tp = pids.numel()
+    torch.testing.assert_close(h_mix[:Tp].float(), h_pre.float(), atol=5e-2, rtol=5e-2)
+    torch.testing.assert_close(h_mix[Tp:Tp + nd].float(), h_dec.float(), atol=5e-2, rtol=5e-2)
+
+
+def test_engine_mixed_schedule_on_gpu():
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+
+    eng = LLMEngine("tiny-llama", device=DEV, max_batch=16, block_size=64, num_blocks=128,
+                    max_prefill_tokens=4096, mixed_prefill_tokens=96)
+    sp = SamplingParams(max_new_tokens=24, ignore_eos=True)
+    rids = [eng.add_request(list(range(10, 10 + 50 + 7 * i)), sp) for i in range(4)]
+    for _ in range(4):
+        eng.step()
+    rids += [eng.add_request(list(range(200, 200 + 120 + 11 * i)), sp) for i in range(6)]
+    while eng.has_unfinished():
+        eng.step()
+    outs = [eng.pop_output(r) for r in rids]
+    assert eng.stats["mixed_steps"] > 0 and eng.stats["graph_replays"] > 0
+    assert all(len(o.token_ids) == 24 for o in outs)
+    assert all(0 <= t < eng.cfg.vocab_size for o in outs for t in o.token_ids)
