@@ -86,6 +86,41 @@ def gemm_suite(which):
         del a, b
 
 
+def skinny_sweep(which):
+    """Split-count sweep of the weight-streaming GEMM at decode batch sizes (cold weights), with the
+    slab reduction timed separately (in the model the consumer kernel sums the slabs)."""
+    for M in (64, 96, 128):
+        for name, N, K in (("llama8b-qkv", 6144, 4096), ("llama8b-o", 4096, 4096), ("llama8b-gateup", 28672, 4096),
+                           ("llama8b-down", 4096, 14336)):
+            if which and which not in name:
+                continue
+            a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            ncopy = max(2, int(2e9 // (N * K * 2)) + 1)
+            ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
+            it = [0]
+
+            def nxt():
+                it[0] = (it[0] + 1) % ncopy
+                return ws[it[0]]
+            byts = 2.0 * N * K
+            res = {"op": name, "M": M, "N": N, "K": K,
+                   "cold_hipblaslt_us": round(timeit(lambda: F.linear(a, nxt()), iters=ncopy * 2) * 1e6, 1)}
+            for S in (1, 2, 4, 8):
+                if K % (S * 256):
+                    continue
+                slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
+                for nt in (False, True):
+                    t = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=nt), iters=ncopy * 2)
+                    res[f"S{S}{'nt' if nt else ''}_us"] = round(t * 1e6, 1)
+                if S > 1:
+                    t_r = timeit(lambda: ops.skinny_reduce(slabs))
+                    res[f"S{S}_reduce_us"] = round(t_r * 1e6, 1)
+            res["weights_tbps_best"] = round(byts / min(v for k, v in res.items() if k.startswith("S") and
+                                                        k.endswith("_us") and "reduce" not in k) / 1e6, 2)
+            emit(**res)
+            del ws
+
+
 def attn_suite():
     # prefill: 16 sequences x 1024 tokens, Llama-3-8B heads
     B, T, Hq, Hkv, D, bs = 16, 1024, 32, 8, 128, 64
@@ -146,6 +181,8 @@ def select_suite():
 
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if which == "skinny":
+        skinny_sweep(sys.argv[2] if len(sys.argv) > 2 else None)
     if which in ("all", "gemm"):
         gemm_suite(sys.argv[2] if len(sys.argv) > 2 else None)
     if which in ("all", "attn"):

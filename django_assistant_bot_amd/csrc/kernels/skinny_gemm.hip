@@ -1,4 +1,4 @@
-// Weight-streaming MFMA GEMM for decode-sized M:  C[M, N] = X[M, K] . W[N, K]^T,  M <= 64.
+// Weight-streaming MFMA GEMM for decode-sized M:  C[M, N] = X[M, K] . W[N, K]^T,  M <= 128.
 //
 // Decode projections are HBM-bound on the weight stream (Llama-3-8B: 436 MB per layer against
 // <= 1.8 MB of activations), so the kernel is organised around reading W exactly once at full rate:
@@ -44,8 +44,10 @@ struct SkinnyParams {
 constexpr int SK_KSTAGE = 256;  // k per pipeline stage
 constexpr int SK_EPI_NONE = 0, SK_EPI_SWIGLU = 2;
 
+// MT <= 4: 2 workgroups per CU (<= 64 KB of X stages each).  MT == 8 (M <= 128): the 128 KB X double
+// buffer allows one workgroup per CU, which in turn gives each wave the whole 512-VGPR budget.
 template <int MT, int RT, bool NT_W>
-__global__ __launch_bounds__(256, 2) void skinny_gemm_kernel(SkinnyParams p) {
+__global__ __launch_bounds__(256, (MT >= 8 ? 1 : 2)) void skinny_gemm_kernel(SkinnyParams p) {
   // waves = (4 / RT row groups of RT 16-row tiles) x (RT k-groups splitting every stage)
   constexpr int NKG = RT;            // k groups
   constexpr int CPW = 8 / RT;        // 32-deep chunks per wave per stage
@@ -277,14 +279,16 @@ static void launch_skinny(const SkinnyParams& p, hipStream_t s) {
     hipLaunchKernelGGL((skinny_gemm_kernel<1, 4, NT_W>), grid, dim3(256), 0, s, p);
   else if (p.M <= 32)
     hipLaunchKernelGGL((skinny_gemm_kernel<2, 4, NT_W>), grid, dim3(256), 0, s, p);
-  else
+  else if (p.M <= 64)
     hipLaunchKernelGGL((skinny_gemm_kernel<4, 2, NT_W>), grid, dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL((skinny_gemm_kernel<8, 2, NT_W>), grid, dim3(256), 0, s, p);
 }
 
 int skinny_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights) {
   if (M <= 0 || N <= 0) return 0;
-  if (M > 64 || N % 64 || S < 1 || K % (S * SK_KSTAGE) || ldx % 8 || ldw % 8 || ldo % 8) return hipErrorInvalidValue;
+  if (M > 128 || N % 64 || S < 1 || K % (S * SK_KSTAGE) || ldx % 8 || ldw % 8 || ldo % 8) return hipErrorInvalidValue;
   if (epilogue != SK_EPI_NONE && epilogue != SK_EPI_SWIGLU) return hipErrorInvalidValue;
   if (S > 1 && (epilogue != SK_EPI_NONE || residual)) return hipErrorInvalidValue;
   if (residual && ldr % 8) return hipErrorInvalidValue;

@@ -87,8 +87,10 @@ class LlamaModel:
             for i in range(cfg.layers)
         ]
         # decode projections on the weight-streaming kernel: "all", "none", or a comma list of
-        # qkv,o,gate_up,down,lm_head (the kernel beats hipBLASLt on the narrow-N projections)
-        sel = os.environ.get("DAB_SKINNY", "none")  # measured: ties hipBLASLt at M=64 (profiles/)
+        # qkv,o,gate_up,down,lm_head.  Default o,down: split-K beats hipBLASLt there at M 64-128
+        # (o 16.6 vs 24.1 us, down 39.7 vs 48+ us at M=128; decode step 9.50 -> 9.23 ms at batch 128),
+        # ties on qkv and loses on gate_up (profiles/decode_gemm_m128_study.md)
+        sel = os.environ.get("DAB_SKINNY", "o,down")
         sel = {"1": "all", "0": "none"}.get(sel, sel)
         names = ("qkv", "o", "gate_up", "down", "lm_head")
         self.skinny_for = set(names) if sel == "all" else set() if sel == "none" else set(sel.split(","))

@@ -329,11 +329,11 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     return out
 
 
-SKINNY_MAX_M = 64
+SKINNY_MAX_M = 128
 _SK_KSTAGE = 256
 
 
-def skinny_splits(N: int, K: int, target_wgs: int = 384, max_splits: int = 16) -> int:
+def skinny_splits(N: int, K: int, target_wgs: int = 256, max_splits: int = 16) -> int:
     """K-slices for the weight-streaming GEMM: the fewest that give ~target_wgs workgroups (each
     workgroup streams 64 weight rows of one slice)."""
     tiles = N // 64
@@ -365,7 +365,7 @@ def skinny_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=N
     expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
     M, K = x.shape
     N = w.shape[0]
-    expect(w.shape[1] == K and M <= SKINNY_MAX_M, "skinny_gemm: inner dims mismatch or M > 64")
+    expect(w.shape[1] == K and M <= SKINNY_MAX_M, "skinny_gemm: inner dims mismatch or M > 128")
     expect(N % 64 == 0 and K % (splits * _SK_KSTAGE) == 0, "skinny_gemm needs N % 64 == 0 and K % (256*splits) == 0")
     expect(x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0, "row strides must be multiples of 8")
     if splits > 1:

@@ -208,7 +208,7 @@ def test_gemm_swiglu():
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("M", [1, 7, 16, 33, 64])
+@pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 65, 100, 128])
 @pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (192, 1792, 7), (128, 4096, 16)])
 def test_skinny_gemm(M, N, K, S):
     x, w = bf(M, K), bf(N, K, scale=0.05)
@@ -225,7 +225,7 @@ def test_skinny_gemm(M, N, K, S):
         close(ops.skinny_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [3, 64])
+@pytest.mark.parametrize("M", [3, 64, 128])
 def test_skinny_swiglu_and_strided_x(M):
     F, K = 512, 1024
     xs, wg, wu = bf(M, K + 64), bf(F, K, scale=0.05), bf(F, K, scale=0.05)

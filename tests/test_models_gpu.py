@@ -33,7 +33,7 @@ def _run(model, cfg, prompts, device, dtype):
     return h, model.logits(h)
 
 
-@pytest.mark.parametrize("B", [3, 20, 64])
+@pytest.mark.parametrize("B", [3, 20, 64, 128])
 def test_decode_skinny_matches_library_path_and_reference(B):
     cfg = decoder_config("tiny-llama")
     w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True)
