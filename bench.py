@@ -13,14 +13,17 @@ the batched mirror of the reference's ContextService -> ChatCompletion chain):
 
 Two load shapes (``--mode``):
 
-  * ``serve`` (default) -- a bot's real traffic: questions keep arriving.  Closed loop at a fixed
+  * ``serve`` -- a bot's real traffic: questions keep arriving.  Closed loop at a fixed
     concurrency C (= ``--batch``) per GPU: whenever ``--admit-group`` slots are free, that many new
     questions are retrieved and queued; their prompt chunks ride along inside the running decode
     steps (``LLMEngine`` mixed steps).  Arrivals are staggered over the first generation length so
     the load is in steady state; one "step" = C completed questions (warmup steps are not timed).
     The index is replicated per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
-  * ``batch`` -- one step = a batch of C questions answered together (retrieve all, prefill all,
-    decode all); the index is sharded across the ranks with an all-gather merge.
+  * ``batch`` (default) -- one step = a batch of C questions answered together (retrieve all,
+    prefill all, decode all); the index is sharded across the ranks with an all-gather merge.
+    Measured at C=128 on one MI355X: batch 32.5 q/s p50 3.9 s; serve 30.3 q/s p50 4.2 s (mixed
+    2048) -- large-M prefill GEMMs run at ~1.6 PFLOP/s, so mixing decode rows into smaller prefill
+    chunks costs more than it saves (profiles/serving_mixed_steps.md).
 
 Weights are random-init with the real architectures; corpus / questions are synthetic: each
 question has planted "paraphrase" rows near its embedding in 3-5 target documents so retrieval
@@ -99,7 +102,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mode", choices=("serve", "batch"), default="serve")
+    ap.add_argument("--mode", choices=("serve", "batch"), default="batch")
     ap.add_argument("--batch", type=int, default=128,
                     help="questions in flight per GPU (serve) / per batch (batch); one step = this many answers")
     ap.add_argument("--admit-group", type=int, default=16, help="serve: questions retrieved + queued together")
