@@ -7,6 +7,7 @@ compiled by hipcc as host C++, and everything is linked into one shared object n
 source or header is newer than the object.
 
     python -m django_assistant_bot_amd.build [--force] [-j N] [--debug]
+    python -m django_assistant_bot_amd.build --selftest asan|tsan   # host runtime under sanitizers
 """
 from __future__ import annotations
 
@@ -86,7 +87,7 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     if failed:
         raise RuntimeError(f"native build failed for: {failed}")
     if force or jobs_list or not out.exists():
-        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(out), "-lpthread"]
+        link = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *[str(o) for o in objs], "-o", str(out), "-lpthread", "-ldl"]
         cmd, rc, log = _compile(link)
         if rc:
             print(" ".join(cmd), file=sys.stderr)
@@ -95,13 +96,39 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
     return out
 
 
+SANITIZERS = {"asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-fno-sanitize-recover=undefined"],
+              "tsan": ["-fsanitize=thread"]}
+
+
+def selftest(kind: str = "asan", out_dir: Path | None = None) -> tuple[int, str]:
+    """Compiles csrc/tests/runtime_selftest.cpp with the host runtime sources (plain g++, no HIP:
+    GPU sanitizers are not available on this hardware pool) under ASan+UBSan or TSan, runs it and
+    returns (exit code, output)."""
+    out_dir = out_dir or BUILD
+    out_dir.mkdir(exist_ok=True)
+    exe = out_dir / f"runtime_selftest_{kind}"
+    srcs = [CSRC / "tests" / "runtime_selftest.cpp", *sorted((CSRC / "runtime").glob("*.cpp"))]
+    cmd = ["g++", "-std=c++17", "-g", "-O1", *SANITIZERS[kind], f"-I{CSRC}", *map(str, srcs), "-o", str(exe),
+           "-ldl", "-lpthread"]
+    _, rc, log = _compile(cmd)
+    if rc:
+        return rc, log
+    p = subprocess.run([str(exe)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=600)
+    return p.returncode, p.stdout
+
+
 def main() -> None:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("--debug", action="store_true")
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--selftest", choices=sorted(SANITIZERS), default=None)
     a = ap.parse_args()
+    if a.selftest:
+        rc, log = selftest(a.selftest)
+        print(log)
+        sys.exit(rc)
     print(build(force=a.force, jobs=a.jobs, debug=a.debug, verbose=a.verbose))
 
 

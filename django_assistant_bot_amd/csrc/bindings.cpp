@@ -13,6 +13,7 @@
 #include "runtime/kv_manager.h"
 #include "runtime/rag.h"
 #include "runtime/tokenizer.h"
+#include "runtime/trace.h"
 
 namespace py = pybind11;
 using u = uintptr_t;
@@ -27,6 +28,10 @@ static void check(int err, const char* name) {
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X (gfx950) kernels and native runtime of django_assistant_bot_amd";
+  m.def("roctx_available", &dab::trace::available);
+  m.def("roctx_push", [](const std::string& name) { return dab::trace::range_push(name.c_str()); });
+  m.def("roctx_pop", &dab::trace::range_pop);
+  m.def("roctx_mark", [](const std::string& name) { dab::trace::mark(name.c_str()); });
 
   // ---------------- kernels ----------------
   m.def("rmsnorm", [](u out, u res_out, u x, u res_in, u w, int rows, int cols, float eps, u s) {

@@ -33,6 +33,7 @@ from .. import ops
 from ..models import AttnMeta, KVCache, LlamaModel, decoder_config, random_decoder_weights
 from ..models.configs import DecoderConfig
 from ..ops._lib import native
+from ..utils import trace
 from .tokenizer import Tokenizer
 
 
@@ -181,6 +182,8 @@ class LLMEngine:
         self._graphs: dict = {}
         self._buckets = _bucket_sizes(max_batch)
         self._graph_pool = None
+        # GPU spans of the engine phases (HIP events, read where the host syncs anyway) -> stats
+        self.timer = trace.GpuTimer(enabled=self.is_gpu)
 
     # ------------------------------------------------------------------ public API
     def add_request(self, prompt_ids: list, params: SamplingParams | None = None, request_id: int | None = None) -> int:
@@ -309,7 +312,8 @@ class LLMEngine:
         to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
         meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
                         cu_q=to(cu), max_q=max(n for _, _, n in chunks))
-        hidden = self.model.forward(to(ids), meta, self.kv)
+        with self.timer.phase("prefill"):
+            hidden = self.model.forward(to(ids), meta, self.kv)
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
         self.stats["prefill_tokens"] += T
         self.stats["prefill_steps"] += 1
@@ -318,6 +322,7 @@ class LLMEngine:
             logits = self.model.logits(hidden.index_select(0, sel))
             reqs = [chunks[i][0] for i in last_rows]
             toks = self._sample(logits, reqs)
+        self._collect_gpu_times(block=bool(last_rows))
         for r, s, n in chunks:
             r.computed = s + n
         now = time.perf_counter()
@@ -377,13 +382,15 @@ class LLMEngine:
                         cu_q=to(cu), max_q=max(n for _, _, n in chunks), workspace=self._workspace,
                         part_size=self.part_size, n_decode=Bp, dec_block_tables=self._d_bt[:Bp],
                         dec_ctx_lens=self._d_ctx[:Bp])
-        hidden = self.model.forward(to(ids), meta, self.kv)
+        with self.timer.phase("mixed"):
+            hidden = self.model.forward(to(ids), meta, self.kv)
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
         sel = [int(cu[i + 1]) - 1 for i in last_rows] + list(range(Tp, Tp + B))
         sel_d = torch.as_tensor(sel, dtype=torch.long).to(dev, non_blocking=True)
         logits = self.model.logits(hidden.index_select(0, sel_d))
         preqs = [chunks[i][0] for i in last_rows]
         toks = self._sample(logits, preqs + batch)
+        self._collect_gpu_times()
         now = time.perf_counter()
         self.stats["prefill_tokens"] += Tp
         self.stats["decode_tokens"] += B
@@ -401,6 +408,11 @@ class LLMEngine:
             r.preempted = 0
             self.running.append(r)
             self._accept_token(r, int(t), now)
+
+    def _collect_gpu_times(self, block: bool = True):
+        for name, ms in self.timer.collect(block).items():
+            key = f"gpu_{name}_ms"
+            self.stats[key] = self.stats.get(key, 0.0) + ms
 
     def _sample(self, logits, reqs):
         n = len(reqs)
@@ -503,22 +515,23 @@ class LLMEngine:
             d[:Bp].copy_(h[:Bp], non_blocking=True)
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
         t1 = time.perf_counter()
+        g = None
         if self.use_graphs:
             g = self._graphs.get((Bp, self._fast))
             if g is None:
                 g = self._capture(Bp)
+        with self.timer.phase("decode"):
             if g is not None:
                 g.replay()
                 self.stats["graph_replays"] += 1
             else:
                 self._decode_body(Bp)
-        else:
-            self._decode_body(Bp)
         if self.is_gpu:
             self._tp_sync_tokens(self._d_tokens[:Bp])
             self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
         t2 = time.perf_counter()
+        self._collect_gpu_times()
         toks = self._h_tokens[:B].tolist()
         now = time.perf_counter()
         self.stats["decode_steps"] += 1

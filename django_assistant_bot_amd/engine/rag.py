@@ -31,6 +31,7 @@ import numpy as np
 import torch
 
 from ..ops._lib import native
+from ..utils import trace
 from .llm_engine import LLMEngine, SamplingParams
 
 
@@ -111,18 +112,22 @@ class RAGPipeline:
         self.max_documents, self.max_tokens_share = max_documents, max_tokens_share
         self._native = native()
         self._inflight: dict = {}
+        self.timer = trace.GpuTimer(device=getattr(llm, "device", None))
 
     def retrieve(self, questions: list[str], bot_group: int | None = None):
         """-> per question (documents list, debug dict); one embed + one search for the whole batch."""
         t0 = time.perf_counter()
-        emb = self.embedder.embed(questions)
+        with self.timer.phase("embed"):
+            emb = self.embedder.embed(questions)
         t1 = time.perf_counter()
         k = self.max_scores_n * self.top_n * 10
         groups = None if bot_group is None else [bot_group] * len(questions)
-        sims, ids, docs = self.index.search(emb, k, q_groups=groups)
+        with self.timer.phase("search"):
+            sims, ids, docs = self.index.search(emb, k, q_groups=groups)
         dist = (1.0 - sims).float().cpu().numpy()
         ids_h = ids.cpu().numpy()
         docs_h = docs.cpu().numpy()
+        gpu_ms = {f"{k_}_gpu_ms": round(v, 3) for k_, v in self.timer.collect().items()}
         t2 = time.perf_counter()
         out = []
         for qi in range(len(questions)):
@@ -145,6 +150,7 @@ class RAGPipeline:
             dbg["documents"] = [f"[{doc.id} {s:.4f}] {doc.name}" for doc, (_, s) in zip(docs_q, picked)]
             dbg["took"] = (t2 - t0)
             dbg["embed_s"] = t1 - t0
+            dbg.update(gpu_ms)
             out.append((docs_q, dbg))
         return out
 
