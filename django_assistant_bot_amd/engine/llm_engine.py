@@ -48,6 +48,7 @@ class SamplingParams:
     seed: int | None = None
     stop_token_ids: tuple = ()
     do_sample: bool = True
+    timeout_s: float | None = None  # per-request deadline from arrival: finish_reason "timeout"
 
 
 @dataclass
@@ -141,6 +142,7 @@ class LLMEngine:
             num_blocks = max(2, min(num_blocks, max_batch * self.max_blocks_per_seq + 8))
         self.kv = KVCache(cfg.layers, num_blocks, hkv, block_size, cfg.head_dim, self.device)
         self.blocks = native().KVBlockManager(num_blocks, block_size, prefix_cache)
+        self._prefix_cache = prefix_cache
         self.seed = seed
         self.waiting: deque[_Req] = deque()
         self.prefilling: list[_Req] = []
@@ -184,6 +186,8 @@ class LLMEngine:
         self._graph_pool = None
         # GPU spans of the engine phases (HIP events, read where the host syncs anyway) -> stats
         self.timer = trace.GpuTimer(enabled=self.is_gpu)
+        # test hook: called at the start of every step (fault injection, e.g. raise a HIP error)
+        self.fault_hook = None
 
     # ------------------------------------------------------------------ public API
     def add_request(self, prompt_ids: list, params: SamplingParams | None = None, request_id: int | None = None) -> int:
@@ -237,6 +241,9 @@ class LLMEngine:
         * otherwise a decode step (HIP-graph replay).
         """
         done_before = set(self.finished)
+        if self.fault_hook is not None:
+            self.fault_hook(self)
+        self._expire_deadlines()
         if self.running and self.mixed_prefill_tokens > 0 and (self.waiting or self.prefilling):
             batch = self._reserve_decode()
             chunks = self._schedule_prefill(self.mixed_prefill_tokens) if batch else self._schedule_prefill()
@@ -255,6 +262,41 @@ class LLMEngine:
                 if batch:
                     self._run_decode(batch)
         return [k for k in self.finished if k not in done_before]
+
+    def abort(self, rid: int, reason: str = "abort") -> bool:
+        """Stops a request wherever it is (queued, prefilling or decoding) and frees its KV blocks;
+        its output (tokens so far) is kept under ``finish_reason=reason``."""
+        for q in (self.waiting, self.prefilling, self.running):
+            for r in q:
+                if r.rid == rid:
+                    q.remove(r)
+                    if r.admitted:
+                        self.blocks.free_sequence(r.seq)
+                    r.finish_reason = reason
+                    r.finish_t = time.perf_counter()
+                    self.finished[rid] = r
+                    self.stats["aborted"] = self.stats.get("aborted", 0) + 1
+                    return True
+        return False
+
+    def fail_all(self) -> list[int]:
+        """Drops every unfinished request (after an engine fault) and returns their ids; the block
+        pool is rebuilt so nothing leaks if the fault left the bookkeeping half-updated."""
+        ids = [r.rid for q in (self.waiting, self.prefilling, self.running) for r in q]
+        self.waiting.clear()
+        self.prefilling.clear()
+        self.running.clear()
+        self.blocks = native().KVBlockManager(self.blocks.num_blocks(), self.block_size, self._prefix_cache)
+        self.timer.collect()
+        return ids
+
+    def _expire_deadlines(self):
+        now = time.perf_counter()
+        for q in (self.waiting, self.prefilling, self.running):
+            for r in list(q):
+                t = r.params.timeout_s
+                if t is not None and now - r.arrival > t:
+                    self.abort(r.rid, "timeout")
 
     # ------------------------------------------------------------------ scheduling
     def _schedule_prefill(self, budget: int | None = None):

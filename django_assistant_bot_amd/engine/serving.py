@@ -33,6 +33,9 @@ class LLMWorker:
         self._stop = False
         self._lock = threading.Lock()
         self.requests = 0
+        self.faults = 0
+        self.healthy = True  # False after a sticky device error: /health reports 503 for a restart
+        self.last_error = ""
         self._thread = threading.Thread(target=self._run, name="dab-llm-worker", daemon=True)
         self._thread.start()
 
@@ -43,7 +46,16 @@ class LLMWorker:
         return fut
 
     async def generate(self, prompt_ids, params):
-        return await asyncio.wrap_future(self.submit(prompt_ids, params))
+        fut = self.submit(prompt_ids, params)
+        try:
+            return await asyncio.wrap_future(fut)
+        except asyncio.CancelledError:  # caller gone (client disconnect / timeout): free its slot
+            self.cancel(fut)
+            raise
+
+    def cancel(self, fut: Future) -> None:
+        self._inbox.put(("__cancel__", None, fut))
+        self._wake.set()
 
     def _drain(self):
         while True:
@@ -51,6 +63,13 @@ class LLMWorker:
                 ids, params, fut = self._inbox.get_nowait()
             except queue.Empty:
                 return
+            if ids == "__cancel__":
+                for rid, f in list(self._futures.items()):
+                    if f is fut:
+                        self.engine.abort(rid, "cancelled")
+                        self.engine.pop_output(rid)
+                        del self._futures[rid]
+                continue
             try:
                 rid = self.engine.add_request(ids, params)
                 self._futures[rid] = fut
@@ -69,11 +88,16 @@ class LLMWorker:
                 finished = self.engine.step()
             except Exception as exc:  # engine fault: fail every in-flight request, keep serving
                 logger.exception("engine step failed")
+                self.faults += 1
+                self.last_error = f"{type(exc).__name__}: {exc}"
+                if _sticky_device_error(exc):
+                    # a HIP fault poisons the context: stop taking work, let the supervisor restart
+                    self.healthy = False
                 for fut in self._futures.values():
                     if not fut.done():
                         fut.set_exception(exc)
                 self._futures.clear()
-                self._reset_engine()
+                self.engine.fail_all()
                 continue
             for rid in finished:
                 fut = self._futures.pop(rid, None)
@@ -81,18 +105,18 @@ class LLMWorker:
                 if fut is not None and not fut.done():
                     fut.set_result(out)
 
-    def _reset_engine(self):
-        eng = self.engine
-        for q in (eng.waiting, eng.prefilling, eng.running):
-            for r in list(q):
-                eng.blocks.free_sequence(r.seq)
-        eng.waiting.clear()
-        eng.prefilling.clear()
-        eng.running.clear()
-
     def stop(self):
         self._stop = True
         self._wake.set()
+
+
+def _sticky_device_error(exc: BaseException) -> bool:
+    """HIP errors that leave the device context unusable (memory faults, illegal instructions,
+    ECC, hardware exceptions); after one the process must be restarted."""
+    msg = str(exc).lower()
+    return any(k in msg for k in ("illegal address", "illegal memory access", "memory access fault", "hiperrorillegal", "ecc error",
+                                  "hardware exception", "device-side assert", "unspecified launch failure",
+                                  "hiperrorlaunchfailure", "device lost"))
 
 
 class EmbedWorker:
@@ -152,6 +176,21 @@ _emb: dict = {}
 _lock = threading.Lock()
 
 
+def setting(name: str, default):
+    """Engine setting (SURVEY.md 5.6 keys) from the app settings when available, else the env."""
+    try:
+        from assistant.conf import settings
+
+        v = settings.get(name, default)
+    except ImportError:
+        import os
+
+        v = os.environ.get(name, default)
+    if v is None or default is None:
+        return v
+    return type(default)(v)
+
+
 def engine_device():
     import torch
 
@@ -167,6 +206,8 @@ def get_llm_worker(model: str, **engine_kwargs) -> LLMWorker:
 
             engine_kwargs.setdefault("device", engine_device())
             engine_kwargs.setdefault("max_batch", 64 if engine_kwargs["device"] == "cuda" else 4)
+            engine_kwargs.setdefault("block_size", setting("KV_BLOCK_SIZE", 64))
+            engine_kwargs.setdefault("max_prefill_tokens", setting("MAX_BATCH_TOKENS", 65536))
             if engine_kwargs["device"] == "cpu":
                 engine_kwargs.setdefault("max_model_len", 2048)
             w = _llm[key] = LLMWorker(LLMEngine(model, **engine_kwargs))
@@ -185,6 +226,12 @@ def get_embed_worker(model: str, **engine_kwargs) -> EmbedWorker:
         return w
 
 
+def health() -> dict:
+    """Worker health for gpu_service /health (unhealthy after a sticky device fault)."""
+    bad = {k: w.last_error for k, w in _llm.items() if not w.healthy}
+    return {"healthy": not bad, "unhealthy_workers": bad}
+
+
 def loaded_models() -> dict:
     return {"embedders": sorted(_emb), "providers": sorted(_llm)}
 
@@ -197,7 +244,7 @@ def engine_metrics() -> dict:
         m["embedders"][k] = {"requests": w.requests, **w.engine.stats, "queue_depth": w._inbox.qsize()}
     for k, w in _llm.items():
         e = w.engine
-        m["providers"][k] = {"requests": w.requests, **e.stats, "running": len(e.running), "waiting": len(e.waiting),
+        m["providers"][k] = {"requests": w.requests, "faults": w.faults, "healthy": int(w.healthy), **e.stats, "running": len(e.running), "waiting": len(e.waiting),
                              "kv_free_blocks": e.blocks.num_free_blocks(), "kv_total_blocks": e.blocks.num_blocks(),
                              "prefix_hit_tokens": e.blocks.prefix_hits()}
     if torch.cuda.is_available():

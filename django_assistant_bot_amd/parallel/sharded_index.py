@@ -48,6 +48,48 @@ class ShardedIndex:
         self.local.add(ids[sel], v, d, g)
         return int(mine.sum())
 
+    # ------------------------------------------------------------------ snapshots
+    def save(self, directory: str) -> str:
+        """Every rank writes its shard as ``shard-RRR-of-WWW.safetensors`` (the index is a cache of
+        the DB vectors; the snapshot is only for a fast warm start)."""
+        import os
+
+        os.makedirs(directory, exist_ok=True)
+        self.local.compact()
+        path = os.path.join(directory, f"shard-{self.rank:03d}-of-{self.world:03d}.safetensors")
+        self.local.save(path)
+        return path
+
+    @classmethod
+    def load(cls, directory: str, device=None, group=None) -> "ShardedIndex":
+        """Warm start from a snapshot written by any world size: each rank reads every shard file
+        (memory-mapped by safetensors) and keeps the rows it owns under the CURRENT world size."""
+        import glob
+        import os
+
+        from safetensors import safe_open
+
+        files = sorted(glob.glob(os.path.join(directory, "shard-*-of-*.safetensors")))
+        if not files:
+            raise FileNotFoundError(f"no index shards in {directory}")
+        with safe_open(files[0], framework="pt") as f:
+            dim = f.get_slice("vecs").get_shape()[1]
+        idx = cls(dim, device, group)
+        for path in files:
+            with safe_open(path, framework="pt") as f:
+                ids = f.get_tensor("ids")
+                live = ids >= 0
+                if not bool(live.any()):
+                    continue
+                ids_np = ids[live].numpy()
+                mine = idx.owner(ids_np) == idx.rank
+                if not mine.any():
+                    continue
+                sel = torch.nonzero(live).view(-1)[torch.from_numpy(np.nonzero(mine)[0])]
+                idx.local.add(ids_np[mine], f.get_tensor("vecs")[sel], f.get_tensor("docs")[sel].numpy(),
+                              f.get_tensor("group")[sel].numpy())
+        return idx
+
     def remove(self, ids) -> int:
         ids = np.asarray(ids, dtype=np.int64).reshape(-1)
         return self.local.remove(ids[self.owner(ids) == self.rank])

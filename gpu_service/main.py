@@ -138,7 +138,12 @@ def _index(name: str, dim: Optional[int] = None, create: bool = False):
             from django_assistant_bot_amd.engine.serving import engine_device
             from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
-            idx = indexes[name] = VectorIndex(dim, device=engine_device())
+            import torch
+
+            from django_assistant_bot_amd.engine.serving import setting
+
+            dtype = getattr(torch, str(setting("INDEX_DTYPE", "bfloat16")))
+            idx = indexes[name] = VectorIndex(dim, device=engine_device(), dtype=dtype)
         return idx
 
 
@@ -185,10 +190,17 @@ async def index_search(name: str, request: SearchRequest):
 
 @app.get("/health")
 async def health():
-    from django_assistant_bot_amd.engine.serving import engine_device
+    """200 when serving; 503 after a sticky device fault in an engine worker (the supervisor /
+    gunicorn restarts the process)."""
+    from fastapi.responses import JSONResponse
 
-    return {"status": "ok", "device": str(engine_device()), "embedders": sorted(embedders),
-            "providers": sorted(providers), "indexes": {k: len(v) for k, v in indexes.items()}}
+    from django_assistant_bot_amd.engine.serving import engine_device, health as engine_health
+
+    h = engine_health()
+    body = {"status": "ok" if h["healthy"] else "unhealthy", "device": str(engine_device()),
+            "embedders": sorted(embedders), "providers": sorted(providers),
+            "indexes": {k: len(v) for k, v in indexes.items()}, **({} if h["healthy"] else h)}
+    return JSONResponse(body, status_code=200 if h["healthy"] else 503)
 
 
 def _flatten(prefix: str, obj, out: list, labels: str = ""):

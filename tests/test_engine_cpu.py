@@ -54,3 +54,68 @@ def test_mixed_step_accounting():
     first, second = eng.running
     assert len(first.out) == 4
     assert len(second.out) == 1
+
+
+def test_deadline_and_abort_free_blocks():
+    eng = _engine(0, _weights())
+    free0 = eng.blocks.num_free_blocks()
+    sp = SamplingParams(max_new_tokens=50, do_sample=False, temperature=0.0, ignore_eos=True)
+    a = eng.add_request(list(range(10, 40)), sp)
+    b = eng.add_request(list(range(50, 70)), SamplingParams(max_new_tokens=50, ignore_eos=True, timeout_s=0.0))
+    c = eng.add_request(list(range(80, 100)), sp)
+    eng.step()
+    assert eng.finished[b].finish_reason == "timeout"
+    for _ in range(3):
+        eng.step()
+    assert eng.abort(a)
+    assert not eng.abort(12345)
+    out_a = eng.pop_output(a)
+    assert out_a.finish_reason == "abort" and 1 <= len(out_a.token_ids) < 50
+    while eng.has_unfinished():
+        eng.step()
+    assert len(eng.pop_output(c).token_ids) == 50
+    assert eng.blocks.num_free_blocks() == free0
+
+
+def test_worker_survives_injected_faults_and_flags_sticky_ones():
+    from django_assistant_bot_amd.engine import serving
+
+    eng = _engine(0, _weights())
+    worker = serving.LLMWorker(eng)
+    try:
+        sp = SamplingParams(max_new_tokens=5, do_sample=False, temperature=0.0, ignore_eos=True)
+        fired = []
+
+        def fault_once(e):
+            if not fired:
+                fired.append(1)
+                raise RuntimeError("injected step failure")
+        eng.fault_hook = fault_once
+        fut = worker.submit(list(range(5, 25)), sp)
+        try:
+            fut.result(timeout=60)
+            raise AssertionError("expected the injected failure")
+        except RuntimeError as exc:
+            assert "injected" in str(exc)
+        assert worker.faults == 1 and worker.healthy
+        # the engine keeps serving after the reset, with the block pool intact
+        out = worker.submit(list(range(5, 25)), sp).result(timeout=60)
+        assert len(out.token_ids) == 5
+        assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
+        # a sticky device error marks the worker unhealthy (gpu_service /health -> 503)
+        eng.fault_hook = lambda e: (_ for _ in ()).throw(
+            RuntimeError("HIP error: an illegal memory access was encountered"))
+        fut = worker.submit(list(range(5, 25)), sp)
+        try:
+            fut.result(timeout=60)
+        except RuntimeError:
+            pass
+        assert not worker.healthy and "illegal memory access" in worker.last_error
+        serving._llm["fault-test"] = worker
+        try:
+            h = serving.health()
+            assert not h["healthy"] and "fault-test" in h["unhealthy_workers"]
+        finally:
+            serving._llm.pop("fault-test", None)
+    finally:
+        worker.stop()

@@ -119,3 +119,42 @@ def test_dp_corpus_embedding_matches_single_rank(tmp_path):
     out = str(tmp_path / "dp.pt")
     _run(_dp_embed_body, out)
     assert torch.load(out, weights_only=True)["err"] < 1e-5
+
+
+def _snapshot_body(info, directory):
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    g = torch.Generator().manual_seed(3)
+    n, dim = 600, 32
+    vecs = torch.randn(n, dim, generator=g)
+    ids = np.arange(n, dtype=np.int64) * 7 + 1
+    idx = ShardedIndex(dim, "cpu")
+    idx.add(ids, vecs, doc_ids=ids // 10, groups=np.zeros(n, dtype=np.int32))
+    idx.remove(ids[:5])
+    idx.save(directory)
+    torch.distributed.barrier()
+    back = ShardedIndex.load(directory, "cpu")  # same world size
+    q = torch.randn(4, dim, generator=g)
+    a, b = idx.search(q, 20), back.search(q, 20)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+
+
+def test_sharded_index_snapshot_reshards(tmp_path):
+    d = str(tmp_path / "snap")
+    _run(_snapshot_body, d)
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    single = ShardedIndex.load(d, "cpu")  # world 1: both shard files merged into one
+    assert len(single) == 595
+    g = torch.Generator().manual_seed(3)
+    n, dim = 600, 32
+    vecs = torch.randn(n, dim, generator=g)
+    ids = np.arange(n, dtype=np.int64) * 7 + 1
+    ref = VectorIndex(dim, "cpu")
+    ref.add(ids[5:], vecs[5:], doc_ids=ids[5:] // 10, groups=np.zeros(n - 5, dtype=np.int32))
+    q = torch.randn(4, dim, generator=g)
+    s1, i1, d1 = single.search(q, 20)
+    s2, i2, d2 = ref.search(q, 20)
+    assert torch.equal(i1, i2) and torch.equal(d1, d2) and torch.allclose(s1, s2)
