@@ -159,6 +159,38 @@ def attn_suite():
         del kc, vc
 
 
+def decode_sweep():
+    """Paged decode attention at the bench's decode shape (128 sequences, ~1.2k context, Llama-3-8B
+    heads) across partition sizes, with shuffled block tables like the block manager produces."""
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    g = torch.Generator().manual_seed(0)
+    for Bd in (32, 128, 256):
+        ctx_h = torch.randint(1100, 1400, (Bd,), generator=g)
+        nbs = [math.ceil(int(c) / bs) for c in ctx_h]
+        nbd = sum(nbs)
+        kc = torch.randn(nbd, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        perm = torch.randperm(nbd, generator=g)
+        maxb = max(nbs)
+        bt = torch.zeros((Bd, maxb), dtype=torch.int32)
+        o = 0
+        for i, n in enumerate(nbs):
+            bt[i, :n] = perm[o:o + n].to(torch.int32)
+            o += n
+        bt = bt.cuda()
+        qd = torch.randn(Bd, Hq, D, device="cuda").to(torch.bfloat16)
+        ctx = ctx_h.to(torch.int32).cuda()
+        byts = 2.0 * float(ctx_h.sum()) * Hkv * D * 2
+        res = {"op": "paged-decode-sweep", "B": Bd, "mean_ctx": int(ctx_h.float().mean())}
+        for part in (256, 512, 1024, 2048):
+            ws = ops.DecodeWorkspace(Bd, Hq, D, math.ceil(4096 / part), "cuda")
+            t = timeit(lambda: ops.paged_decode(qd, kc, vc, bt, ctx, part, ws), iters=50)
+            res[f"p{part}_us"] = round(t * 1e6, 1)
+            res[f"p{part}_tbps"] = round(byts / t / 1e12, 2)
+        emit(**res)
+        del kc, vc
+
+
 def select_suite():
     logits = torch.randn(64, 128256, device="cuda").to(torch.bfloat16)
     temp = torch.ones(64, device="cuda")
@@ -183,6 +215,8 @@ if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which == "skinny":
         skinny_sweep(sys.argv[2] if len(sys.argv) > 2 else None)
+    if which == "decode":
+        decode_sweep()
     if which in ("all", "gemm"):
         gemm_suite(sys.argv[2] if len(sys.argv) > 2 else None)
     if which in ("all", "attn"):
