@@ -188,6 +188,9 @@ class LLMEngine:
         self.timer = trace.GpuTimer(enabled=self.is_gpu)
         # test hook: called at the start of every step (fault injection, e.g. raise a HIP error)
         self.fault_hook = None
+        # deadlines are checked by step() unless a TP leader drives them explicitly (wall clocks of
+        # the ranks differ; every rank must drop a request at the same step)
+        self.auto_expire = True
 
     # ------------------------------------------------------------------ public API
     def add_request(self, prompt_ids: list, params: SamplingParams | None = None, request_id: int | None = None) -> int:
@@ -243,7 +246,8 @@ class LLMEngine:
         done_before = set(self.finished)
         if self.fault_hook is not None:
             self.fault_hook(self)
-        self._expire_deadlines()
+        if self.auto_expire:
+            self.expire_deadlines()
         if self.running and self.mixed_prefill_tokens > 0 and (self.waiting or self.prefilling):
             batch = self._reserve_decode()
             chunks = self._schedule_prefill(self.mixed_prefill_tokens) if batch else self._schedule_prefill()
@@ -290,13 +294,16 @@ class LLMEngine:
         self.timer.collect()
         return ids
 
-    def _expire_deadlines(self):
+    def expired(self) -> list[int]:
         now = time.perf_counter()
-        for q in (self.waiting, self.prefilling, self.running):
-            for r in list(q):
-                t = r.params.timeout_s
-                if t is not None and now - r.arrival > t:
-                    self.abort(r.rid, "timeout")
+        return [r.rid for q in (self.waiting, self.prefilling, self.running) for r in q
+                if r.params.timeout_s is not None and now - r.arrival > r.params.timeout_s]
+
+    def expire_deadlines(self) -> list[int]:
+        ids = self.expired()
+        for rid in ids:
+            self.abort(rid, "timeout")
+        return ids
 
     # ------------------------------------------------------------------ scheduling
     def _schedule_prefill(self, budget: int | None = None):

@@ -109,6 +109,9 @@ class LLMWorker:
         self._stop = True
         self._wake.set()
 
+    def join(self, timeout: float | None = None) -> None:
+        self._thread.join(timeout)
+
 
 def _sticky_device_error(exc: BaseException) -> bool:
     """HIP errors that leave the device context unusable (memory faults, illegal instructions,

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import glob
 import os
+import re
 
 import torch
 
@@ -71,13 +72,17 @@ def random_decoder_weights(cfg: DecoderConfig, device="cpu", dtype=torch.bfloat1
     H, F, D = cfg.hidden, cfg.intermediate, cfg.head_dim
     assert cfg.heads % tp_size == 0 and cfg.kv_heads % tp_size == 0 and F % tp_size == 0
     hq, hkv, f = cfg.heads // tp_size, cfg.kv_heads // tp_size, F // tp_size
-    g = _gen(device, seed * 1000003 + tp_rank)
+    # replicated tensors (embedding, LM head) are identical on every rank; the layer shards draw from
+    # a per-rank stream (tp_size == 1 keeps the single stream)
+    g = _gen(device, seed * 1000003)
     w = {
         "embed": _randn((cfg.vocab_size, H), g, device, dtype),
         "final_norm": torch.ones(H, device=device, dtype=dtype),
     }
     if not cfg.tie_embeddings:
         w["lm_head"] = _randn((cfg.vocab_size, H), g, device, dtype)
+    if tp_size > 1:
+        g = _gen(device, seed * 1000003 + 1 + tp_rank)
     for i in range(cfg.layers):
         w[f"l{i}.attn_norm"] = torch.ones(H, device=device, dtype=dtype)
         w[f"l{i}.qkv_w"] = _randn(((hq + 2 * hkv) * D, H), g, device, dtype)
@@ -96,7 +101,7 @@ def shard_decoder_weights(full: dict, cfg: DecoderConfig, tp_rank: int, tp_size:
     (column parallel), O / down by input columns (row parallel)."""
     H, F, D = cfg.hidden, cfg.intermediate, cfg.head_dim
     hq, hkv, f = cfg.heads // tp_size, cfg.kv_heads // tp_size, F // tp_size
-    out = {k: v for k, v in full.items() if not k.startswith("l")}
+    out = {k: v for k, v in full.items() if not re.match(r"l\d+\.", k)}  # embed, final_norm, lm_head
     for i in range(cfg.layers):
         qkv = full[f"l{i}.qkv_w"]
         q = qkv[: cfg.heads * D].view(cfg.heads, D, H)[tp_rank * hq:(tp_rank + 1) * hq].reshape(-1, H)

@@ -159,3 +159,13 @@ def test_llama_interleaved_mlp_layout_matches():
     h_a, _ = _prefill(LlamaModel(cfg, full, "cpu"), cfg, ids)
     h_b, _ = _prefill(LlamaModel(cfg, inter, "cpu", interleaved_mlp=True), cfg, ids)
     assert torch.allclose(h_a, h_b, atol=1e-5)
+
+
+def test_random_tp_shards_replicate_embedding_and_lm_head():
+    cfg = decoder_config("tiny-llama")
+    a = random_decoder_weights(cfg, dtype=torch.float32, seed=4, tp_rank=0, tp_size=2)
+    b = random_decoder_weights(cfg, dtype=torch.float32, seed=4, tp_rank=1, tp_size=2)
+    assert torch.equal(a["embed"], b["embed"]) and torch.equal(a["lm_head"], b["lm_head"])
+    assert not torch.equal(a["l0.qkv_w"], b["l0.qkv_w"])
+    full = random_decoder_weights(cfg, dtype=torch.float32, seed=4)
+    assert torch.equal(shard_decoder_weights(full, cfg, 1, 2)["lm_head"], full["lm_head"])

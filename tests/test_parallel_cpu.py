@@ -60,13 +60,15 @@ def _tp_body(info, out_path):
         ref_model = LlamaModel(cfg, full, "cpu")
         kv2 = KVCache(cfg.layers, 4, cfg.kv_heads, 64, cfg.head_dim, "cpu", dtype=torch.float32)
         ref = ref_model.forward(ids, meta, kv2)
-        torch.save({"err": (h - ref).abs().max().item()}, out_path)
+        lg_err = (model.logits(h) - ref_model.logits(ref)).abs().max().item()
+        torch.save({"err": (h - ref).abs().max().item(), "logits_err": lg_err}, out_path)
 
 
 def test_tensor_parallel_forward_matches_full_model(tmp_path):
     out = str(tmp_path / "tp.pt")
     _run(_tp_body, out)
-    assert torch.load(out, weights_only=True)["err"] < 1e-4
+    res = torch.load(out, weights_only=True)
+    assert res["err"] < 1e-4 and res["logits_err"] < 1e-4
 
 
 def _index_body(info, out_path):
@@ -158,3 +160,65 @@ def test_sharded_index_snapshot_reshards(tmp_path):
     s1, i1, d1 = single.search(q, 20)
     s2, i2, d2 = ref.search(q, 20)
     assert torch.equal(i1, i2) and torch.equal(d1, d2) and torch.allclose(s1, s2)
+
+
+def _tp_engine(cfg, weights, **kw):
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine
+
+    return LLMEngine(cfg, device="cpu", weights=weights, max_batch=4, block_size=16, num_blocks=64,
+                     max_prefill_tokens=64, use_graphs=False, interleaved_mlp=False, **kw)
+
+
+def _tp_requests():
+    from django_assistant_bot_amd.engine.llm_engine import SamplingParams
+
+    sp = SamplingParams(max_new_tokens=7, do_sample=False, temperature=0.0, ignore_eos=True)
+    return [(list(range(5, 5 + n)), sp) for n in (30, 90, 12, 50, 3)]  # 90 > 64: chunked prefill
+
+
+def _drive(engine):
+    reqs = _tp_requests()
+    rids = [engine.add_request(p, sp) for p, sp in reqs[:3]]
+    for _ in range(2):
+        engine.step()
+    rids += [engine.add_request(p, sp) for p, sp in reqs[3:]]  # arrive while others decode
+    engine.abort(rids[2])  # a client that went away
+    while engine.has_unfinished():
+        engine.step()
+    return [engine.pop_output(r).token_ids for r in rids]
+
+
+def _tp_serving_body(info, out_path):
+    from django_assistant_bot_amd.models.configs import decoder_config
+    from django_assistant_bot_amd.models.weights import random_decoder_weights, shard_decoder_weights
+    from django_assistant_bot_amd.parallel import dist as pdist
+    from django_assistant_bot_amd.parallel import tp_serving
+
+    cfg = decoder_config("tiny-llama")
+    full = random_decoder_weights(cfg, dtype=torch.float32, seed=21)
+    group, tp_rank, _ = pdist.tp_groups(WORLD)
+    ctrl = tp_serving.control_group(list(range(WORLD)))
+    eng = _tp_engine(cfg, shard_decoder_weights(full, cfg, tp_rank, WORLD), tp_group=group, tp_size=WORLD,
+                     tp_rank=tp_rank)
+    if info.rank == 0:
+        leader = tp_serving.TPLeader(eng, ctrl)
+        toks = _drive(leader)
+        leader.shutdown()
+        torch.save(toks, out_path)
+    else:
+        steps = tp_serving.follow(eng, ctrl)
+        assert steps > 5
+        assert not eng.has_unfinished()
+
+
+def test_tp_leader_follower_serving_matches_single_process(tmp_path):
+    out = str(tmp_path / "tp_tokens.pt")
+    _run(_tp_serving_body, out)
+    from django_assistant_bot_amd.models.configs import decoder_config
+    from django_assistant_bot_amd.models.weights import random_decoder_weights
+
+    cfg = decoder_config("tiny-llama")
+    ref = _drive(_tp_engine(cfg, random_decoder_weights(cfg, dtype=torch.float32, seed=21)))
+    got = torch.load(out, weights_only=True)
+    assert got == ref
+    assert [len(t) for t in got] == [7, 7, len(got[2]), 7, 7] and len(got[2]) < 7
