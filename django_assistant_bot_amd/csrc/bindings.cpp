@@ -29,6 +29,31 @@ static void check(int err, const char* name) {
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X (gfx950) kernels and native runtime of django_assistant_bot_amd";
   m.def("roctx_available", &dab::trace::available);
+  // one-shot all-reduce over IPC peer buffers (parallel/custom_allreduce.py)
+  m.def("allreduce_signal_bytes", &dab::allreduce_signal_bytes);
+  m.def("custom_allreduce", [](const std::vector<uintptr_t>& bases, int rank, u data, long nbytes, long half_bytes,
+                               long spin_limit, u s) {
+    check(dab::custom_allreduce(bases, rank, VP(data), nbytes, half_bytes, spin_limit, ST(s)), "custom_allreduce");
+  });
+  m.def("allreduce_buffer_alloc", [](long bytes) {
+    uintptr_t p = 0;
+    check(dab::allreduce_buffer_alloc(bytes, &p), "allreduce_buffer_alloc");
+    return p;
+  });
+  m.def("allreduce_buffer_free", [](u ptr) { check(dab::allreduce_buffer_free(ptr), "allreduce_buffer_free"); });
+  m.def("ipc_get_handle", [](u ptr) {
+    std::string h;
+    check(dab::ipc_get_handle(ptr, &h), "ipc_get_handle");
+    return py::bytes(h);
+  });
+  m.def("ipc_open_handle", [](const std::string& h) {
+    uintptr_t p = 0;
+    check(dab::ipc_open_handle(h, &p), "ipc_open_handle");
+    return p;
+  });
+  m.def("ipc_probe", [](u ptr) { check(dab::ipc_probe(ptr), "ipc_probe"); });
+  m.def("ipc_close_handle", [](u ptr) { check(dab::ipc_close_handle(ptr), "ipc_close_handle"); });
+  m.def("allreduce_error", &dab::allreduce_error, py::arg("base"), py::arg("clear") = 1);
   m.def("roctx_push", [](const std::string& name) { return dab::trace::range_push(name.c_str()); });
   m.def("roctx_pop", &dab::trace::range_pop);
   m.def("roctx_mark", [](const std::string& name) { dab::trace::mark(name.c_str()); });

@@ -1,0 +1,194 @@
+// One-shot all-reduce over IPC-mapped peer buffers, for tensor-parallel decode on one xGMI node.
+//
+// A TP decode step all-reduces a [batch, hidden] bf16 activation twice per layer.  That is 16 KB to
+// 2 MB, which is latency-bound.  RCCL's ring moves it in 2(W-1) serial hops over 2 of the 7 links.
+// Here every rank reads all W-1 peers directly, one xGMI hop each and all links at once
+// (SURVEY.md 5.8, 7.4 #5).
+//
+//   * Rank r owns one IPC allocation: a signal area, then two staging halves of `half_bytes`.
+//   * The grid size is fixed (AR_BLOCKS).  Block b owns a contiguous segment of the vector.  Per
+//     call, block b:
+//       1. copies its segment of the local input into staging[e & 1];
+//       2. writes system-scope release flags into every peer's signal area;
+//       3. waits for the W flags addressed to it;
+//       4. reads that segment from all W staging buffers;
+//       5. sums in fp32 in rank order 0..W-1, so every rank produces bitwise the same result;
+//       6. writes the result over the local input (in place).
+//   * The epoch e lives in device memory (one counter per block, advanced by the kernel).  A
+//     captured HIP graph replays correctly.
+//   * Parity double-buffers the staging.  A peer that is one call ahead writes the other half.  It
+//     cannot get two calls ahead, because its next barrier needs our flag.  One barrier per call
+//     is therefore enough.
+//   * Spins are bounded.  A missing peer sets `error` and the block moves on, so a broken group
+//     cannot hang the GPU.  The host checks `error` after synchronising.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+constexpr int AR_MAX_RANKS = 8;
+constexpr int AR_BLOCKS = 64;
+constexpr int AR_THREADS = 512;
+
+struct ArSignal {
+  uint32_t flag[AR_BLOCKS][AR_MAX_RANKS];  // flag[b][src]: latest epoch rank src reached in block b
+  uint32_t epoch[AR_BLOCKS];              // this rank's per-block call counter
+  uint32_t error;
+  uint32_t pad[63];
+};
+
+struct ArParams {
+  char* base[AR_MAX_RANKS];  // each rank's IPC allocation (signal area, then 2 staging halves)
+  bf16* data;                // local in/out
+  long n16;                  // 16-B vectors
+  long half_bytes;
+  int rank;
+  long spin_limit;
+};
+
+size_t allreduce_signal_bytes() { return (sizeof(ArSignal) + 4095) / 4096 * 4096; }
+
+template <int W>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArParams p) {
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const size_t sig_bytes = (sizeof(ArSignal) + 4095) / 4096 * 4096;
+  ArSignal* me = reinterpret_cast<ArSignal*>(p.base[p.rank]);
+  __shared__ uint32_t e_sh;
+  if (tid == 0) e_sh = me->epoch[b] + 1;
+  __syncthreads();
+  const uint32_t e = e_sh;
+  const size_t stage_off = sig_bytes + (size_t)(e & 1) * p.half_bytes;
+
+  const long per = (p.n16 + AR_BLOCKS - 1) / AR_BLOCKS;
+  const long s0 = min(p.n16, (long)b * per), s1 = min(p.n16, s0 + per);
+  u32x4* mine = reinterpret_cast<u32x4*>(p.base[p.rank] + stage_off);
+  const u32x4* src = reinterpret_cast<const u32x4*>(p.data);
+  for (long i = s0 + tid; i < s1; i += AR_THREADS) mine[i] = src[i];
+  __threadfence_system();  // staging visible to every peer before the flag
+  __syncthreads();
+  if (tid < W) {
+    ArSignal* peer = reinterpret_cast<ArSignal*>(p.base[tid]);
+    __hip_atomic_store(&peer->flag[b][p.rank], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    long spins = 0;
+    // >= : a peer already one call ahead has overwritten the flag with e + 1
+    while ((int)(__hip_atomic_load(&me->flag[b][tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (++spins > p.spin_limit) {
+        __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+
+  const u32x4* stage[W];
+#pragma unroll
+  for (int r = 0; r < W; ++r) stage[r] = reinterpret_cast<const u32x4*>(p.base[r] + stage_off);
+  u32x4* dst = reinterpret_cast<u32x4*>(p.data);
+  for (long i = s0 + tid; i < s1; i += AR_THREADS) {
+    u32x4 v[W];
+#pragma unroll
+    for (int r = 0; r < W; ++r) v[r] = __builtin_nontemporal_load(stage[r] + i);
+    float acc[8], t[8];
+    unpack8(v[0], acc);
+#pragma unroll
+    for (int r = 1; r < W; ++r) {
+      unpack8(v[r], t);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += t[j];
+    }
+    dst[i] = pack8(acc);
+  }
+  __syncthreads();
+  if (tid == 0) me->epoch[b] = e;
+}
+
+int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, long nbytes, long half_bytes,
+                     long spin_limit, hipStream_t s) {
+  const int W = (int)bases.size();
+  if (W < 1 || W > AR_MAX_RANKS || rank < 0 || rank >= W) return hipErrorInvalidValue;
+  if (nbytes % 16 || nbytes > half_bytes || ((uintptr_t)data & 15)) return hipErrorInvalidValue;
+  if (nbytes == 0) return 0;
+  ArParams p;
+  for (int r = 0; r < AR_MAX_RANKS; ++r) p.base[r] = r < W ? reinterpret_cast<char*>(bases[r]) : nullptr;
+  p.data = (bf16*)data;
+  p.n16 = nbytes / 16;
+  p.half_bytes = half_bytes;
+  p.rank = rank;
+  p.spin_limit = spin_limit;
+  const dim3 grid(AR_BLOCKS), block(AR_THREADS);
+  switch (W) {
+    case 1: hipLaunchKernelGGL(allreduce_kernel<1>, grid, block, 0, s, p); break;
+    case 2: hipLaunchKernelGGL(allreduce_kernel<2>, grid, block, 0, s, p); break;
+    case 3: hipLaunchKernelGGL(allreduce_kernel<3>, grid, block, 0, s, p); break;
+    case 4: hipLaunchKernelGGL(allreduce_kernel<4>, grid, block, 0, s, p); break;
+    case 5: hipLaunchKernelGGL(allreduce_kernel<5>, grid, block, 0, s, p); break;
+    case 6: hipLaunchKernelGGL(allreduce_kernel<6>, grid, block, 0, s, p); break;
+    case 7: hipLaunchKernelGGL(allreduce_kernel<7>, grid, block, 0, s, p); break;
+    default: hipLaunchKernelGGL(allreduce_kernel<8>, grid, block, 0, s, p); break;
+  }
+  return hipGetLastError();
+}
+
+// ---- IPC buffer management (host) ------------------------------------------------------------
+
+int allreduce_buffer_alloc(long bytes, uintptr_t* out) {
+  void* ptr = nullptr;
+  hipError_t err = hipMalloc(&ptr, (size_t)bytes);
+  if (err != hipSuccess) return err;
+  err = hipMemset(ptr, 0, (size_t)bytes);
+  if (err != hipSuccess) {
+    (void)hipFree(ptr);
+    return err;
+  }
+  *out = reinterpret_cast<uintptr_t>(ptr);
+  return hipDeviceSynchronize();
+}
+
+int allreduce_buffer_free(uintptr_t ptr) { return hipFree(reinterpret_cast<void*>(ptr)); }
+
+int ipc_get_handle(uintptr_t ptr, std::string* handle) {
+  hipIpcMemHandle_t h;
+  const hipError_t err = hipIpcGetMemHandle(&h, reinterpret_cast<void*>(ptr));
+  if (err != hipSuccess) return err;
+  handle->assign(reinterpret_cast<const char*>(&h), sizeof(h));
+  return 0;
+}
+
+int ipc_open_handle(const std::string& handle, uintptr_t* out) {
+  if (handle.size() != sizeof(hipIpcMemHandle_t)) return hipErrorInvalidValue;
+  hipIpcMemHandle_t h;
+  std::memcpy(&h, handle.data(), sizeof(h));
+  void* ptr = nullptr;
+  const hipError_t err = hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess);
+  if (err != hipSuccess) return err;
+  *out = reinterpret_cast<uintptr_t>(ptr);
+  return 0;
+}
+
+// host-driven read of a mapped peer buffer: a broken mapping fails here as an API error instead of
+// as a memory fault inside the all-reduce kernel
+int ipc_probe(uintptr_t ptr) {
+  uint32_t tmp[4];
+  const hipError_t err = hipMemcpy(tmp, reinterpret_cast<const void*>(ptr), sizeof(tmp), hipMemcpyDeviceToHost);
+  return err;
+}
+
+int ipc_close_handle(uintptr_t ptr) { return hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)); }
+
+int allreduce_error(uintptr_t base, int clear) {
+  uint32_t err = 0;
+  ArSignal* sig = reinterpret_cast<ArSignal*>(base);
+  if (hipMemcpy(&err, &sig->error, sizeof(err), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (clear && err) {
+    const uint32_t z = 0;
+    (void)hipMemcpy(&sig->error, &z, sizeof(z), hipMemcpyHostToDevice);
+  }
+  return (int)err;
+}
+
+}  // namespace dab

@@ -6,6 +6,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
 namespace dab {
 
 inline int div_up_host(int a, int b) { return (a + b - 1) / b; }
@@ -66,5 +69,17 @@ int sample_tokens_2stage(const void* logits, int logits_f32, long ld, int rows, 
                          int* out_tokens, void* workspace, size_t workspace_bytes, hipStream_t s);
 int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx,
                      int64_t index_base, int64_t* out_idx64, void* workspace, size_t workspace_bytes, hipStream_t s);
+
+// allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers (TP decode on one node)
+size_t allreduce_signal_bytes();
+int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, long nbytes, long half_bytes,
+                     long spin_limit, hipStream_t s);
+int allreduce_buffer_alloc(long bytes, uintptr_t* out);
+int allreduce_buffer_free(uintptr_t ptr);
+int ipc_get_handle(uintptr_t ptr, std::string* handle);
+int ipc_open_handle(const std::string& handle, uintptr_t* out);
+int ipc_close_handle(uintptr_t ptr);
+int ipc_probe(uintptr_t ptr);
+int allreduce_error(uintptr_t base, int clear);
 
 }  // namespace dab

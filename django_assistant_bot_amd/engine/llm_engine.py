@@ -115,6 +115,10 @@ class LLMEngine:
         self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
                                 interleaved_mlp=interleaved_mlp)
         del weights
+        if tp_size > 1 and self.is_gpu:
+            from ..parallel.custom_allreduce import maybe_create
+
+            self.model.custom_ar = maybe_create(tp_group, self.device, tp_size)
         self.tuned_gemms = 0
         if self.device.type == "cuda" and os.environ.get("DAB_GEMM_TUNING", "1") != "0":
             from ..ops import tuning

@@ -96,6 +96,7 @@ class LlamaModel:
         self.skinny_for = set(names) if sel == "all" else set() if sel == "none" else set(sel.split(","))
         self.use_skinny = bool(self.skinny_for)
         self._split_cache: dict = {}
+        self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -104,7 +105,12 @@ class LlamaModel:
         return self.embed.dtype
 
     def _all_reduce(self, x):
+        """TP partial sums: the one-shot IPC all-reduce for decode-sized messages when the engine
+        attached one (``custom_ar``), RCCL otherwise (prefill, CPU/gloo)."""
         if self.tp_size > 1:
+            ar = self.custom_ar
+            if ar is not None and ar.eligible(x):
+                return ar.all_reduce(x)
             import torch.distributed as dist
 
             dist.all_reduce(x, group=self.tp_group)

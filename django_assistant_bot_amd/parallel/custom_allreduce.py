@@ -1,0 +1,108 @@
+"""One-shot all-reduce over IPC-mapped peer buffers (kernel: csrc/kernels/allreduce.hip).
+
+For the latency-bound all-reduces of TP decode (2 per layer, [batch, hidden] bf16: 16 KB - 2 MB).
+Every rank reads all peers directly over xGMI, one hop on all 7 links at once.  RCCL's ring instead
+takes 2(W-1) serial steps over 2 of the links.  Larger messages (prefill) fall back to RCCL.
+
+    ar = CustomAllReduce(group, device)      # collective: exchanges IPC handles over `group`
+    ar.all_reduce(x)                         # in place; x bf16, contiguous, <= max_bytes
+    ar.close()
+
+The buffers come from hipMalloc, outside the torch caching allocator, so IPC handles cover the
+whole allocation.  Each rank has one buffer: a signal area plus two staging halves of
+``max_bytes``.  The kernel's epochs live on the device, so calls can be captured in HIP graphs.
+A peer that never arrives makes the kernel set an error flag instead of hanging;
+``check_error`` raises it on the host.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+from ..ops._lib import native, stream
+
+
+class CustomAllReduceError(RuntimeError):
+    pass
+
+
+class CustomAllReduce:
+    def __init__(self, group=None, device=None, max_bytes: int = 8 << 20, spin_limit: int = 1 << 24,
+                 exchange_group=None):
+        """``group``: the ranks that reduce together.  ``exchange_group``: where the IPC handles
+        travel; it defaults to ``group`` and may be a gloo group."""
+        self.group = group
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        if self.world > 8:
+            raise ValueError("one-shot all-reduce supports up to 8 ranks (one xGMI node)")
+        self.device = torch.device(device if device is not None else "cuda")
+        self.max_bytes = int(max_bytes)
+        self.spin_limit = int(spin_limit)
+        n = native()
+        self._n = n
+        sig = n.allreduce_signal_bytes()
+        with torch.cuda.device(self.device):
+            self.base = n.allreduce_buffer_alloc(sig + 2 * self.max_bytes)
+            handle = n.ipc_get_handle(self.base)
+            handles = [None] * self.world
+            if self.world > 1:
+                dist.all_gather_object(handles, handle, group=exchange_group or group)
+            else:
+                handles = [handle]
+            self.bases = [self.base if r == self.rank else n.ipc_open_handle(handles[r]) for r in range(self.world)]
+            for b in self.bases:
+                n.ipc_probe(b)  # a bad mapping raises here, never inside the kernel
+        self._closed = False
+        self._exchange = exchange_group or group
+        if self.world > 1:
+            dist.barrier(group=self._exchange)
+
+    def eligible(self, x: torch.Tensor) -> bool:
+        nb = x.numel() * x.element_size()
+        return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous() and nb % 16 == 0
+                and 0 < nb <= self.max_bytes and x.data_ptr() % 16 == 0)
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        """In-place sum over the group.  Every rank gets bitwise the same result, because the fp32
+        sum runs in rank order."""
+        if not self.eligible(x):
+            raise ValueError("custom all-reduce needs a contiguous bf16 CUDA tensor of <= max_bytes (16-B multiple)")
+        self._n.custom_allreduce(self.bases, self.rank, x.data_ptr(), x.numel() * 2, self.max_bytes, self.spin_limit,
+                                 stream(x))
+        return x
+
+    def check_error(self) -> None:
+        """Call after a synchronisation point: raises if a peer failed to arrive within the spin limit."""
+        if self._n.allreduce_error(self.base, 1):
+            raise CustomAllReduceError("custom all-reduce: a peer did not arrive (group broken or desynchronised)")
+
+    def close(self) -> None:
+        """Collective: no rank frees its buffer while a peer's last kernel may still read it."""
+        if self._closed:
+            return
+        self._closed = True
+        torch.cuda.synchronize(self.device)
+        if self.world > 1 and dist.is_initialized():
+            dist.barrier(group=self._exchange)
+        for r, b in enumerate(self.bases):
+            if r != self.rank:
+                self._n.ipc_close_handle(b)
+        self._n.allreduce_buffer_free(self.base)
+
+
+
+def maybe_create(group, device, world: int):
+    """The TP all-reduce for the model.  None (-> RCCL) when disabled (``DAB_CUSTOM_AR=0``), on one
+    rank, or when IPC mapping fails (e.g. ranks on different nodes)."""
+    if world <= 1 or os.environ.get("DAB_CUSTOM_AR", "1") == "0" or not torch.cuda.is_available():
+        return None
+    try:
+        return CustomAllReduce(group, device)
+    except Exception as exc:  # pragma: no cover - depends on the runtime
+        import logging
+
+        logging.getLogger(__name__).warning("custom all-reduce unavailable (%s); using RCCL", exc)
+        return None
