@@ -41,7 +41,7 @@ def gemm_suite(which):
     shapes += [("llama8b-lmhead", 64, 128256, 4096)]
     for M in (4096, 16384):
         shapes += [("llama8b-qkv", M, 6144, 4096), ("llama8b-gateup", M, 28672, 4096), ("llama8b-down", M, 4096, 14336)]
-    for M in (2048, 32768):
+    for M in (2048, 32768, 65536):
         shapes += [("bge-qkv", M, 2304, 768), ("bge-o", M, 768, 768), ("bge-up", M, 3072, 768), ("bge-down", M, 768, 3072)]
     shapes += [("index-scan", 64, 1_000_000, 768), ("index-scan", 512, 1_000_000, 768)]
     for name, M, N, K in shapes:

@@ -51,28 +51,33 @@ class EmbeddingEngine:
         lens = np.diff(offsets)
         order = np.argsort(-lens, kind="stable")
         out = torch.empty((n, self.cfg.hidden), dtype=out_dtype, device=self.device)
-        i = 0
         pin = self.device.type == "cuda"
+
+        def t(a):
+            x = torch.from_numpy(np.ascontiguousarray(a))
+            return (x.pin_memory() if pin else x).to(self.device, non_blocking=True)
+
+        # batch boundaries over the length-sorted order: greedy token budget (vectorised)
+        sorted_lens = lens[order]
+        csum = np.concatenate([[0], np.cumsum(sorted_lens)])
+        i = 0
         while i < n:
-            j, tok = i, 0
-            while j < n and (j == i or tok + lens[order[j]] <= self.max_batch_tokens):
-                tok += int(lens[order[j]])
-                j += 1
+            # last j with csum[j] - csum[i] <= budget (at least one text per batch)
+            j = int(np.searchsorted(csum, csum[i] + self.max_batch_tokens, side="right")) - 1
+            j = max(j, i + 1)
             idx = order[i:j]
-            seg_lens = lens[idx]
+            seg_lens = sorted_lens[i:j]
             cu = np.zeros(len(idx) + 1, dtype=np.int32)
             np.cumsum(seg_lens, out=cu[1:])
-            ids = np.concatenate([flat[offsets[k]:offsets[k + 1]] for k in idx]).astype(np.int32, copy=False)
-            pos = np.concatenate([np.arange(int(L), dtype=np.int32) for L in seg_lens])
-
-            def t(a):
-                x = torch.from_numpy(np.ascontiguousarray(a))
-                return (x.pin_memory() if pin else x).to(self.device, non_blocking=True)
-
+            total = int(cu[-1])
+            # gather index of every token of the batch and its position, without per-text slices
+            seg_start = np.repeat(cu[:-1], seg_lens)
+            pos = (np.arange(total, dtype=np.int64) - seg_start).astype(np.int32)
+            ids = flat[np.repeat(offsets[idx], seg_lens) + pos].astype(np.int32, copy=False)
             emb = self.model.encode(t(ids), t(pos), t(cu), int(seg_lens.max()), normalize=norm)
-            out[torch.from_numpy(idx).to(self.device)] = emb.to(out_dtype)
+            out[t(idx.astype(np.int64))] = emb.to(out_dtype)  # pinned + async: no stream sync per batch
             self.stats["batches"] += 1
-            self.stats["tokens"] += int(cu[-1])
+            self.stats["tokens"] += total
             i = j
         self.stats["texts"] += n
         return out

@@ -68,27 +68,41 @@ class VectorIndex:
         grp = np.zeros(n, dtype=np.int32) if groups is None else np.asarray(groups, dtype=np.int32)
         if (grp < 0).any():
             raise ValueError("groups must be >= 0 (negative marks deleted rows)")
-        rows = np.empty(n, dtype=np.int64)
-        fresh = []
-        for i, x in enumerate(ids.tolist()):
-            r = self._row_of.get(x)
-            if r is None:
-                fresh.append(i)
-            else:
-                rows[i] = r
-        if fresh:
-            need = self.n + len(fresh)
-            if need > self._cap:
-                self._grow(max(need, 2 * self._cap))
-            for j, i in enumerate(fresh):
-                rows[i] = self.n + j
-                self._row_of[int(ids[i])] = self.n + j
-            self.n += len(fresh)
-        r = torch.from_numpy(rows).to(self.device)
+        idl = ids.tolist()
+        if len(set(idl)) == n and not (self._row_of.keys() & set(idl)):
+            # bulk insert of new ids (ingest): C-speed bookkeeping, contiguous rows
+            if self.n + n > self._cap:
+                self._grow(max(self.n + n, 2 * self._cap))
+            rows = np.arange(self.n, self.n + n, dtype=np.int64)
+            self._row_of.update(zip(idl, range(self.n, self.n + n)))
+            self.n += n
+        else:
+            rows = np.empty(n, dtype=np.int64)
+            fresh = []
+            for i, x in enumerate(idl):
+                r = self._row_of.get(x)
+                if r is None:
+                    fresh.append(i)
+                else:
+                    rows[i] = r
+            if fresh:
+                need = self.n + len(fresh)
+                if need > self._cap:
+                    self._grow(max(need, 2 * self._cap))
+                for j, i in enumerate(fresh):
+                    rows[i] = self.n + j
+                    self._row_of[idl[i]] = self.n + j
+                self.n += len(fresh)
+        pin = self.device.type == "cuda"
+
+        def dev(a):
+            x = torch.from_numpy(np.ascontiguousarray(a))
+            return (x.pin_memory() if pin else x).to(self.device, non_blocking=True)
+        r = dev(rows)
         self.vecs[r] = v
-        self.row_ids[r] = torch.from_numpy(ids).to(self.device)
-        self.row_docs[r] = torch.from_numpy(docs).to(self.device)
-        self.row_group[r] = torch.from_numpy(grp).to(self.device)
+        self.row_ids[r] = dev(ids)
+        self.row_docs[r] = dev(docs)
+        self.row_group[r] = dev(grp)
 
     def remove(self, ids) -> int:
         rows = [self._row_of.pop(int(x)) for x in np.asarray(ids).reshape(-1).tolist() if int(x) in self._row_of]

@@ -31,14 +31,29 @@ def embed_corpus(engine, text_of: Callable[[int], str], n: int, rank: int = 0, w
     ids = owned_ids(n, rank, world, first_id)
     keep = [] if (index is None or gather) else None
     out_vecs = []
-    for s in range(0, len(ids), chunk):
+    # the next chunk is tokenised on a helper thread (the native tokenizer releases the GIL) while
+    # this chunk's batches run on the GPU
+    from concurrent.futures import ThreadPoolExecutor
+
+    def tokenize(s):
+        return engine.tokenize([text_of(int(i)) for i in ids[s:s + chunk]])
+
+    starts = list(range(0, len(ids), chunk))
+    pool = ThreadPoolExecutor(1) if len(starts) > 1 else None
+    nxt = pool.submit(tokenize, starts[0]) if pool else None
+    for k, s in enumerate(starts):
         part = ids[s:s + chunk]
-        v = engine.embed([text_of(int(i)) for i in part], out_dtype=torch.float32)
+        flat, offs = nxt.result() if pool else tokenize(s)
+        if pool and k + 1 < len(starts):
+            nxt = pool.submit(tokenize, starts[k + 1])
+        v = engine.embed_tokens(np.asarray(flat), np.asarray(offs), out_dtype=torch.float32)
         if index is not None:
             target = getattr(index, "local", index)  # ShardedIndex -> its local VectorIndex (we own these ids)
             target.add(part, v, doc_ids=None if doc_of is None else doc_of(part))
         if keep is not None or gather:
             out_vecs.append(v)
+    if pool:
+        pool.shutdown()
     local = torch.cat(out_vecs) if out_vecs else None
     total = len(ids)
     if world > 1 and dist.is_initialized():
