@@ -109,6 +109,9 @@ def main():
     ap.add_argument("--batch", type=int, default=128,
                     help="questions in flight per GPU (serve) / per batch (batch); one step = this many answers")
     ap.add_argument("--admit-group", type=int, default=16, help="serve: questions retrieved + queued together")
+    ap.add_argument("--qps", type=float, default=0.0,
+                    help="serve: open-loop arrivals at this rate per replica (fixed-QPS load, BASELINE config 5); "
+                         "latency then counts from the scheduled arrival, queueing included")
     ap.add_argument("--mixed-tokens", type=int, default=2048,
                     help="serve: prompt tokens mixed into one decode step (0: separate prefill steps)")
     ap.add_argument("--max-new-tokens", type=int, default=256)
@@ -229,17 +232,28 @@ def main():
         warm_n, total_n = args.warmup * B, n_steps * B
         t0 = None
         stats0, t0 = (sync_start() if warm_n == 0 else (None, None))
+        arrival_of: dict = {}
+        t_open = time.perf_counter()
         while done < total_n:
-            while (rag.in_flight + G <= B and next_q + G <= len(my_q)
+            if args.qps > 0:  # open loop: everything scheduled to have arrived by now is submitted
+                due = min(len(my_q), int((time.perf_counter() - t_open) * args.qps) + 1)
+                if due > next_q:
+                    rids = rag.submit(my_q[next_q:due], params, bot_group=0)
+                    for j, rid in enumerate(rids):
+                        arrival_of[rid] = t_open + (next_q + j) / args.qps
+                    admitted += due - next_q
+                    next_q = due
+            while (args.qps <= 0 and rag.in_flight + G <= B and next_q + G <= len(my_q)
                    and (admitted >= B or llm.stats["decode_steps"] >= next_admit)):
                 rag.submit(my_q[next_q:next_q + G], params, bot_group=0)
                 next_q += G
                 admitted += G
                 next_admit += pace
-            for _, r in rag.poll():
+            for rid, r in rag.poll():
                 done += 1
                 if t0 is not None:
-                    latencies.append(r.latency_s)
+                    sched = arrival_of.pop(rid, None)
+                    latencies.append(time.perf_counter() - sched if sched is not None else r.latency_s)
                     prompt_lens.append(r.usage["prompt_tokens"])
                     n_docs_used.append(len(r.documents))
                     phases["retrieve_s"].append(r.debug_info["took"])
@@ -293,8 +307,10 @@ def main():
             "seq_len": int(np.mean(prompt_lens)) if prompt_lens else 0,
             "max_new_tokens": args.max_new_tokens,
             "parallelism": f"dp{n_rep}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
-            "mode": (f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"
-                     if serve else "batch"),
+            "mode": ("batch" if not serve else
+                     f"serve (open loop, {args.qps} q/s per replica offered, max batch {B}, mixed {args.mixed_tokens})"
+                     if args.qps > 0 else
+                     f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"),
             "index_rows": n_rows,
             "index": "replicated per GPU" if serve else "sharded (all-gather merge)",
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
