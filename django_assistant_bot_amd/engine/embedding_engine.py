@@ -28,7 +28,9 @@ class EmbeddingEngine:
 
                 weights = load_encoder_checkpoint(checkpoint, self.cfg)
             else:
-                weights = random_encoder_weights(self.cfg, self.device, seed=seed)
+                # bf16 on the GPU (MFMA); fp32 on the CPU, where bf16 GEMMs have no fast path
+                dtype = torch.bfloat16 if self.device.type == "cuda" else torch.float32
+                weights = random_encoder_weights(self.cfg, self.device, seed=seed, dtype=dtype)
         self.model = BertEncoder(self.cfg, weights, self.device)
         self.tokenizer = Tokenizer.for_encoder(self.cfg, checkpoint)
         self.max_batch_tokens = max_batch_tokens

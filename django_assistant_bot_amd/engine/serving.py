@@ -128,6 +128,7 @@ class EmbedWorker:
         self.max_wait_s = max_wait_s
         self.max_batch_texts = max_batch_texts
         self._inbox: queue.Queue = queue.Queue()
+        self._concurrent = False
         self.requests = 0
         self._thread = threading.Thread(target=self._run, name="dab-embed-worker", daemon=True)
         self._thread.start()
@@ -145,17 +146,19 @@ class EmbedWorker:
             first = self._inbox.get()
             batch = [first]
             n = len(first[0])
-            deadline = time.perf_counter() + self.max_wait_s
+            # wait for company only when callers have recently been concurrent; a lone sequential
+            # client gets no added latency (requests already queued are always taken)
+            wait = self.max_wait_s if self._concurrent else 0.0
+            deadline = time.perf_counter() + wait
             while n < self.max_batch_texts:
                 left = deadline - time.perf_counter()
-                if left <= 0:
-                    break
                 try:
-                    item = self._inbox.get(timeout=left)
+                    item = self._inbox.get(timeout=left) if left > 0 else self._inbox.get_nowait()
                 except queue.Empty:
                     break
                 batch.append(item)
                 n += len(item[0])
+            self._concurrent = len(batch) > 1 or not self._inbox.empty()
             groups: dict = {}
             for texts, norm, fut in batch:
                 groups.setdefault(norm, []).append((texts, fut))
@@ -195,8 +198,14 @@ def setting(name: str, default):
 
 
 def engine_device():
+    """``GPU_SERVICE_DEVICE`` (e.g. ``cpu`` for the plumbing-only config) overrides the default."""
+    import os
+
     import torch
 
+    forced = os.environ.get("GPU_SERVICE_DEVICE")
+    if forced:
+        return forced
     return "cuda" if torch.cuda.is_available() else "cpu"
 
 
