@@ -122,6 +122,14 @@ PYBIND11_MODULE(_native, m) {
                        (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s)),
           "gemm_bt");
   });
+  m.def("gemm_score_candidates", [](u A, long lda, u B, long ldb, int M, int N, int K, u row_group, u q_group, u thr,
+                                    u cnt, u cand_val, u cand_idx, int cap, u s) {
+    check(dab::gemm_score_candidates(CVP(A), lda, CVP(B), ldb, M, N, K, reinterpret_cast<const int*>(row_group),
+                                     reinterpret_cast<const int*>(q_group), reinterpret_cast<const float*>(thr),
+                                     reinterpret_cast<int*>(cnt), reinterpret_cast<float*>(cand_val),
+                                     reinterpret_cast<int*>(cand_idx), cap, ST(s)),
+          "gemm_score_candidates");
+  });
   m.def("skinny_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
                           int S, int epilogue, u s, int nt) {
     check(dab::skinny_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt),

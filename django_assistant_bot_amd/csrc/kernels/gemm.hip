@@ -20,7 +20,7 @@
 
 namespace dab {
 
-enum EpiMode { EPI_NONE = 0, EPI_GELU = 1, EPI_SWIGLU = 2, EPI_SCORES = 3 };
+enum EpiMode { EPI_NONE = 0, EPI_GELU = 1, EPI_SWIGLU = 2, EPI_SCORES = 3, EPI_CANDIDATES = 4 };
 
 struct GemmParams {
   const bf16* A;
@@ -35,6 +35,13 @@ struct GemmParams {
   long lda, ldb, ldc, ldr;
   int allow_words;
   int out_f32;
+  // EPI_CANDIDATES: filtered scores >= thr[m] are appended to query m's candidate list instead of
+  // writing the [M, N] score matrix (exact threshold top-k, see VectorIndex.search)
+  const float* thr;  // [M]
+  int* cnt;          // [M] appended count (may exceed cap: overflow, caller falls back)
+  float* cand_val;   // [M, cap]
+  int* cand_idx;     // [M, cap] column n
+  int cap;
 };
 
 __device__ __forceinline__ int gsw(int r) { return 2 * ((r >> 1) & 3); }
@@ -157,7 +164,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
       float o[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = acc[ni][mi][r];
-      if (EPI == EPI_SCORES) {
+      if (EPI == EPI_SCORES || EPI == EPI_CANDIDATES) {
         const int qg = p.q_group ? p.q_group[m] : -1;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -168,6 +175,20 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
           }
           if (p.allow) ok = ok && ((p.allow[(size_t)m * p.allow_words + ((n + r) >> 5)] >> ((n + r) & 31)) & 1u);
           if (!ok) o[r] = -__builtin_huge_valf();
+        }
+        if (EPI == EPI_CANDIDATES) {
+          const float t = p.thr[m];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (o[r] >= t && o[r] != -__builtin_huge_valf()) {
+              const int slot = atomicAdd(p.cnt + m, 1);
+              if (slot < p.cap) {
+                p.cand_val[(size_t)m * p.cap + slot] = o[r];
+                p.cand_idx[(size_t)m * p.cap + slot] = n + r;
+              }
+            }
+          }
+          continue;  // no score matrix
         }
       } else {
         if (p.bias) {
@@ -242,6 +263,31 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
     case EPI_SCORES: return launch_gemm<EPI_SCORES>(p, big, s);
     default: return hipErrorInvalidValue;
   }
+}
+
+int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
+                          const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                          hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 64 || N % 4 || lda % 8 || ldb % 8 || cap <= 0 || !thr || !cnt || !cand_val || !cand_idx)
+    return hipErrorInvalidValue;
+  GemmParams p{};
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.row_group = row_group;
+  p.q_group = q_group;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.thr = thr;
+  p.cnt = cnt;
+  p.cand_val = cand_val;
+  p.cand_idx = cand_idx;
+  p.cap = cap;
+  const bool big = M >= 2048 && N >= 512 && ((long)((M + 255) / 256) * ((N + 255) / 256)) >= 160;
+  return launch_gemm<EPI_CANDIDATES>(p, big, s);
 }
 
 }  // namespace dab

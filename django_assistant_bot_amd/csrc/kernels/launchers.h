@@ -70,6 +70,11 @@ int sample_tokens_2stage(const void* logits, int logits_f32, long ld, int rows, 
 int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx,
                      int64_t index_base, int64_t* out_idx64, void* workspace, size_t workspace_bytes, hipStream_t s);
 
+// gemm.hip: scores >= thr[m] appended per query (exact threshold top-k of the vector index)
+int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
+                          const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                          hipStream_t s);
+
 // allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers (TP decode on one node)
 size_t allreduce_signal_bytes();
 int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, long nbytes, long half_bytes,

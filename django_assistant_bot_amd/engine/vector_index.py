@@ -28,6 +28,7 @@ class VectorIndex:
         self.dtype = dtype
         self._cap = 0
         self.n = 0  # rows in use (live + tombstoned)
+        self.stats = {"threshold_searches": 0, "threshold_overflows": 0}
         self.vecs = self.row_ids = self.row_docs = self.row_group = None
         self._row_of: dict[int, int] = {}
         self._dead = 0
@@ -48,6 +49,11 @@ class VectorIndex:
             grp[: self.n] = self.row_group[: self.n]
         self.vecs, self.row_ids, self.row_docs, self.row_group = vecs, ids, docs, grp
         self._cap = cap
+
+    # exact threshold search (no score matrix) for large indexes on the GPU: see _threshold_search
+    threshold_search = True
+    threshold_min_rows = 1 << 19
+    sample_stride = 16
 
     def __len__(self) -> int:
         return len(self._row_of)
@@ -161,9 +167,16 @@ class VectorIndex:
         if self.n == 0 or k <= 0:
             z = torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=self.device)
             return torch.full((nq, max(k, 0)), float("-inf"), device=self.device), z, z.clone()
-        s = self.scores(queries, q_groups, allowed)
-        kk = min(k, s.shape[1], 1024)
-        vals, rows = ops.topk_rows(s, kk)
+        got = None
+        if (self.device.type == "cuda" and allowed is None and self.n >= self.threshold_min_rows
+                and k <= 1024 and self.threshold_search):
+            got = self._threshold_search(queries, k, q_groups)
+        if got is not None:
+            vals, rows = got
+        else:
+            s = self.scores(queries, q_groups, allowed)
+            kk = min(k, s.shape[1], 1024)
+            vals, rows = ops.topk_rows(s, kk)
         rows = rows.long()
         ids = self.row_ids[rows]
         docs = self.row_docs[rows]
@@ -171,6 +184,35 @@ class VectorIndex:
         ids = ids.masked_fill(dead, -1)
         docs = docs.masked_fill(dead, -1)
         return vals, ids, docs
+
+    def _threshold_search(self, queries, k: int, q_groups=None):
+        """Exact top-k without the [q, n] score matrix.  The k-th best score over a strided 1/16
+        sample of the rows is a lower bound for the k-th best over all rows.  So the score GEMM
+        appends only scores >= that bound (about 16k per query on unstructured data), and an exact
+        top-k runs over those.  Returns None when a candidate list overflowed; the caller then
+        takes the full path."""
+        q = F.normalize(torch.as_tensor(queries).to(self.device, torch.float32), dim=-1).to(self.dtype)
+        qg = None if q_groups is None else torch.as_tensor(q_groups, dtype=torch.int32).to(self.device)
+        n4 = (self.n + 3) // 4 * 4
+        ns = (self.n // self.sample_stride) // 4 * 4
+        if ns < k:  # the sample's k-th best is a valid bound only if the sample holds k rows
+            return None
+        kk = k
+        samp = self.vecs[: ns * self.sample_stride: self.sample_stride]
+        samp_group = self.row_group[: ns * self.sample_stride: self.sample_stride].contiguous()
+        s_scores = ops.gemm_bt(q, samp, epilogue=ops.EPI_SCORES, out_f32=True, row_group=samp_group, q_group=qg)
+        tv, _ = ops.topk_rows(s_scores, kk)
+        del s_scores
+        thr = tv[:, kk - 1].contiguous()
+        cap = max(4096, 64 * k * self.sample_stride // 16)
+        cand_val, cand_idx, cnt = ops.score_candidates(q, self.vecs[:n4], thr, cap, self.row_group[:n4], qg)
+        if int(cnt.max()) > cap:
+            self.stats["threshold_overflows"] += 1
+            return None
+        self.stats["threshold_searches"] += 1
+        vals, pos = ops.topk_rows(cand_val, min(k, cap))
+        rows = torch.gather(cand_idx, 1, pos.long())
+        return vals, rows.masked_fill(torch.isinf(vals), 0)
 
     # ------------------------------------------------------------------ persistence
     def save(self, path: str) -> None:

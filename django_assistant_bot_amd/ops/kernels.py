@@ -329,6 +329,31 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     return out
 
 
+def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
+    """Filtered cosine scores of A [M, K] against B [N, K] that are >= thr[m], appended per query
+    (no [M, N] score matrix).  -> (cand_val fp32 [M, cap] (-inf padded), cand_idx int32 [M, cap],
+    count int32 [M]; count > cap means the list overflowed)."""
+    expect(A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 CUDA operands required")
+    expect(A.stride(-1) == 1 and B.stride(-1) == 1 and A.stride(0) % 8 == 0 and B.stride(0) % 8 == 0,
+           "operands must be K-contiguous with row strides % 8 == 0")
+    M, K = A.shape
+    N = B.shape[0]
+    expect(B.shape[1] == K and K % 64 == 0 and N % 4 == 0, "score_candidates needs K % 64 == 0 and N % 4 == 0")
+    expect(thr.dtype == torch.float32 and thr.is_contiguous() and thr.numel() >= M, "thr must be fp32 [M]")
+    if row_group is not None:
+        _i32(row_group)
+        expect(row_group.numel() >= N, "row_group shorter than N")
+    if q_group is not None:
+        _i32(q_group)
+        expect(q_group.numel() >= M, "q_group shorter than M")
+    cand_val = torch.full((M, cap), float("-inf"), dtype=torch.float32, device=A.device)
+    cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
+    cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
+    native().gemm_score_candidates(ptr(A), A.stride(0), ptr(B), B.stride(0), M, N, K, ptr(row_group), ptr(q_group),
+                                   ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
+    return cand_val, cand_idx, cnt
+
+
 SKINNY_MAX_M = 128
 _SK_KSTAGE = 256
 
