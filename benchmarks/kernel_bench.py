@@ -121,6 +121,77 @@ def skinny_sweep(which):
             del ws
 
 
+def graph_time(calls, reps=5):
+    """Device time per call of a list of zero-arg launches, captured into one HIP graph and replayed
+    (no host launch overhead in the number: the decode step replays a graph too)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for f in calls:
+            f()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        for f in calls:
+            f()
+    g.replay()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        g.replay()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / 1e3 / len(calls))
+    del g
+    return best
+
+
+def stream_sweep(which, Ms=(128,)):
+    """Decode projections of Llama-3-8B (+ LM head) at decode batch M with cold weights (a rotation
+    of > 2 GB of weight copies, as in a decode step that streams 16 GB): hipBLASLt vs the split-K
+    skinny kernel vs the warp-specialised stream kernel per configuration and split count.  Graph-
+    timed, microseconds per call."""
+    shapes = (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
+              ("lm_head", 128256, 4096))
+    n_cfg = 17
+    cfgs = [int(c) for c in os.environ.get("STREAM_CFGS", "").split(",") if c] or list(range(n_cfg))
+    for M in Ms:
+        for name, N, K in shapes:
+            if which and which not in name:
+                continue
+            a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+            ncopy = max(2, int(2.5e9 // (N * K * 2)) + 1)
+            ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
+            res = {"op": name, "M": M, "N": N, "K": K, "weights_mb": round(N * K * 2 / 1e6, 1)}
+            res["hipblaslt_us"] = round(graph_time([lambda w=w: F.linear(a, w) for w in ws]) * 1e6, 1)
+            if M <= ops.SKINNY_MAX_M and N % 64 == 0:
+                S = ops.skinny_splits(N, K)
+                slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
+                res[f"skinny_S{S}_us"] = round(graph_time(
+                    [lambda w=w: ops.skinny_gemm(a, w, splits=S, out=slabs) for w in ws]) * 1e6, 1)
+            for cfg in cfgs:
+                bn, mm = ops.native().stream_gemm_bn(cfg), ops.native().stream_gemm_max_m(cfg)
+                if M > mm or N % bn:
+                    continue
+                wl = ws if not ops.native().stream_gemm_shuffled(cfg) else [ops.shuffle_weights(w) for w in ws]
+                for S in (1, 2, 4, 8):
+                    if K % (S * 128) or (N // bn) * S > 2048 or (N // bn) * S < 96:
+                        continue
+                    slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
+                    for nt in ((0, 1) if os.environ.get("STREAM_NT") else (0,)):
+                        t = graph_time([lambda w=w: ops.stream_gemm(a, w, splits=S, out=slabs, nt=nt, cfg=cfg)
+                                        for w in wl])
+                        res[f"c{cfg}_S{S}{'nt' if nt else ''}_us"] = round(t * 1e6, 1)
+            best = min((v, k) for k, v in res.items() if k.endswith("_us"))
+            res["best"] = best[1]
+            res["best_tbps"] = round(N * K * 2 / best[0] / 1e12, 2)
+            emit(**res)
+            del ws
+
+
 def attn_suite():
     # prefill: 16 sequences x 1024 tokens, Llama-3-8B heads
     B, T, Hq, Hkv, D, bs = 16, 1024, 32, 8, 128, 64
@@ -215,6 +286,9 @@ if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
     if which == "skinny":
         skinny_sweep(sys.argv[2] if len(sys.argv) > 2 else None)
+    if which == "stream":
+        stream_sweep(sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else None,
+                     tuple(int(m) for m in sys.argv[3].split(",")) if len(sys.argv) > 3 else (128,))
     if which == "decode":
         decode_sweep()
     if which in ("all", "gemm"):

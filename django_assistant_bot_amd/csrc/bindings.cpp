@@ -137,6 +137,15 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
      py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
      py::arg("nt") = 0);
+  m.def("stream_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
+                          int S, int epilogue, u s, int nt, int cfg) {
+    check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
+                           cfg),
+          "stream_gemm");
+  });
+  m.def("stream_gemm_bn", &dab::stream_gemm_bn);
+  m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
+  m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);
   m.def("skinny_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
     check(dab::skinny_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "skinny_reduce");
   });

@@ -78,7 +78,28 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     const float* src = slabs + (size_t)t * ld + (size_t)h * D;
 #pragma unroll
     for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
-    for (int sl = 0; sl < S; ++sl, src += slab_stride) {
+    int sl = 0;
+    for (; sl + 2 <= S; sl += 2, src += 2 * slab_stride) {  // two slabs' loads in flight per round
+      f32x4 a0[2], a1[2], b0[2], b1[2];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const float* sq = src + q * slab_stride;
+        a0[q] = *reinterpret_cast<const f32x4*>(sq + i0);
+        a1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + 4);
+        b0[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half);
+        b1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half + 4);
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x1[j] += a0[q][j];
+          x1[4 + j] += a1[q][j];
+          x2[j] += b0[q][j];
+          x2[4 + j] += b1[q][j];
+        }
+    }
+    for (; sl < S; ++sl, src += slab_stride) {
       const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + i0), a1 = *reinterpret_cast<const f32x4*>(src + i0 + 4);
       const f32x4 b0 = *reinterpret_cast<const f32x4*>(src + i0 + half);
       const f32x4 b1 = *reinterpret_cast<const f32x4*>(src + i0 + half + 4);

@@ -56,6 +56,14 @@ int skinny_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
 int skinny_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
                   hipStream_t s);
 
+// stream_gemm.hip (warp-specialised decode GEMM, M <= 128; same outputs as skinny_gemm; cfg selects
+// the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
+int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
+int stream_gemm_bn(int cfg);
+int stream_gemm_max_m(int cfg);
+int stream_gemm_shuffled(int cfg);  // 1: cfg reads weights in the ops.shuffle_weights layout
+
 // select.hip
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
                   const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,

@@ -1,0 +1,360 @@
+// Warp-specialised weight-streaming MFMA GEMM for decode batches:  C[M, N] = X[M, K] . W[N, K]^T,
+// M <= 128.  Successor of skinny_gemm.hip at M 65..128 (and an alternative at M <= 64).
+//
+// Why a second decode kernel: at M = 128 the single-queue design of skinny_gemm waits, every stage,
+// for an X load that sits behind the newest weight loads in the wave's in-order vmcnt queue, so at
+// most ~1.5 stages of weights are ever in flight and each 16-33 MB projection runs at 2-3 TB/s
+// (profiles/decode_gemm_m128_study.md).  Here the two operands travel on different waves:
+//
+//   * 4 compute waves stream W straight into VGPRs (MFMA A fragments, 16-B buffer loads) through an
+//     NWIN-stage register ring: a slot is reloaded NWIN stages ahead right behind its MFMAs, and
+//     since these waves issue nothing but weight loads, the compiler's in-order vmcnt waits only
+//     ever wait for the oldest slot (NWIN x 4-8 KB per wave in flight, ~100 KB per CU);
+//   * 1 loader wave stages X (L2-resident, shared by the compute waves) into an NB-deep LDS ring
+//     with global_load_lds (no VGPRs, source-swizzled so the image is lane-linear), retires each
+//     stage with a counted vmcnt and publishes it with the stage barrier (raw s_barrier: every wave
+//     passes one barrier per stage, nobody drains a queue at it);
+//   * waves = KG k-groups x (4 / KG) row groups of RT 16-row tiles; v_mfma_f32_16x16x32_bf16 with W
+//     as A and X as B (one LDS fragment feeds RT MFMAs); partial tiles of the k-groups meet in LDS.
+//
+// Outputs as skinny_gemm: S == 1 -> bf16 (optional residual add, or SwiGLU over 16-row interleaved
+// [gate | up] weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue
+// (rmsnorm / rope+KV write) or by skinny_reduce.  Block -> (tile, slice) keeps a tile's slices on
+// one XCD (bijective remap, slice-minor).
+#include <type_traits>
+
+#include "common.h"
+#include "launchers.h"
+
+#define DAB_INLINE __attribute__((always_inline))
+
+namespace dab {
+
+struct StreamParams {
+  const bf16* X;
+  long ldx;
+  const bf16* W;
+  long ldw;
+  void* out;
+  long ldo;
+  const bf16* residual;
+  long ldr;
+  int M, N, K, S, kc;
+  int epi;  // 0 none, 2 swiglu
+};
+
+constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2;
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
+
+// vmcnt(N) with expcnt / lgkmcnt left unconstrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xc07f); }
+
+// f(integral_constant<I>) for I in [B, E) while it returns true
+template <int B, int E, typename F>
+__device__ __forceinline__ bool static_for(F&& f) {
+  if constexpr (B < E) {
+    if (!f(std::integral_constant<int, B>{})) return false;
+    return static_for<B + 1, E>(f);
+  }
+  return true;
+}
+
+template <int MT, int RT, int KG, int KS, int NB, int NWIN, int NL, bool SHUF, bool NT_W>
+__global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamParams p) {
+  constexpr int NWC = 4;              // compute waves (waves 4.. are the NL X loaders)
+  constexpr int RG = NWC / KG;        // row groups
+  constexpr int BN = 16 * RT * RG;    // weight rows per workgroup
+  constexpr int MP = 16 * MT;         // padded M
+  constexpr int ROWB = KS * 2;        // bytes per staged X row
+  constexpr int CPR = KS / 8;         // 16-B chunks per staged row
+  constexpr int XBUF = MP * ROWB;     // bytes per X stage
+  constexpr int GPS = XBUF / 1024;    // global_load_lds per stage (64 lanes x 16 B), all loaders
+  constexpr int GPL = GPS / NL;       // ... per loader wave
+  constexpr int KW = KS / KG;         // k per compute wave per stage
+  constexpr int CPW = KW / 32;        // 32-deep MFMA chunks per wave per stage
+  constexpr int RED = KG * MP * BN * 4;
+  constexpr int SMEM = NB * XBUF > RED ? NB * XBUF : RED;
+  static_assert(CPR >= 16 && CPW >= 1 && KW % 32 == 0, "stage shape");
+  static_assert(NB >= 2 && (NB - 2) * GPL <= 63 && GPS % NL == 0, "loader vmcnt range");
+  static_assert(NWC % KG == 0, "k groups");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tiles = p.N / BN;
+  const int nwg = tiles * p.S;
+  const int bid = blockIdx.x;
+  const int xcd = bid % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int tile = sid / p.S, slice = sid % p.S;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int n0 = tile * BN;
+  const int k_begin = slice * p.kc;
+  const int nst = p.kc / KS;
+
+  float* red = reinterpret_cast<float*>(smem);  // epilogue partials (after the K loop)
+  if (w >= NWC) {
+    // ------------------------------------------------------------------ X loader waves
+    // loader l issues instructions i = l, l + NL, ... of each stage (1 KB each)
+    const int l = w - NWC;
+    // stage s image: row r (= m), physical chunk pc holds logical chunk pc ^ (r & 15); rows >= M
+    // repeat row M-1 (their outputs are never stored)
+    const bf16* xk = p.X + k_begin;
+    auto issue = [&](int s) DAB_INLINE {
+      char* buf = smem + (s % NB) * XBUF;
+#pragma unroll
+      for (int j = 0; j < GPL; ++j) {
+        const int i = j * NL + l;
+        const int e = i * 64 + lane;
+        const int r = e / CPR, pc = e % CPR;
+        const bf16* src = xk + (size_t)min(r, p.M - 1) * p.ldx + s * KS + (pc ^ (r & 15)) * 8;
+        __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(buf + i * 1024),
+                                         16, 0, 0);
+      }
+    };
+    // retire everything but the newest `n` stages (n <= NB - 2)
+    auto retire = [&](int n) DAB_INLINE {
+      static_for<0, NB - 1>([&](auto I) DAB_INLINE {
+        constexpr int i = decltype(I)::value;
+        if (n == i) wait_vm<i * GPL>();
+        return true;
+      });
+    };
+    const int pre = min(NB - 1, nst);
+    for (int s = 0; s < pre; ++s) issue(s);
+    retire(pre - 1);
+    __builtin_amdgcn_s_barrier();
+    for (int st = 0; st < nst; ++st) {
+      if (st + NB - 1 < nst) issue(st + NB - 1);  // into the buffer read in stage st - 1
+      if (st + 1 < nst) retire(min(st + NB - 1, nst - 1) - (st + 1));
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    // ------------------------------------------------------------------ compute waves
+    const int rg = w / KG, kg = w % KG;
+    const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)n0 * p.ldw), 0, (int)(BN * p.ldw * 2),
+                                                        0x00020000);
+    // row-major W: lane (li, g) reads row li, k 8g..8g+7 of a 16 x 32 chunk (16 rows x 64 B per load);
+    // SHUF (shuffle_weights layout [N/16][K/32][64 lanes][8]): every load is 1 KB contiguous
+    const int w_voff = SHUF ? lane * 16 + ((k_begin + kg * KW) / 32) * 1024
+                            : (int)(((16 * RT * rg + li) * p.ldw + k_begin + kg * KW + 8 * g) * 2);
+    const int a_stride = SHUF ? p.K * 32 : 16 * (int)p.ldw * 2;
+    const int w_rowtile0 = SHUF ? RT * rg * p.K * 32 : 0;
+    bf16x8 wr[NWIN][RT][CPW];
+    // clamped past the slice end: the ring keeps a branch-free load stream, so the compiler's
+    // in-order vmcnt count stays exact (the spare loads re-read the last stage from L2)
+    auto load_w = [&](int slot, int st, int a, int c) DAB_INLINE {
+      const int soff = min(st, nst - 1) * KS * (SHUF ? 32 : 2) + a * a_stride + w_rowtile0;
+      wr[slot][a][c] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + (SHUF ? 1024 : 64) * c, soff, NT_W ? 2 : 0));
+    };
+    static_for<0, NWIN>([&](auto S_) DAB_INLINE {
+      constexpr int s = decltype(S_)::value;
+#pragma unroll
+      for (int a = 0; a < RT; ++a)
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) load_w(s, s, a, c);
+      return true;
+    });
+    f32x4 acc[RT][MT];
+#pragma unroll
+    for (int a = 0; a < RT; ++a)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // one stage: ring slot H (static), LDS buffer st % NB (runtime address only)
+    auto stage = [&](auto H_, int st) DAB_INLINE {
+      constexpr int h = decltype(H_)::value;
+      const char* xb = smem + (st % NB) * XBUF;
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) {
+        const int lc = kg * (KW / 8) + 4 * c + g;  // logical chunk: this lane's 8 k of chunk c
+        bf16x8 bx[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+          bx[t] = *reinterpret_cast<const bf16x8*>(xb + (16 * t + li) * ROWB + 16 * (lc ^ li));
+#pragma unroll
+        for (int a = 0; a < RT; ++a) {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[a][t] = mfma16(wr[h][a][c], bx[t], acc[a][t]);
+          load_w(h, st + NWIN, a, c);
+          // keep the reload right behind its MFMAs (the scheduler would otherwise sink every
+          // reload to the stage end and halve the bytes in flight)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      wait_lgkm0();
+      __builtin_amdgcn_s_barrier();
+    };
+    __builtin_amdgcn_s_barrier();
+    int st0 = 0;
+    for (; st0 + NWIN <= nst; st0 += NWIN)
+      static_for<0, NWIN>([&](auto J) DAB_INLINE {
+        stage(J, st0 + decltype(J)::value);
+        return true;
+      });
+    // tail: the remaining nst % NWIN stages keep their static slots
+    const int rem = nst - st0;
+    static_for<0, NWIN - 1>([&](auto J) DAB_INLINE {
+      if (decltype(J)::value >= rem) return false;
+      stage(J, st0 + decltype(J)::value);
+      return true;
+    });
+    // partial tile of k-group kg: red[kg][m][BN], 4-float column groups XOR-swizzled by m (every
+    // wave has passed the last stage barrier: the X ring is dead)
+#pragma unroll
+    for (int a = 0; a < RT; ++a)
+#pragma unroll
+      for (int t = 0; t < MT; ++t) {
+        const int m = 16 * t + li;
+        const int col = (16 * (RT * rg + a) + 4 * g) ^ (4 * (m & 15));
+        *reinterpret_cast<f32x4*>(red + (kg * MP + m) * BN + col) = acc[a][t];
+      }
+  }
+
+  // ---------------------------------------------------------------- epilogue (all 5 waves)
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+  auto tile4 = [&](int m, int c4) DAB_INLINE {
+    const int col = c4 ^ (4 * (m & 15));
+    f32x4 v = *reinterpret_cast<const f32x4*>(red + m * BN + col);
+#pragma unroll
+    for (int q = 1; q < KG; ++q) v += *reinterpret_cast<const f32x4*>(red + (q * MP + m) * BN + col);
+    return v;
+  };
+  constexpr int NT = 64 * (NWC + NL);
+  if (p.S > 1) {
+    float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
+    for (int e = tid; e < MP * (BN / 4); e += NT) {
+      const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
+      if (m < p.M) *reinterpret_cast<f32x4*>(slab + (size_t)m * p.N + n0 + c4) = tile4(m, c4);
+    }
+    return;
+  }
+  bf16* out = (bf16*)p.out;
+  if (p.epi == ST_EPI_SWIGLU) {
+    // rows [32i, 32i+16) gate, [32i+16, 32i+32) up -> output columns n0/2 + 16i + j
+    for (int e = tid; e < MP * (BN / 8); e += NT) {
+      const int m = e / (BN / 8), part = e % (BN / 8);
+      if (m >= p.M) continue;
+      const int i = part >> 2, j0 = (part & 3) * 4;
+      const f32x4 gt = tile4(m, 32 * i + j0), up = tile4(m, 32 * i + 16 + j0);
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = gt[j] / (1.f + __expf(-gt[j])) * up[j];
+      u32x2 v;
+      v[0] = pack2bf(o[0], o[1]);
+      v[1] = pack2bf(o[2], o[3]);
+      *reinterpret_cast<u32x2*>(out + (size_t)m * p.ldo + n0 / 2 + 16 * i + j0) = v;
+    }
+    return;
+  }
+  for (int e = tid; e < MP * (BN / 8); e += NT) {
+    const int m = e / (BN / 8), c8 = (e % (BN / 8)) * 8;
+    if (m >= p.M) continue;
+    const f32x4 lo = tile4(m, c8), hi = tile4(m, c8 + 4);
+    float o[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    if (p.residual) {
+      const u32x4 rv = *reinterpret_cast<const u32x4*>(p.residual + (size_t)m * p.ldr + n0 + c8);
+      float r[8];
+      unpack8(rv, r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j])) + r[j];  // round like bf16 GEMM + bf16 add
+    }
+    *reinterpret_cast<u32x4*>(out + (size_t)m * p.ldo + n0 + c8) = pack8(o);
+  }
+}
+
+// Configurations (cfg id -> template).  BN = weight rows per workgroup (16 RT 4/KG), KS = 128 k per
+// stage, NB = X ring buffers (X issued NB-1 stages ahead), NWIN = weight register-ring stages,
+// NL = loader waves.
+struct StreamCfg {
+  int mt, rt, kg, nb, nwin, nl;
+  bool shuf;  // weights in the shuffle_weights layout
+};
+static constexpr StreamCfg kStreamCfgs[] = {
+    {8, 2, 2, 3, 3, 1, false},  // 0: M<=128 BN 64
+    {8, 2, 1, 3, 3, 1, false},  // 1: M<=128 BN 128
+    {8, 2, 2, 4, 4, 2, false},  // 2: M<=128 BN 64, 2 loaders
+    {8, 2, 2, 4, 4, 4, false},  // 3: M<=128 BN 64, 4 loaders
+    {8, 2, 1, 4, 3, 2, false},  // 4: M<=128 BN 128, 2 loaders
+    {8, 2, 1, 4, 3, 4, false},  // 5: M<=128 BN 128, 4 loaders
+    {4, 2, 2, 4, 4, 1, false},  // 6: M<=64  BN 64
+    {4, 2, 2, 4, 4, 4, false},  // 7: M<=64  BN 64, 4 loaders
+    {4, 2, 1, 4, 4, 2, false},  // 8: M<=64  BN 128, 2 loaders
+    {8, 2, 2, 4, 4, 2, true},   // 9: = 2, shuffled weights
+    {8, 2, 1, 4, 3, 4, true},   // 10: = 5, shuffled weights
+    {8, 2, 2, 3, 6, 1, true},   // 11: M<=128 BN 64, 6-stage ring, shuffled
+    {4, 2, 2, 4, 4, 4, true},   // 12: = 7, shuffled weights
+    {4, 2, 1, 4, 4, 2, true},   // 13: = 8, shuffled weights
+    {8, 2, 1, 4, 4, 4, true},   // 14: M<=128 BN 128, 4-stage ring, 4 loaders, shuffled
+    {8, 2, 1, 4, 4, 2, true},   // 15: M<=128 BN 128, 4-stage ring, 2 loaders, shuffled
+    {4, 2, 1, 4, 6, 4, true},   // 16: M<=64  BN 128, 6-stage ring, 4 loaders, shuffled
+};
+constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
+
+template <int C>
+static void launch_cfg(const StreamParams& p, hipStream_t s, bool nt) {
+  constexpr StreamCfg c = kStreamCfgs[C];
+  const dim3 grid((p.N / (16 * c.rt * (4 / c.kg))) * p.S), block(64 * (4 + c.nl));
+  if (nt)
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true>), grid, block, 0,
+                       s, p);
+  else
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, false>), grid, block, 0,
+                       s, p);
+}
+
+int stream_gemm_bn(int cfg) {
+  if (cfg < 0 || cfg >= kNumStreamCfgs) return 0;
+  return 16 * kStreamCfgs[cfg].rt * (4 / kStreamCfgs[cfg].kg);
+}
+
+int stream_gemm_max_m(int cfg) { return (cfg < 0 || cfg >= kNumStreamCfgs) ? 0 : 16 * kStreamCfgs[cfg].mt; }
+
+int stream_gemm_shuffled(int cfg) { return (cfg < 0 || cfg >= kNumStreamCfgs) ? 0 : (int)kStreamCfgs[cfg].shuf; }
+
+template <int C = 0>
+static void launch_any(int cfg, const StreamParams& p, hipStream_t s, bool nt) {
+  if constexpr (C < kNumStreamCfgs) {
+    if (cfg == C) return launch_cfg<C>(p, s, nt);
+    launch_any<C + 1>(cfg, p, s, nt);
+  }
+}
+
+int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg) {
+  constexpr int KS = 128;
+  if (M <= 0 || N <= 0) return 0;
+  const int bn = stream_gemm_bn(cfg);
+  if (!bn || M > stream_gemm_max_m(cfg)) return hipErrorInvalidValue;
+  if (N % bn || S < 1 || K % (S * KS) || ldx % 8 || ldw % 8 || ldo % 8) return hipErrorInvalidValue;
+  if (epilogue != ST_EPI_NONE && epilogue != ST_EPI_SWIGLU) return hipErrorInvalidValue;
+  if (S > 1 && (epilogue != ST_EPI_NONE || residual)) return hipErrorInvalidValue;
+  if (residual && ldr % 8) return hipErrorInvalidValue;
+  if ((long)bn * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;  // buffer descriptor range
+  if (kStreamCfgs[cfg].shuf && (ldw != K || K % 32)) return hipErrorInvalidValue;
+  StreamParams p;
+  p.X = (const bf16*)X;
+  p.ldx = ldx;
+  p.W = (const bf16*)W;
+  p.ldw = ldw;
+  p.out = out;
+  p.ldo = ldo;
+  p.residual = (const bf16*)residual;
+  p.ldr = ldr;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.S = S;
+  p.kc = K / S;
+  p.epi = epilogue;
+  launch_any(cfg, p, s, nt_weights != 0);
+  return hipGetLastError();
+}
+
+}  // namespace dab

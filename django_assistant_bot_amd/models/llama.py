@@ -34,6 +34,11 @@ class DecoderLayer:
     mlp_norm: torch.Tensor
     gate_up_w: torch.Tensor
     down_w: torch.Tensor
+    # decode copies in the ops.shuffle_weights layout (warp-specialised streaming kernel), or None
+    qkv_ws: torch.Tensor | None = None
+    o_ws: torch.Tensor | None = None
+    gate_up_ws: torch.Tensor | None = None
+    down_ws: torch.Tensor | None = None
 
 
 @dataclass
@@ -96,6 +101,14 @@ class LlamaModel:
         self.skinny_for = set(names) if sel == "all" else set() if sel == "none" else set(sel.split(","))
         self.use_skinny = bool(self.skinny_for)
         self._split_cache: dict = {}
+        # decode projections on the warp-specialised streaming kernel (stream_gemm.hip) over weight
+        # copies in the coalesced shuffle_weights layout: qkv 25.6 -> 16.9 us, o 16.6 -> 14.0, down
+        # 39.7 -> 29.2, gate_up 51.8 + 5.1 (SiLU) -> 53.0 with SwiGLU fused, at M = 128
+        # (profiles/decode_stream_gemm.md).  DAB_DECODE_GEMM=skinny keeps the split-K kernel above.
+        self.stream = False
+        if (os.environ.get("DAB_DECODE_GEMM", "stream") == "stream" and self.device.type == "cuda"
+                and self.use_skinny):
+            self.stream = self._make_stream_copies()
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
@@ -116,6 +129,37 @@ class LlamaModel:
             dist.all_reduce(x, group=self.tp_group)
         return x
 
+    STREAM_CFG_M64, STREAM_CFG_M128 = 13, 10  # stream_gemm.hip configurations (BN 128, shuffled)
+
+    @staticmethod
+    def _stream_ok(w: torch.Tensor) -> bool:
+        return w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
+
+    def _make_stream_copies(self) -> bool:
+        """Shuffled decode copies of the projection weights when they fit comfortably (each copy is
+        the size of the weights; the KV pool is sized from what is left)."""
+        names = ("qkv", "o", "gate_up", "down") if self.interleaved_mlp else ("qkv", "o", "down")
+        mats = [(L, n) for L in self.layers for n in names if self._stream_ok(getattr(L, f"{n}_w"))]
+        extra = sum(getattr(L, f"{n}_w").numel() * 2 for L, n in mats)
+        free, _ = torch.cuda.mem_get_info(self.device)
+        if not mats or extra > 0.4 * free:
+            return False
+        for L, n in mats:
+            setattr(L, f"{n}_ws", ops.shuffle_weights(getattr(L, f"{n}_w")))
+        return True
+
+    @staticmethod
+    def _stream_splits(N: int, K: int) -> int:
+        """K-slices for stream_gemm: the fewest that give >= 192 workgroups of 128 weight rows."""
+        tiles, best = N // 128, 1
+        for s in (1, 2, 4, 8, 16):
+            if K % (128 * s):
+                break
+            best = s
+            if tiles * s >= 192:
+                break
+        return best
+
     def _splits(self, w: torch.Tensor) -> int:
         key = id(w)
         s = self._split_cache.get(key)
@@ -123,9 +167,14 @@ class LlamaModel:
             s = self._split_cache[key] = ops.skinny_splits(w.shape[0], w.shape[1])
         return s
 
-    def _proj(self, x, w, sk: bool, allow_slabs: bool = True, name: str = ""):
+    def _proj(self, x, w, sk: bool, allow_slabs: bool = True, name: str = "", ws=None):
         """Projection of the decode (``sk``: weight-streaming kernel, fp32 split-K slabs when the
         consumer can sum them) or prefill path (hipBLASLt)."""
+        if sk and ws is not None:
+            cfg = self.STREAM_CFG_M64 if x.shape[0] <= 64 else self.STREAM_CFG_M128
+            s = self._stream_splits(w.shape[0], w.shape[1])
+            out = ops.stream_gemm(x, ws, splits=s, cfg=cfg, nt=True)
+            return ops.skinny_reduce(out) if (s > 1 and not allow_slabs) else out
         if not sk or name not in self.skinny_for:
             return tuning.linear(x, w) if x.is_cuda else ops.linear(x, w)
         s = self._splits(w)
@@ -150,7 +199,7 @@ class LlamaModel:
                 residual = x
             else:
                 h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
-            qkv = self._proj(h, L.qkv_w, sk, name="qkv")
+            qkv = self._proj(h, L.qkv_w, sk, name="qkv", ws=L.qkv_ws)
             q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv,
                                   D)
             if meta.decode:
@@ -161,14 +210,17 @@ class LlamaModel:
             else:
                 a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                               meta.max_q, causal=True)
-            o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o"))
+            o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
             h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
-            if sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
+            if sk and self.interleaved_mlp and L.gate_up_ws is not None:
+                act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU, nt=True,
+                                      cfg=self.STREAM_CFG_M64 if T <= 64 else self.STREAM_CFG_M128)
+            elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
                 act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
             else:
                 gu = tuning.linear(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
                 act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
-            x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
+            x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down", ws=L.down_ws))
         out, _ = ops.rmsnorm(x, self.final_norm, cfg.eps, residual=residual)
         return out
 

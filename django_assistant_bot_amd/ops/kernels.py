@@ -414,6 +414,58 @@ def skinny_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=N
     return out
 
 
+STREAM_KS = 128
+
+
+def shuffle_weights(w: torch.Tensor) -> torch.Tensor:
+    """[N, K] row-major -> the same values in the decode-stream layout [N/16][K/32][64 lanes][8]: the
+    16 x 32 tile an MFMA A fragment covers is 1 KB contiguous, in lane order (lane l = row l & 15,
+    k 8 (l >> 4) .. + 8), so every weight load of the streaming kernel is one fully coalesced 1 KB
+    read.  Returned with shape [N, K] (only the memory order changes)."""
+    N, K = w.shape
+    expect(N % 16 == 0 and K % 32 == 0, "shuffle_weights needs N % 16 == 0 and K % 32 == 0")
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+
+
+def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=None, cfg=0):
+    """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): same
+    contract and outputs as ``skinny_gemm`` (bf16 [M, N] / SwiGLU [M, N/2] / fp32 slabs [S, M, N]);
+    ``cfg`` picks the tile / ring configuration (``native().stream_gemm_bn(cfg)`` weight rows per
+    workgroup)."""
+    if not x.is_cuda:
+        return skinny_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual, out=out)
+    expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
+    expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
+    M, K = x.shape
+    N = w.shape[0]
+    bn = native().stream_gemm_bn(cfg)
+    expect(bn > 0 and M <= native().stream_gemm_max_m(cfg), f"stream_gemm cfg {cfg}: bad config or M too large")
+    expect(w.shape[1] == K and N % bn == 0 and K % (splits * STREAM_KS) == 0,
+           f"stream_gemm needs N % {bn} == 0 and K % ({STREAM_KS}*splits) == 0")
+    expect(x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0, "row strides must be multiples of 8")
+    if native().stream_gemm_shuffled(cfg):
+        expect(w.is_contiguous(), "shuffled-layout configurations take a contiguous shuffle_weights() tensor")
+    if splits > 1:
+        expect(epilogue == EPI_NONE and residual is None, "split-K writes raw slabs")
+        if out is None:
+            out = torch.empty((splits, M, N), dtype=torch.float32, device=x.device)
+        expect(out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
+        ldo = N
+    else:
+        n_out = N // 2 if epilogue == EPI_SWIGLU else N
+        if residual is not None:
+            expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
+                   and tuple(residual.shape) == (M, N), "residual must be bf16 [M, N]")
+        if out is None:
+            out = torch.empty((M, n_out), dtype=torch.bfloat16, device=x.device)
+        expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
+        ldo = out.stride(0)
+    native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
+                         residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
+                         int(SKINNY_NT_WEIGHTS if nt is None else nt), int(cfg))
+    return out
+
+
 def skinny_reduce(slabs, residual=None, out=None):
     """fp32 slabs [S, M, N] -> bf16 [M, N] (sum rounded to bf16, then + residual)."""
     if not slabs.is_cuda:

@@ -225,6 +225,44 @@ def test_skinny_gemm(M, N, K, S):
         close(ops.skinny_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("cfg", list(range(17)))
+@pytest.mark.parametrize("M", [1, 37, 64, 100, 128])
+@pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1)])
+def test_stream_gemm(cfg, M, N, K, S):
+    """Warp-specialised streaming GEMM vs the fp32 reference: bf16 out (+ residual) and fp32 slabs,
+    stage counts that do and do not fill the register ring (nst = 1..10)."""
+    bn, max_m = ops.native().stream_gemm_bn(cfg), ops.native().stream_gemm_max_m(cfg)
+    if M > max_m or N % bn:
+        pytest.skip("shape outside this configuration")
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    exp = ref.gemm_bt(x, w, out_f32=True)
+    wk = ops.shuffle_weights(w) if ops.native().stream_gemm_shuffled(cfg) else w
+    if S == 1:
+        close(ops.stream_gemm(x, wk, cfg=cfg), exp.to(torch.bfloat16), atol=3e-2, rtol=2e-2)
+        res = bf(M, N)
+        close(ops.stream_gemm(x, wk, residual=res, cfg=cfg), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
+    else:
+        slabs = ops.stream_gemm(x, wk, splits=S, cfg=cfg)
+        assert slabs.shape == (S, M, N)
+        close(slabs.sum(0), exp, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 3, 5, 6, 8, 10, 13])
+@pytest.mark.parametrize("M", [5, 64, 128])
+def test_stream_swiglu_and_strided_x(cfg, M):
+    if M > ops.native().stream_gemm_max_m(cfg):
+        pytest.skip("M outside this configuration")
+    F, K = 512, 1024
+    xs, wg, wu = bf(M, K + 64), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
+    x = xs[:, :K]  # row stride K + 64
+    w = ops.interleave_gate_up(wg, wu)
+    if ops.native().stream_gemm_shuffled(cfg):
+        w = ops.shuffle_weights(w)
+    got = ops.stream_gemm(x, w, epilogue=ops.EPI_SWIGLU, cfg=cfg)
+    exp = ref.silu_mul(ref.gemm_bt(x.contiguous(), torch.cat([wg, wu], 0)))
+    close(got, exp, atol=3e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("M", [3, 64, 128])
 def test_skinny_swiglu_and_strided_x(M):
     F, K = 512, 1024
