@@ -156,7 +156,7 @@ def stream_sweep(which, Ms=(128,)):
     timed, microseconds per call."""
     shapes = (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
               ("lm_head", 128256, 4096))
-    n_cfg = 17
+    n_cfg = 20
     cfgs = [int(c) for c in os.environ.get("STREAM_CFGS", "").split(",") if c] or list(range(n_cfg))
     for M in Ms:
         for name, N, K in shapes:

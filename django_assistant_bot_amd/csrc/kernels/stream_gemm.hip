@@ -66,7 +66,9 @@ __device__ __forceinline__ bool static_for(F&& f) {
   return true;
 }
 
-template <int MT, int RT, int KG, int KS, int NB, int NWIN, int NL, bool SHUF, bool NT_W>
+// ABL (benchmark ablations only): 1 no X staging, 2 no MFMA, 3 weight stream only (no X, no LDS
+// reads, no MFMA); results are garbage, timings bound the parts.
+template <int MT, int RT, int KG, int KS, int NB, int NWIN, int NL, bool SHUF, bool NT_W, int ABL = 0>
 __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamParams p) {
   constexpr int NWC = 4;              // compute waves (waves 4.. are the NL X loaders)
   constexpr int RG = NWC / KG;        // row groups
@@ -125,11 +127,15 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
         return true;
       });
     };
-    const int pre = min(NB - 1, nst);
+    const int pre = (ABL & 1) ? 1 : min(NB - 1, nst);
     for (int s = 0; s < pre; ++s) issue(s);
     retire(pre - 1);
     __builtin_amdgcn_s_barrier();
     for (int st = 0; st < nst; ++st) {
+      if (ABL & 1) {
+        __builtin_amdgcn_s_barrier();
+        continue;
+      }
       if (st + NB - 1 < nst) issue(st + NB - 1);  // into the buffer read in stage st - 1
       if (st + 1 < nst) retire(min(st + NB - 1, nst - 1) - (st + 1));
       __builtin_amdgcn_s_barrier();
@@ -176,11 +182,19 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
         bf16x8 bx[MT];
 #pragma unroll
         for (int t = 0; t < MT; ++t)
-          bx[t] = *reinterpret_cast<const bf16x8*>(xb + (16 * t + li) * ROWB + 16 * (lc ^ li));
+          if constexpr (ABL != 3) bx[t] = *reinterpret_cast<const bf16x8*>(xb + (16 * t + li) * ROWB + 16 * (lc ^ li));
 #pragma unroll
         for (int a = 0; a < RT; ++a) {
+          if constexpr (ABL >= 2) {
+            asm volatile("" ::"v"(wr[h][a][c]));
+            if constexpr (ABL == 2) {
 #pragma unroll
-          for (int t = 0; t < MT; ++t) acc[a][t] = mfma16(wr[h][a][c], bx[t], acc[a][t]);
+              for (int t = 0; t < MT; ++t) asm volatile("" ::"v"(bx[t]));
+            }
+          } else {
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[a][t] = mfma16(wr[h][a][c], bx[t], acc[a][t]);
+          }
           load_w(h, st + NWIN, a, c);
           // keep the reload right behind its MFMAs (the scheduler would otherwise sink every
           // reload to the stage end and halve the bytes in flight)
@@ -274,7 +288,8 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
 // NL = loader waves.
 struct StreamCfg {
   int mt, rt, kg, nb, nwin, nl;
-  bool shuf;  // weights in the shuffle_weights layout
+  bool shuf;    // weights in the shuffle_weights layout
+  int abl = 0;  // benchmark ablation (see the kernel)
 };
 static constexpr StreamCfg kStreamCfgs[] = {
     {8, 2, 2, 3, 3, 1, false},  // 0: M<=128 BN 64
@@ -294,6 +309,9 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {8, 2, 1, 4, 4, 4, true},   // 14: M<=128 BN 128, 4-stage ring, 4 loaders, shuffled
     {8, 2, 1, 4, 4, 2, true},   // 15: M<=128 BN 128, 4-stage ring, 2 loaders, shuffled
     {4, 2, 1, 4, 6, 4, true},   // 16: M<=64  BN 128, 6-stage ring, 4 loaders, shuffled
+    {8, 2, 1, 4, 3, 4, true, 1},  // 17: = 10 without X staging        (ablation, wrong results)
+    {8, 2, 1, 4, 3, 4, true, 2},  // 18: = 10 without MFMA             (ablation, wrong results)
+    {8, 2, 1, 4, 3, 4, true, 3},  // 19: = 10 weight stream only       (ablation, wrong results)
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
@@ -302,10 +320,10 @@ static void launch_cfg(const StreamParams& p, hipStream_t s, bool nt) {
   constexpr StreamCfg c = kStreamCfgs[C];
   const dim3 grid((p.N / (16 * c.rt * (4 / c.kg))) * p.S), block(64 * (4 + c.nl));
   if (nt)
-    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true>), grid, block, 0,
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true, c.abl>), grid, block, 0,
                        s, p);
   else
-    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, false>), grid, block, 0,
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, false, c.abl>), grid, block, 0,
                        s, p);
 }
 

@@ -97,7 +97,8 @@ class LLMEngine:
                  max_model_len: int | None = None, kv_cache_gb: float | None = None, num_blocks: int | None = None,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
                  tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
-                 part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0):
+                 part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0,
+                 pipeline_decode: bool | None = None):
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -181,6 +182,17 @@ class LLMEngine:
         self._h_topp = mk(mb, dtype=torch.float32)
         self._h_cnt = mk(mb, dtype=torch.int64)
         self._h_tokens = mk(mb, dtype=torch.int32)
+        # pipelined decode (``_step_pipelined``): step t+1 is launched before step t's tokens are read,
+        # its input ids copied on the device from step t's sampled tokens, so the host's per-step
+        # bookkeeping overlaps the GPU instead of idling it.  Two alternating host buffer sets: the
+        # H2D copies of step t may still be pending while step t+1's are filled.
+        if pipeline_decode is None:
+            pipeline_decode = os.environ.get("DAB_PIPELINE_DECODE", "1") == "1"
+        self.pipeline_decode = bool(pipeline_decode) and tp_size == 1
+        self._h_alt = {k: mk(*(getattr(self, k).shape,), dtype=getattr(self, k).dtype)
+                       for k in ("_h_ids", "_h_pos", "_h_slots", "_h_ctx", "_h_bt", "_h_temp", "_h_topk", "_h_topp",
+                                 "_h_cnt", "_h_tokens")}
+        self._inflight = None  # launched decode step whose tokens are not consumed yet
         max_parts = math.ceil(self.max_model_len / part_size)
         self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
             else None
@@ -252,7 +264,11 @@ class LLMEngine:
             self.fault_hook(self)
         if self.auto_expire:
             self.expire_deadlines()
-        if self.running and self.mixed_prefill_tokens > 0 and (self.waiting or self.prefilling):
+        if self._inflight is not None and not self._can_pipeline():
+            self._finish_inflight()
+        if self._can_pipeline():
+            self._step_pipelined()
+        elif self.running and self.mixed_prefill_tokens > 0 and (self.waiting or self.prefilling):
             batch = self._reserve_decode()
             chunks = self._schedule_prefill(self.mixed_prefill_tokens) if batch else self._schedule_prefill()
             if chunks and batch:
@@ -274,6 +290,8 @@ class LLMEngine:
     def abort(self, rid: int, reason: str = "abort") -> bool:
         """Stops a request wherever it is (queued, prefilling or decoding) and frees its KV blocks;
         its output (tokens so far) is kept under ``finish_reason=reason``."""
+        if self._inflight is not None:
+            self._finish_inflight()
         for q in (self.waiting, self.prefilling, self.running):
             for r in q:
                 if r.rid == rid:
@@ -291,6 +309,7 @@ class LLMEngine:
         """Drops every unfinished request (after an engine fault) and returns their ids; the block
         pool is rebuilt so nothing leaks if the fault left the bookkeeping half-updated."""
         ids = [r.rid for q in (self.waiting, self.prefilling, self.running) for r in q]
+        self._inflight = None
         self.waiting.clear()
         self.prefilling.clear()
         self.running.clear()
@@ -522,6 +541,134 @@ class LLMEngine:
             self.stats["preemptions"] += 1
             return True
         return False
+
+    # ------------------------------------------------------------------ pipelined decode
+    def _can_pipeline(self) -> bool:
+        return bool(self.pipeline_decode and self.running and not self.waiting and not self.prefilling)
+
+    def _swap_host_buffers(self) -> None:
+        for k, alt in self._h_alt.items():
+            cur = getattr(self, k)
+            setattr(self, k, alt)
+            self._h_alt[k] = cur
+
+    def _length_done(self, r: _Req, extra: int) -> bool:
+        """Whether ``r`` stops for length once ``extra`` more tokens are accepted (EOS / stop tokens
+        are unknowable in advance: such a sequence decodes one wasted token, discarded)."""
+        n, p = len(r.out) + extra, r.params
+        return (n >= p.max_new_tokens or (p.max_length is not None and len(r.prompt) + n >= p.max_length)
+                or len(r.prompt) + n >= self.max_model_len)
+
+    def _step_pipelined(self):
+        """One decode step with the next one already on the GPU: launch step t+1 (ids = step t's
+        device tokens), then consume step t's tokens.  Finishes that the host can predict (length
+        limits) leave the next batch before it is launched."""
+        prev = self._inflight
+        if prev is None:
+            batch = self._reserve_decode()
+            if not batch:
+                return
+            self._launch_decode(batch, None)
+            prev = self._inflight
+        nxt = [r for r in prev["batch"] if not r.finish_reason and not self._length_done(r, 1)]
+        launched = False
+        if nxt:
+            self._swap_host_buffers()
+            fail = self.blocks.prepare_decode_into(
+                [r.seq for r in nxt], [r.out[-1] if r.out else 0 for r in nxt], self.max_blocks_per_seq,
+                self._h_ids.data_ptr(), self._h_pos.data_ptr(), self._h_slots.data_ptr(), self._h_ctx.data_ptr(),
+                self._h_bt.data_ptr())
+            if fail < 0:
+                pos = {id(r): i for i, r in enumerate(prev["batch"])}
+                self._launch_decode(nxt, [pos[id(r)] for r in nxt], pending=1)
+                launched = True
+            else:  # pool dry: finish step t, the synchronous path preempts
+                self._swap_host_buffers()
+        cur = self._inflight if launched else None
+        self._inflight = prev
+        self._finish_inflight()
+        self._inflight = cur
+
+    def _launch_decode(self, batch: list, src_rows, pending: int = 0):
+        """Enqueue one decode step for ``batch`` (host metadata already in the _h_* buffers).
+        ``src_rows``: None -> input ids from the host buffer; else row i's input token is row
+        src_rows[i] of the previous step's device tokens.  ``pending`` tokens per sequence are
+        sampled but not yet appended (RNG counters count them)."""
+        t0 = time.perf_counter()
+        B = len(batch)
+        self._h_temp[:B] = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in batch])
+        self._h_topk[:B] = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32)
+        self._h_topp[:B] = torch.tensor([r.params.top_p for r in batch])
+        self._h_cnt[:B] = torch.tensor([r.rng_base + len(r.out) + pending for r in batch], dtype=torch.int64)
+        self._fast = all((0 < r.params.top_k <= ops.kernels.SAMPLE_FAST_MAX_K) or not r.params.do_sample
+                         or r.params.temperature <= 0 for r in batch)
+        Bp = next(b for b in self._buckets if b >= B) if self.use_graphs else B
+        if Bp > B:
+            self._h_ids[B:Bp] = 0
+            self._h_pos[B:Bp] = 0
+            self._h_slots[B:Bp] = -1
+            self._h_ctx[B:Bp] = 1
+            self._h_bt[B:Bp] = 0
+            self._h_temp[B:Bp] = 0.0
+            self._h_topk[B:Bp] = 1
+            self._h_topp[B:Bp] = 1.0
+            self._h_cnt[B:Bp] = 0
+        pairs = [(self._d_pos, self._h_pos), (self._d_slots, self._h_slots), (self._d_ctx, self._h_ctx),
+                 (self._d_temp, self._h_temp), (self._d_topk, self._h_topk), (self._d_topp, self._h_topp),
+                 (self._d_cnt, self._h_cnt), (self._d_bt, self._h_bt)]
+        if src_rows is None:
+            pairs.append((self._d_ids, self._h_ids))
+        else:
+            # stream-ordered after the previous step's sampling kernel
+            if src_rows == list(range(B)):
+                self._d_ids[:B].copy_(self._d_tokens[:B])
+            else:
+                idx = torch.as_tensor(src_rows, dtype=torch.long).to(self.device, non_blocking=True)
+                self._d_ids[:B].copy_(self._d_tokens.index_select(0, idx))
+            if Bp > B:
+                self._d_ids[B:Bp].zero_()
+        for d, h in pairs:
+            d[:Bp].copy_(h[:Bp], non_blocking=True)
+        g = None
+        if self.use_graphs:
+            g = self._graphs.get((Bp, self._fast))
+            if g is None:
+                g = self._capture(Bp)
+        with self.timer.phase("decode"):
+            if g is not None:
+                g.replay()
+                self.stats["graph_replays"] += 1
+            else:
+                self._decode_body(Bp)
+        ev = None
+        if self.is_gpu:
+            self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        self._inflight = {"batch": list(batch), "Bp": Bp, "tokens": self._h_tokens, "event": ev}
+        self.stats["decode_host_s"] = self.stats.get("decode_host_s", 0.0) + time.perf_counter() - t0
+
+    def _finish_inflight(self):
+        inf, self._inflight = self._inflight, None
+        if inf is None:
+            return
+        t1 = time.perf_counter()
+        if inf["event"] is not None:
+            inf["event"].synchronize()
+        t2 = time.perf_counter()
+        self._collect_gpu_times(block=False)
+        batch = inf["batch"]
+        toks = inf["tokens"][:len(batch)].tolist()
+        now = time.perf_counter()
+        self.stats["decode_steps"] += 1
+        for r, t in zip(batch, toks):
+            if r.finish_reason:  # finished (EOS) or aborted while this step was in flight
+                continue
+            self.stats["decode_tokens"] += 1
+            self._accept_token(r, int(t), now)
+        t3 = time.perf_counter()
+        self.stats["decode_host_s"] = self.stats.get("decode_host_s", 0.0) + (t3 - t2)
+        self.stats["decode_gpu_wait_s"] = self.stats.get("decode_gpu_wait_s", 0.0) + (t2 - t1)
 
     # ------------------------------------------------------------------ decode
     def _reserve_decode(self) -> list:

@@ -53,7 +53,11 @@ def main():
     dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any("flash_fwd" in n for _, _, n in s)]
     pre = [s for s in steps if any("flash_fwd" in n for _, _, n in s)]
     if pre:
-        lines += window_table(pre[-1], "last prefill step")
+        big = max(pre, key=lambda s: s[-1][1] - s[0][0])
+        lines += window_table(big, "largest prefill step")
+        tot = sum(s[-1][1] - s[0][0] for s in pre) / 1e6
+        busy = sum(e - b for s in pre for b, e, _ in s) / 1e6
+        lines += [f"prefill steps: {len(pre)}, span {tot:.1f} ms, kernels busy {busy:.1f} ms", ""]
     if dec:
         lines += window_table(dec[-1], "last decode step")
         if len(dec) > 1:

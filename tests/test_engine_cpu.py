@@ -119,3 +119,49 @@ def test_worker_survives_injected_faults_and_flags_sticky_ones():
             serving._llm.pop("fault-test", None)
     finally:
         worker.stop()
+
+
+def _pipe_engine(pipeline: bool, weights):
+    return LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(weights), max_batch=8, block_size=16,
+                     num_blocks=64, max_prefill_tokens=256, use_graphs=False, pipeline_decode=pipeline)
+
+
+def test_pipelined_decode_matches_synchronous():
+    """Step t+1 launched before step t's tokens are read (ids from the device tokens) must produce
+    exactly the synchronous engine's tokens: greedy decode with stop tokens (a stopped sequence's
+    extra in-flight token is discarded), sampled decode with per-request lengths (host-predicted
+    finishes; the CPU reference sampler draws per batch, so the batches must match too), and a
+    request arriving mid-decode (the pipeline drains for its prefill)."""
+    w = _weights()
+    prompts = [list(range(7, 7 + n)) for n in (12, 30, 5, 44)]
+    greedy = dict(do_sample=False, temperature=0.0)
+    outs = {}
+    for pipe in (False, True):
+        eng = _pipe_engine(pipe, w)
+        rids = []
+        for i, p in enumerate(prompts):
+            sp = SamplingParams(max_new_tokens=6 + 3 * i, temperature=0.9, top_k=20, top_p=0.9, seed=11,
+                                ignore_eos=True)
+            rids.append(eng.add_request(p, sp))
+        while eng.has_unfinished():
+            eng.step()
+        sampled = [eng.pop_output(r).token_ids for r in rids]
+        # greedy with a request arriving mid-decode (the pipelined engine is one step further when it
+        # arrives; greedy tokens do not depend on the batch composition)
+        rids = [eng.add_request(p, SamplingParams(max_new_tokens=20, **greedy)) for p in prompts]
+        for _ in range(4):
+            eng.step()
+        late = eng.add_request(list(range(900, 925)), SamplingParams(max_new_tokens=9, **greedy))
+        while eng.has_unfinished():
+            eng.step()
+        sampled.append(eng.pop_output(late).token_ids)
+        free_run = [eng.pop_output(r).token_ids for r in rids]
+        stops = tuple({t[3] for t in free_run})
+        rids = [eng.add_request(p, SamplingParams(max_new_tokens=20, stop_token_ids=stops, **greedy)) for p in prompts]
+        while eng.has_unfinished():
+            eng.step()
+        stopped = [(eng.pop_output(r).token_ids, eng.finished.get(r)) for r in rids]
+        outs[pipe] = (sampled, free_run, [t for t, _ in stopped])
+        assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
+        assert all(len(t) <= 4 for t in outs[pipe][2])
+    assert outs[True] == outs[False]

@@ -33,8 +33,12 @@ def _run(model, cfg, prompts, device, dtype):
     return h, model.logits(h)
 
 
+@pytest.mark.parametrize("mode", ["stream", "skinny"])
 @pytest.mark.parametrize("B", [3, 20, 64, 128])
-def test_decode_skinny_matches_library_path_and_reference(B):
+def test_decode_skinny_matches_library_path_and_reference(B, mode, monkeypatch):
+    """Decode projections on the warp-specialised stream kernel (shuffled weights) or the split-K
+    skinny kernel vs hipBLASLt vs the fp32 reference."""
+    monkeypatch.setenv("DAB_DECODE_GEMM", mode)
     cfg = decoder_config("tiny-llama")
     w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True)
     gen = torch.Generator().manual_seed(B)
@@ -42,6 +46,7 @@ def test_decode_skinny_matches_library_path_and_reference(B):
                for n in torch.randint(10, 150, (B,), generator=gen)]
     wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
     m_sk = LlamaModel(cfg, wbf, DEV, interleaved_mlp=True)
+    assert m_sk.stream == (mode == "stream")
     m_sk.skinny_for = {"qkv", "o", "gate_up", "down", "lm_head"}  # every decode projection
     m_sk.use_skinny = True
     h_sk, lg_sk = _run(m_sk, cfg, prompts, DEV, torch.bfloat16)
@@ -130,3 +135,35 @@ def test_engine_mixed_schedule_on_gpu():
     assert eng.stats["mixed_steps"] > 0 and eng.stats["graph_replays"] > 0
     assert all(len(o.token_ids) == 24 for o in outs)
     assert all(0 <= t < eng.cfg.vocab_size for o in outs for t in o.token_ids)
+
+
+def test_engine_pipelined_decode_matches_synchronous_on_gpu():
+    """Pipelined decode (step t+1 replayed before step t's tokens are read, ids copied on the device)
+    == synchronous decode: sampled with per-request lengths, then greedy with stop tokens."""
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+
+    prompts = [list(range(10, 10 + 40 + 9 * i)) for i in range(6)]
+    outs = {}
+    for pipe in (False, True):
+        eng = LLMEngine("tiny-llama", device=DEV, max_batch=16, block_size=64, num_blocks=128, seed=3,
+                        max_prefill_tokens=4096, pipeline_decode=pipe)
+        rids = [eng.add_request(p, SamplingParams(max_new_tokens=10 + 5 * i, ignore_eos=True, seed=7))
+                for i, p in enumerate(prompts)]
+        while eng.has_unfinished():
+            eng.step()
+        sampled = [eng.pop_output(r).token_ids for r in rids]
+        greedy = dict(do_sample=False, temperature=0.0, max_new_tokens=24)
+        rids = [eng.add_request(p, SamplingParams(**greedy)) for p in prompts]
+        while eng.has_unfinished():
+            eng.step()
+        free_run = [eng.pop_output(r).token_ids for r in rids]
+        stops = tuple({t[5] for t in free_run})
+        rids = [eng.add_request(p, SamplingParams(stop_token_ids=stops, **greedy)) for p in prompts]
+        while eng.has_unfinished():
+            eng.step()
+        stopped = [eng.pop_output(r).token_ids for r in rids]
+        assert all(len(t) <= 6 for t in stopped)
+        assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
+        assert eng.stats["graph_replays"] > 0
+        outs[pipe] = (sampled, free_run, stopped)
+    assert outs[True] == outs[False]
