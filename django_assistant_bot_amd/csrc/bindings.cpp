@@ -109,11 +109,11 @@ PYBIND11_MODULE(_native, m) {
                 "flash_attention");
         });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
-                                     int batch, int Hq, int Hkv, int D, int part_size, int max_parts, float scale,
-                                     u s) {
+                                     u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
+                                     float scale, u s) {
     check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
-                                      (float*)po, (float*)pm, (float*)pl, batch, Hq, Hkv, D, part_size, max_parts,
-                                      scale, ST(s)),
+                                      (float*)po, (float*)pm, (float*)pl, (int*)cnt, batch, Hq, Hkv, D, part_size,
+                                      max_parts, scale, ST(s)),
           "paged_decode_attention");
   });
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,

@@ -5,7 +5,8 @@
 //                  - Llama prefill (causal, GQA, K/V read from the paged KV cache, so chunked
 //                    prefill and shared prefixes need no special path)                         (N10)
 //  paged_decode: single-token decode over the paged KV cache, split over key partitions
-//                (flash-decoding) + a small cross-partition reduce kernel                       (N9)
+//                (flash-decoding); the last workgroup to finish a (sequence, kv head) combines
+//                its partitions in the same launch                                              (N9)
 //
 // Both compute S^T = K Q^T so that the MFMA C layout leaves the QUERY on the lane and the keys in
 // the registers; the probabilities P are then already the B operand of O^T = V^T P^T (no LDS round
@@ -51,24 +52,39 @@ struct FlashParams {
   float scale_log2;
 };
 
-// One workgroup = 64 queries (4 waves x 16) of one (sequence, head); 64-key tiles staged through
-// LDS with register prefetch of the next tile during compute (issue early / write late).
-template <int D, bool CAUSAL, bool PAGED>
-__global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
+// One workgroup = 16 NW queries (NW waves x 16) of one (sequence, head); 64-key tiles staged
+// through LDS with register prefetch of the next tile during compute (issue early / write late).
+// The K/V tiles of a (sequence, kv head) are re-read by every query block of its GQA heads, so the
+// grid is walked XCD-major: a (sequence, kv head)'s workgroups get ids that share blockIdx % 8 and
+// land on one XCD, whose L2 then serves the re-reads (round-robin dispatch puts block i on XCD i % 8).
+template <int D, bool CAUSAL, bool PAGED, int NW>
+__global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
   constexpr int KT = 64;
+  constexpr int NT = 64 * NW;
+  constexpr int QB = 16 * NW;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
   constexpr int CPR = D / 8;
   constexpr int TILE_BYTES = KT * D * 2;
-  constexpr int CH = KT * CPR / 256;
+  constexpr int CH = KT * CPR / NT;
+  static_assert(CH >= 1, "tile too small for the workgroup");
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
   char* ks = smem;
   char* vs = smem + TILE_BYTES;
 
-  const int b = blockIdx.z, h = blockIdx.y;
+  // linear block id -> XCD-major id (bijective for any grid size) -> (query block, head, sequence)
+  // with query blocks fastest and the heads of one GQA group adjacent
+  const int nqb = gridDim.x;
+  const int nwg = nqb * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+  const int qb = sid % nqb;
+  const int h = (sid / nqb) % gridDim.y;
+  const int b = sid / (nqb * gridDim.y);
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
-  const int q0 = blockIdx.x * 64;
+  const int q0 = qb * QB;
   if (q0 >= seqlen_q) return;
   int kv_len, k_start = 0;
   if (PAGED) {
@@ -95,7 +111,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
 
   int n_keys = kv_len;
   if (CAUSAL) {
-    const int last_q = min(q0 + 63, seqlen_q - 1);
+    const int last_q = min(q0 + QB - 1, seqlen_q - 1);
     n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
   }
   const int n_tiles = div_up(n_keys, KT);
@@ -116,7 +132,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
     }
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * 256;
+      const int idx = tid + c * NT;
       const int row = min(idx / CPR, last), ch = idx % CPR;
       const size_t off = base + (PAGED ? (size_t)row * D : (size_t)row * p.kv_stride_tok) + ch * 8;
       kreg[c] = *reinterpret_cast<const u32x4*>((PAGED ? p.k_cache : p.k) + off);
@@ -126,7 +142,7 @@ __global__ __launch_bounds__(256) void flash_fwd_kernel(FlashParams p) {
   auto store_tile = [&]() {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
-      const int idx = tid + c * 256;
+      const int idx = tid + c * NT;
       const int row = idx / CPR, ch = idx % CPR;
       *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
       *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
@@ -240,6 +256,7 @@ struct DecodeParams {
   float* part_o;
   float* part_m;
   float* part_l;
+  int* counters;  // [B * Hkv] partition arrivals (zero between launches; the last arriver resets)
   int Hq, Hkv, part_size, max_parts;
   float scale_log2;
 };
@@ -254,7 +271,10 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
   constexpr int CH = KT * CPR / 64;  // 16-B chunks per lane per sub-tile (K and V each)
   constexpr int RED_BYTES = 4 * 16 * D * 4 + 2 * 4 * 16 * 4;
   constexpr int STAGE_BYTES = 4 * 2 * SUB_BYTES;
-  __shared__ __attribute__((aligned(16))) char smem[STAGE_BYTES > RED_BYTES ? STAGE_BYTES : RED_BYTES];
+  // one LDS array (a second __shared__ object can cost vmcnt(0) waits); the last-arriver flag
+  // lives right after the reduction area
+  __shared__ __attribute__((aligned(16))) char smem[(STAGE_BYTES > RED_BYTES + 16 ? STAGE_BYTES : RED_BYTES + 16)];
+  int* last_flag = reinterpret_cast<int*>(smem + RED_BYTES);
 
   const int G = p.Hq / p.Hkv;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -394,7 +414,8 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
       lred[w * 16 + li] = l_run;
     }
     __syncthreads();
-    const bool direct = p.max_parts == 1;
+    const int np = min(p.max_parts, div_up(ctx, p.part_size));
+    const bool direct = np == 1;
     for (int e = tid; e < G * D; e += 256) {
       const int qh = e / D, d = e % D;
       float M = -1e30f;
@@ -412,34 +433,49 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
         p.out[hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
       } else {
         const size_t pi = hq * p.max_parts + part;
-        p.part_o[pi * D + d] = O;
+        // write-through (sc1) stores: visible to the combining workgroup on any XCD without a
+        // release fence (cdna_hip_programming.md Guideline 16, R1)
+        __hip_atomic_store(p.part_o + pi * D + d, O, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (d == 0) {
-          p.part_m[pi] = M;
-          p.part_l[pi] = L;
+          __hip_atomic_store(p.part_m + pi, M, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(p.part_l + pi, L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    if (!direct) {
+      // partition combine by the last arriving workgroup of this (sequence, kv head), in the same
+      // launch (Guideline 16, R1): every storing wave drains its sc1 partial stores, barrier, one
+      // lane takes an agent-scope arrival ticket; the last arriver reads the partials with sc1
+      // loads (no acquire fence: nothing it reads can sit stale in its L1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(p.counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == np - 1;
+        if (last) __hip_atomic_store(p.counters + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *last_flag = last;
+      }
+      __syncthreads();
+      if (*last_flag) {
+        auto ld = [](const float* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+        for (int e = tid; e < G * D; e += 256) {
+          const int qh = e / D, d = e % D;
+          const size_t hq = (size_t)b * p.Hq + hk * G + qh;
+          const size_t base = hq * p.max_parts;
+          float M = -1e30f;
+          for (int i = 0; i < np; ++i) M = fmaxf(M, ld(p.part_m + base + i));
+          float L = 0.f, O = 0.f;
+          for (int i = 0; i < np; ++i) {
+            const float f = exp2f(ld(p.part_m + base + i) - M);
+            L += f * ld(p.part_l + base + i);
+            O += f * ld(p.part_o + (base + i) * D + d);
+          }
+          p.out[hq * D + d] = f2bf(L > 0.f ? O / L : 0.f);
         }
       }
     }
     __syncthreads();  // LDS is restaged by the next item
   }
-}
-
-// out[b, hq, :] = sum_p exp2(m_p - M) o_p / sum_p exp2(m_p - M) l_p over the partitions that hold keys.
-template <int D>
-__global__ __launch_bounds__(D) void decode_reduce_kernel(DecodeParams p) {
-  const int hq = blockIdx.x, b = blockIdx.y;
-  const int ctx = p.ctx_lens[b];
-  const int np = min(p.max_parts, div_up(ctx, p.part_size));
-  const size_t base = ((size_t)b * p.Hq + hq) * p.max_parts;
-  float M = -1e30f;
-  for (int i = 0; i < np; ++i) M = fmaxf(M, p.part_m[base + i]);
-  float L = 0.f, O = 0.f;
-  const int d = threadIdx.x;
-  for (int i = 0; i < np; ++i) {
-    const float f = exp2f(p.part_m[base + i] - M);
-    L += f * p.part_l[base + i];
-    O += f * p.part_o[(base + i) * D + d];
-  }
-  p.out[((size_t)b * p.Hq + hq) * D + d] = f2bf(L > 0.f ? O / L : 0.f);
 }
 
 // -----------------------------------------------------------------------------------------------
@@ -473,8 +509,18 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  dim3 grid((max_seqlen_q + 63) / 64, Hq, batch);
-#define DAB_FLASH(DD, C, P) hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P>), grid, dim3(256), 0, s, prm)
+  // 128-query blocks (8 waves) halve the K/V tile traffic per query; short sequences keep 64
+  const bool wide = max_seqlen_q > 64 && D == 128;
+  const int qb = wide ? 128 : 64;
+  dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
+#define DAB_FLASH(DD, C, P)                                                                              \
+  do {                                                                                                  \
+    if (wide)                                                                                           \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD == 128 ? 8 : 4)>), grid, dim3(DD == 128 ? 512 : 256), 0, s, \
+                         prm);                                                                          \
+    else                                                                                                \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4>), grid, dim3(256), 0, s, prm);                  \
+  } while (0)
 #define DAB_FLASH_D(DD)                    \
   if (paged) {                             \
     if (causal) DAB_FLASH(DD, true, true); \
@@ -499,10 +545,11 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
 
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
-                           float* part_m, float* part_l, int batch, int Hq, int Hkv, int D, int part_size,
-                           int max_parts, float scale, hipStream_t s) {
+                           float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
+                           int part_size, int max_parts, float scale, hipStream_t s) {
   if (batch <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1 || block_size % 32) return hipErrorInvalidValue;
+  if (max_parts > 1 && !counters) return hipErrorInvalidValue;
   DecodeParams prm;
   prm.q = (const bf16*)q;
   prm.k_cache = (const bf16*)k_cache;
@@ -515,6 +562,7 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_o = part_o;
   prm.part_m = part_m;
   prm.part_l = part_l;
+  prm.counters = counters;
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.part_size = part_size;
@@ -524,10 +572,8 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   dim3 grid(total_items < 2048 ? total_items : 2048);
   if (D == 128) {
     hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(256), 0, s, prm, total_items);
-    if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<128>, dim3(Hq, batch), dim3(128), 0, s, prm);
   } else if (D == 64) {
     hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(256), 0, s, prm, total_items);
-    if (max_parts > 1) hipLaunchKernelGGL(decode_reduce_kernel<64>, dim3(Hq, batch), dim3(64), 0, s, prm);
   } else {
     return hipErrorInvalidValue;
   }

@@ -79,10 +79,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
 #pragma unroll
     for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
     int sl = 0;
-    for (; sl + 2 <= S; sl += 2, src += 2 * slab_stride) {  // two slabs' loads in flight per round
-      f32x4 a0[2], a1[2], b0[2], b1[2];
+    for (; sl + 4 <= S; sl += 4, src += 4 * slab_stride) {  // four slabs' loads in flight per round
+      f32x4 a0[4], a1[4], b0[4], b1[4];
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
+      for (int q = 0; q < 4; ++q) {
         const float* sq = src + q * slab_stride;
         a0[q] = *reinterpret_cast<const f32x4*>(sq + i0);
         a1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + 4);
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
         b1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half + 4);
       }
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           x1[j] += a0[q][j];

@@ -76,9 +76,24 @@ __global__ __launch_bounds__(NT) void rmsnorm_slab_kernel(bf16* __restrict__ out
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
       const float* src = slabs + row * cols + (size_t)i * 8;
-      // four slabs per round with all their loads issued before the adds (a plain runtime loop
+      // eight slabs per round with all their loads issued before the adds (a plain runtime loop
       // waits out one L2/HBM round trip per slab)
       int sl = 0;
+      for (; sl + 8 <= S; sl += 8, src += 8 * slab_stride) {
+        f32x4 a[8], b[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          a[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride);
+          b[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride + 4);
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            v[k][j] += a[q][j];
+            v[k][4 + j] += b[q][j];
+          }
+      }
       for (; sl + 4 <= S; sl += 4, src += 4 * slab_stride) {
         f32x4 a[4], b[4];
 #pragma unroll

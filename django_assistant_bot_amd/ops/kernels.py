@@ -251,6 +251,9 @@ class DecodeWorkspace:
         self.o = torch.empty((max_batch * Hq * max_parts * D,), dtype=torch.float32, device=device)
         self.m = torch.empty((max_batch * Hq * max_parts,), dtype=torch.float32, device=device)
         self.l = torch.empty((max_batch * Hq * max_parts,), dtype=torch.float32, device=device)
+        # partition arrival counters of the in-launch combine (one per (sequence, kv head) <= Hq);
+        # zero at rest: the last arriving workgroup resets its counter
+        self.cnt = torch.zeros((max_batch * Hq,), dtype=torch.int32, device=device)
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
@@ -272,14 +275,15 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
     if workspace is None:
         # single partition covering the longest allowed context
         part_size = max(part_size, ((block_tables.shape[1] * bs + 127) // 128) * 128)
-        ws_o = ws_m = ws_l = None
+        ws_o = ws_m = ws_l = ws_c = None
     else:
-        expect(workspace.o.numel() >= B * Hq * max_parts * D, "decode workspace too small")
-        ws_o, ws_m, ws_l = workspace.o, workspace.m, workspace.l
+        expect(workspace.o.numel() >= B * Hq * max_parts * D and workspace.cnt.numel() >= B * Hkv,
+               "decode workspace too small")
+        ws_o, ws_m, ws_l, ws_c = workspace.o, workspace.m, workspace.l, workspace.cnt
     out = torch.empty_like(q) if out is None else out
     native().paged_decode_attention(ptr(q), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
-                                    ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), B, Hq, Hkv, D,
-                                    int(part_size), int(max_parts), float(scale), stream(q))
+                                    ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
+                                    D, int(part_size), int(max_parts), float(scale), stream(q))
     return out
 
 
