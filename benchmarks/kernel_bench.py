@@ -273,9 +273,19 @@ def select_suite():
     ws = ops.kernels.sample_workspace(64, 128256, "cuda")
     t = timeit(lambda: ops.sample_tokens(logits, temp, topk, topp, 1, cnt, fast=True, workspace=ws))
     emit(op="sample-topk50-topp95-2stage", rows=64, vocab=128256, us=round(t * 1e6, 1))
+    for R in (128,):
+        lg = torch.randn(R, 128256, device="cuda").to(torch.bfloat16) * 2
+        t_, k_, p_, c_ = (torch.ones(R, device="cuda"), torch.full((R,), 50, dtype=torch.int32, device="cuda"),
+                          torch.full((R,), 0.95, device="cuda"), torch.zeros(R, dtype=torch.int64, device="cuda"))
+        ws = ops.kernels.sample_workspace(R, 128256, "cuda")
+        t = timeit(lambda: ops.sample_tokens(lg, t_, k_, p_, 1, c_, fast=True, workspace=ws))
+        emit(op="sample-topk50-topp95-2stage", rows=R, vocab=128256, us=round(t * 1e6, 1))
     s = torch.randn(64, 1_000_000, device="cuda")
     t = timeit(lambda: ops.topk_rows(s, 250), iters=5)
     emit(op="topk-250", rows=64, n=1_000_000, us=round(t * 1e6, 1), gbps=round(4 * 64e6 / t / 1e9))
+    s = torch.randn(64, 1_000_000, device="cuda") * 0.05 + 0.3  # cosine-like: keys share a top byte
+    t = timeit(lambda: ops.topk_rows(s, 250), iters=5)
+    emit(op="topk-250-cosine-like", rows=64, n=1_000_000, us=round(t * 1e6, 1), gbps=round(4 * 64e6 / t / 1e9))
     x = torch.randn(64, 4096, device="cuda").to(torch.bfloat16)
     w = torch.randn(4096, device="cuda").to(torch.bfloat16)
     t = timeit(lambda: ops.rmsnorm(x, w, 1e-5, residual=x))

@@ -280,29 +280,19 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = tid; i < 256; i += CH_NT) hist[i] = 0;
     __syncthreads();
-    if (shift == 24) {
-      // top byte (sign + high exponent bits): a handful of distinct bins, so one leader per bin adds
-      // the wave's count (plain atomics would serialise up to 64 lanes on one address)
+    // LDS atomics straight into the 256-bin histogram: they serialise only on equal bins, so the
+    // one badly clustered case -- a whole wave in one bin (cosine scores share the top byte) -- takes
+    // one wave-aggregated add instead (a ballot/leader loop per distinct bin measured slower on
+    // logits, whose keys spread over a dozen top-byte bins)
 #pragma unroll
-      for (int j = 0; j < PT; ++j) {
-        const int i = j * CH_NT + tid;
-        const int bin = i < len ? (int)(key[j] >> 24) : -1;
-        unsigned long long active = __ballot(bin >= 0);
-        while (active) {
-          const int leader = __ffsll((long long)active) - 1;
-          const int lb = __shfl(bin, leader, 64);
-          const unsigned long long eq = __ballot(bin == lb);
-          if (lane == leader) atomicAdd(&hist[lb], (uint32_t)__popcll(eq));
-          active &= ~eq;
-        }
-      }
-    } else {
-      // lower bytes of the keys still in the threshold bin: spread over many bins (the leader loop
-      // would run once per distinct bin, up to 64 times per step), so plain LDS atomics
-#pragma unroll
-      for (int j = 0; j < PT; ++j) {
-        const int i = j * CH_NT + tid;
-        if (i < len && (key[j] & pmask) == prefix) atomicAdd(&hist[(key[j] >> shift) & 255u], 1u);
+    for (int j = 0; j < PT; ++j) {
+      const int i = j * CH_NT + tid;
+      const int bin = (i < len && (key[j] & pmask) == prefix) ? (int)((key[j] >> shift) & 255u) : -1;
+      const int b0 = __builtin_amdgcn_readfirstlane(bin);
+      if (__all(bin == b0)) {
+        if (lane == 0 && b0 >= 0) atomicAdd(&hist[b0], 64u);
+      } else if (bin >= 0) {
+        atomicAdd(&hist[bin], 1u);
       }
     }
     __syncthreads();
