@@ -52,16 +52,19 @@ struct FlashParams {
   float scale_log2;
 };
 
-// One workgroup = 16 NW queries (NW waves x 16) of one (sequence, head); 64-key tiles staged
-// through LDS with register prefetch of the next tile during compute (issue early / write late).
+// One workgroup = 16 QT NW queries (NW waves x QT 16-query sub-tiles) of one (sequence, head);
+// 64-key tiles staged through LDS with register prefetch of the next tile during compute (issue
+// early / write late).  Each K / V fragment read from LDS feeds QT MFMAs (QT = 2 halves the LDS
+// reads per MFMA but needs 294 registers, one wave per SIMD, and measured 45 % slower than QT = 1
+// with 8 waves; see the launcher).
 // The K/V tiles of a (sequence, kv head) are re-read by every query block of its GQA heads, so the
 // grid is walked XCD-major: a (sequence, kv head)'s workgroups get ids that share blockIdx % 8 and
 // land on one XCD, whose L2 then serves the re-reads (round-robin dispatch puts block i on XCD i % 8).
-template <int D, bool CAUSAL, bool PAGED, int NW>
+template <int D, bool CAUSAL, bool PAGED, int NW, int QT>
 __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
   constexpr int KT = 64;
   constexpr int NT = 64 * NW;
-  constexpr int QB = 16 * NW;
+  constexpr int QB = 16 * QT * NW;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
   constexpr int CPR = D / 8;
@@ -95,17 +98,21 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
   }
   const int hk = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
-  const int my_q = q0 + w * 16 + li;
-  const bool q_valid = my_q < seqlen_q;
-  const int q_pos = kv_len - seqlen_q + my_q;
-
-  bf16x8 qf[NKK];
-  {
-    const bf16* qrow = p.q + (size_t)(q_start + (q_valid ? my_q : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
+  // this lane's query in sub-tile qt: row q0 + 16 (QT w + qt) + li
+  int my_q[QT], q_pos[QT];
+  bool q_valid[QT];
+  bf16x8 qf[QT][NKK];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    my_q[qt] = q0 + 16 * (QT * w + qt) + li;
+    q_valid[qt] = my_q[qt] < seqlen_q;
+    q_pos[qt] = kv_len - seqlen_q + my_q[qt];
+    const bf16* qrow =
+        p.q + (size_t)(q_start + (q_valid[qt] ? my_q[qt] : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
 #pragma unroll
     for (int kk = 0; kk < NKK; ++kk) {
       bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-      qf[kk] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
+      qf[qt][kk] = q_valid[qt] ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
     }
   }
 
@@ -149,10 +156,17 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
     }
   };
 
-  f32x4 o[NTD];
+  f32x4 o[QT][NTD];
 #pragma unroll
-  for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m_run = -1e30f, l_run = 0.f;
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) o[qt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run[QT], l_run[QT];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt) {
+    m_run[qt] = -1e30f;
+    l_run[qt] = 0.f;
+  }
 
   if (n_tiles > 0) {
     load_tile(0);
@@ -161,55 +175,68 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
   for (int kt = 0; kt < n_tiles; ++kt) {
     __syncthreads();
     if (kt + 1 < n_tiles) load_tile(kt + 1);
-    f32x4 s[4];
+    // S^T = K Q^T: each K fragment feeds QT MFMAs
+    f32x4 s[QT][4];
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
-      s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) s[qt][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < NKK; ++kk) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
-        s[m] = mfma16(a, qf[kk], s[m]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) s[qt][m] = mfma16(a, qf[qt][kk], s[qt][m]);
       }
     }
-    float mx = kNegInf;
+    // online softmax per query sub-tile; only the tail / diagonal tiles need the mask
+    const bool need_mask = (kt + 1) * KT > kv_len || (CAUSAL && (kt + 1) * KT - 1 > kv_len - seqlen_q + q0);
+    bf16x8 pb[QT][2];
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int qt = 0; qt < QT; ++qt) {
+      float mx = kNegInf;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = kt * KT + 16 * m + 4 * g + r;
-        float v = s[m][r] * p.scale_log2;
-        if (key >= kv_len || (CAUSAL && key > q_pos)) v = kNegInf;
-        s[m][r] = v;
-        mx = fmaxf(mx, v);
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = s[qt][m][r] * p.scale_log2;
+          if (need_mask) {
+            const int key = kt * KT + 16 * m + 4 * g + r;
+            if (key >= kv_len || (CAUSAL && key > q_pos[qt])) v = kNegInf;
+          }
+          s[qt][m][r] = v;
+          mx = fmaxf(mx, v);
+        }
       }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
-    float ls = 0.f;
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run[qt], mx);
+      const float alpha = exp2f(m_run[qt] - m_new);
+      float ls = 0.f;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+      for (int m = 0; m < 4; ++m) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = exp2f(s[m][r] - m_new);
-        s[m][r] = e;
-        ls += e;
+        for (int r = 0; r < 4; ++r) {
+          const float e = exp2f(s[qt][m][r] - m_new);
+          s[qt][m][r] = e;
+          ls += e;
+        }
       }
-    }
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
+      l_run[qt] = l_run[qt] * alpha + ls;
+      m_run[qt] = m_new;
 #pragma unroll
-    for (int t = 0; t < NTD; ++t) o[t] *= alpha;
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[qt][ss][j] = (short)f2bf(s[qt][2 * ss][j]);
+          pb[qt][ss][j + 4] = (short)f2bf(s[qt][2 * ss + 1][j]);
+        }
+#pragma unroll
+      for (int t = 0; t < NTD; ++t) o[qt][t] *= alpha;
+    }
+    // O^T += V^T P^T: each transposed V fragment feeds QT MFMAs
+    const int qq = li >> 2, pp = li & 3;
 #pragma unroll
     for (int ss = 0; ss < 2; ++ss) {
-      bf16x8 pb;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        pb[j] = (short)f2bf(s[2 * ss][j]);
-        pb[j + 4] = (short)f2bf(s[2 * ss + 1][j]);
-      }
-      const int qq = li >> 2, pp = li & 3;
 #pragma unroll
       for (int t = 0; t < NTD; ++t) {
         const int ch = 2 * t + (pp >> 1);
@@ -217,25 +244,29 @@ __global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
         const bf16x4 lo = ds_read_tr16(vs + swz<D>(32 * ss + 4 * g + qq, ch) + boff);
         const bf16x4 hi = ds_read_tr16(vs + swz<D>(32 * ss + 16 + 4 * g + qq, ch) + boff);
         const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        o[t] = mfma16(a, pb, o[t]);
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) o[qt][t] = mfma16(a, pb[qt][ss], o[qt][t]);
       }
     }
     __syncthreads();
     if (kt + 1 < n_tiles) store_tile();
   }
 
-  float l_tot = l_run;
-  l_tot += __shfl_xor(l_tot, 16, 64);
-  l_tot += __shfl_xor(l_tot, 32, 64);
-  if (!q_valid) return;
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16* orow = p.out + (size_t)(q_start + my_q) * p.o_stride_tok + (size_t)h * p.o_stride_head;
 #pragma unroll
-  for (int t = 0; t < NTD; ++t) {
-    u32x2 v;
-    v[0] = pack2bf(o[t][0] * inv, o[t][1] * inv);
-    v[1] = pack2bf(o[t][2] * inv, o[t][3] * inv);
-    *reinterpret_cast<u32x2*>(orow + 16 * t + 4 * g) = v;
+  for (int qt = 0; qt < QT; ++qt) {
+    float l_tot = l_run[qt];
+    l_tot += __shfl_xor(l_tot, 16, 64);
+    l_tot += __shfl_xor(l_tot, 32, 64);
+    if (!q_valid[qt]) continue;
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    bf16* orow = p.out + (size_t)(q_start + my_q[qt]) * p.o_stride_tok + (size_t)h * p.o_stride_head;
+#pragma unroll
+    for (int t = 0; t < NTD; ++t) {
+      u32x2 v;
+      v[0] = pack2bf(o[qt][t][0] * inv, o[qt][t][1] * inv);
+      v[1] = pack2bf(o[qt][t][2] * inv, o[qt][t][3] * inv);
+      *reinterpret_cast<u32x2*>(orow + 16 * t + 4 * g) = v;
+    }
   }
 }
 
@@ -509,17 +540,29 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  // 128-query blocks (8 waves) halve the K/V tile traffic per query; short sequences keep 64
-  const bool wide = max_seqlen_q > 64 && D == 128;
+  // Long D=128 sequences (Llama prefill): 128-query blocks of 8 waves x 16 queries halve the K/V
+  // tile traffic per query (16x1024 causal: 298 -> 355 TFLOP/s).  DAB_FLASH_VARIANT selects for
+  // A/B runs (benchmarks/kernel_bench.py attn): w4 = 64-query blocks everywhere, qt2 = 4 waves x 2
+  // sub-tiles of 16 (halves LDS reads per MFMA but drops to 1 wave/SIMD: 196 TFLOP/s), w8 = 8 waves
+  // also for D <= 64 (the encoder is 5 % slower that way).
+  static const int variant = [] {
+    const char* v = getenv("DAB_FLASH_VARIANT");
+    if (v == nullptr) return -1;
+    return (v[0] == 'w' && v[1] == '8') ? 1 : (v[0] == 'w' && v[1] == '4') ? 2 : (v[0] == 'q') ? 0 : -1;
+  }();
+  const int var = variant >= 0 ? variant : (D == 128 ? 1 : 2);
+  const bool wide = max_seqlen_q > 64 && var != 2;
   const int qb = wide ? 128 : 64;
   dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
-#define DAB_FLASH(DD, C, P)                                                                              \
-  do {                                                                                                  \
-    if (wide)                                                                                           \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD == 128 ? 8 : 4)>), grid, dim3(DD == 128 ? 512 : 256), 0, s, \
-                         prm);                                                                          \
-    else                                                                                                \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4>), grid, dim3(256), 0, s, prm);                  \
+#define DAB_FLASH(DD, C, P)                                                                \
+  do {                                                                                    \
+    if (wide && var == 1)                                                                 \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD >= 64 ? 8 : 4), (DD >= 64 ? 1 : 2)>), grid, \
+                         dim3(DD >= 64 ? 512 : 256), 0, s, prm);                          \
+    else if (wide)                                                                        \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 2>), grid, dim3(256), 0, s, prm); \
+    else                                                                                  \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1>), grid, dim3(256), 0, s, prm); \
   } while (0)
 #define DAB_FLASH_D(DD)                    \
   if (paged) {                             \
