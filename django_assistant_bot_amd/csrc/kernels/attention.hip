@@ -293,7 +293,7 @@ struct DecodeParams {
 };
 
 template <int D>
-__global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int total_items) {
+__global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, int total_items) {
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
@@ -338,19 +338,33 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
       }
     }
 
-    u32x4 kreg[CH], vreg[CH];
-    // a 32-key sub-tile never straddles a cache block (block_size % 32 == 0): one uniform lookup
-    auto load_sub = [&](int k0) {
-      const int blk = p.block_tables[(size_t)b * p.max_blocks + k0 / p.block_size];
-      const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (k0 % p.block_size)) * D;
-      const int last = k_end - 1 - k0;
+    // Two register buffers of one 32-key sub-tile (K and V) per wave: the sub-tile two steps ahead
+    // is in flight while one computes.  Buffer loads with the sub-tile's uniform base in the
+    // descriptor and lane offsets lane*16 + c*1024 (no per-chunk 64-bit address registers); rows
+    // past the partition end, and whole sub-tiles past it, read as zeros without memory traffic
+    // (descriptor range), and are masked to -inf below.
+    u32x4 kA[CH], vA[CH], kB[CH], vB[CH];
+    const int k_last = ((k_end - 1) / KT) * KT;
+    auto load_sub = [&](u32x4(&kr)[CH], u32x4(&vr)[CH], int k0) {
+      const int kc = min(k0, k_last);
+      const int blk = p.block_tables[(size_t)b * p.max_blocks + kc / p.block_size];
+      const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (kc % p.block_size)) * D;
+      const int bytes = k0 > k_last ? 0 : min(KT, k_end - k0) * D * 2;
+      const auto kd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.k_cache + base), 0, bytes, 0x00020000);
+      const auto vd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), 0, bytes, 0x00020000);
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        kr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(kd, lane * 16, c * 1024, 0));
+        vr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vd, lane * 16, c * 1024, 0));
+      }
+    };
+    auto stage = [&](const u32x4(&kr)[CH], const u32x4(&vr)[CH]) {
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
         const int idx = lane + c * 64;
-        const int row = min(idx / CPR, last), ch = idx % CPR;
-        const size_t off = base + (size_t)row * D + ch * 8;
-        kreg[c] = *reinterpret_cast<const u32x4*>(p.k_cache + off);
-        vreg[c] = *reinterpret_cast<const u32x4*>(p.v_cache + off);
+        const int row = idx / CPR, ch = idx % CPR;
+        *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kr[c];
+        *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vr[c];
       }
     };
 
@@ -359,17 +373,7 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
     for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m_run = -1e30f, l_run = 0.f;
 
-    int k0 = k_begin + w * KT;
-    if (k0 < k_end) load_sub(k0);
-    for (; k0 < k_end; k0 += 4 * KT) {
-#pragma unroll
-      for (int c = 0; c < CH; ++c) {
-        const int idx = lane + c * 64;
-        const int row = idx / CPR, ch = idx % CPR;
-        *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
-        *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
-      }
-      if (k0 + 4 * KT < k_end) load_sub(k0 + 4 * KT);
+    auto compute = [&](const int k0) {
       __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
       __builtin_amdgcn_wave_barrier();
       f32x4 s[2];
@@ -429,6 +433,18 @@ __global__ __launch_bounds__(256) void paged_decode_kernel(DecodeParams p, int t
       }
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
+    };
+    const int kw = k_begin + w * KT;
+    load_sub(kA, vA, kw);
+    load_sub(kB, vB, kw + 4 * KT);
+    for (int k0 = kw; k0 < k_end; k0 += 8 * KT) {
+      stage(kA, vA);
+      load_sub(kA, vA, k0 + 8 * KT);
+      compute(k0);
+      if (k0 + 4 * KT >= k_end) break;
+      stage(kB, vB);
+      load_sub(kB, vB, k0 + 12 * KT);
+      compute(k0 + 4 * KT);
     }
 
     // combine the 4 waves of the workgroup through LDS

@@ -134,6 +134,11 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         self.mixed_prefill_tokens = mixed_prefill_tokens
         self.part_size = part_size
+        # Key partition of the split-K decode attention per step size: partitions of 2048 keys (one
+        # per sequence at RAG context lengths) stream 12 % faster than 512 at batch 128 (fewer
+        # combines, longer streams per workgroup: benchmarks/kernel_bench.py decode), but small
+        # batches need the finer split to give every CU work.
+        self.long_part_size = max(part_size, 2048)
         hkv = cfg.kv_heads // tp_size
         per_block = KVCache.bytes_per_block(cfg.layers, hkv, block_size, cfg.head_dim)
         if num_blocks is None:
@@ -452,7 +457,7 @@ class LLMEngine:
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
         meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
                         cu_q=to(cu), max_q=max(n for _, _, n in chunks), workspace=self._workspace,
-                        part_size=self.part_size, n_decode=Bp, dec_block_tables=self._d_bt[:Bp],
+                        part_size=self._decode_part(Bp), n_decode=Bp, dec_block_tables=self._d_bt[:Bp],
                         dec_ctx_lens=self._d_ctx[:Bp])
         with self.timer.phase("mixed"):
             hidden = self.model.forward(to(ids), meta, self.kv)
@@ -742,10 +747,16 @@ class LLMEngine:
         self.stats["decode_host_s"] = self.stats.get("decode_host_s", 0.0) + (t1 - t0) + (t3 - t2)
         self.stats["decode_gpu_wait_s"] = self.stats.get("decode_gpu_wait_s", 0.0) + (t2 - t1)
 
+    def _decode_part(self, Bp: int) -> int:
+        """Decode attention key partition for a step of Bp sequences: long partitions once the
+        (sequence, kv head) pairs alone cover every CU twice over (512 pairs on 256 CUs)."""
+        hkv = self.cfg.kv_heads // self.tp_size
+        return self.long_part_size if Bp * hkv >= 512 else self.part_size
+
     def _decode_body(self, Bp: int):
         meta = AttnMeta(decode=True, positions=self._d_pos[:Bp], slots=self._d_slots[:Bp],
                         block_tables=self._d_bt[:Bp], ctx_lens=self._d_ctx[:Bp], workspace=self._workspace,
-                        part_size=self.part_size)
+                        part_size=self._decode_part(Bp))
         h = self.model.forward(self._d_ids[:Bp], meta, self.kv)
         logits = self.model.logits(h)
         if self.is_gpu:
