@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--mixed-tokens", type=int, default=2048,
                     help="serve: prompt tokens mixed into one decode step (0: separate prefill steps)")
     ap.add_argument("--max-new-tokens", type=int, default=256)
+    ap.add_argument("--prefill-tokens", type=int, default=32768, help="prompt tokens per prefill step")
     ap.add_argument("--index-rows", type=int, default=1_000_000, help="question rows in the whole (sharded) index")
     ap.add_argument("--rows-per-doc", type=int, default=10)
     ap.add_argument("--embed-model", default="bge-base-en")
@@ -157,7 +158,7 @@ def main():
     t_setup = time.perf_counter()
     embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
     llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
-                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb, max_prefill_tokens=32768,
+                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb, max_prefill_tokens=args.prefill_tokens,
                     mixed_prefill_tokens=args.mixed_tokens if serve else 0, tp_group=tp_group, tp_size=args.tp,
                     tp_rank=tp_rank)
     # ---- synthetic corpus: index rows (questions) grouped into documents

@@ -98,7 +98,7 @@ class LLMEngine:
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
                  tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
                  part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0,
-                 pipeline_decode: bool | None = None):
+                 pipeline_decode: bool | None = None, prefill_streams: int | None = None):
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -133,6 +133,15 @@ class LLMEngine:
         self.max_blocks_per_seq = math.ceil(self.max_model_len / block_size)
         self.max_prefill_tokens = max_prefill_tokens
         self.mixed_prefill_tokens = mixed_prefill_tokens
+        # Opt-in: large prefill steps as two sub-batches on two HIP streams (forward_overlapped), so
+        # the memory-bound kernels of one can overlap the GEMMs of the other.  Measured slower on the
+        # headline bench (prefill 1528 ms per 128-question batch with 2 streams vs 1452 with 1; 1492
+        # with 2 streams of 32K tokens each): the concurrent kernels slow hipBLASLt's GEMMs by more
+        # than they hide.  TP keeps one stream: its all-reduces must be issued in one order on every rank.
+        if prefill_streams is None:
+            prefill_streams = int(os.environ.get("DAB_PREFILL_STREAMS", "1"))
+        self.prefill_streams = prefill_streams if tp_size == 1 else 1
+        self.prefill_split_min = int(os.environ.get("DAB_PREFILL_SPLIT_MIN", "4096"))
         self.part_size = part_size
         # Key partition of the split-K decode attention per step size: partitions of 2048 keys (one
         # per sequence at RAG context lengths) stream 12 % faster than 512 at batch 128 (fewer
@@ -365,6 +374,24 @@ class LLMEngine:
     def _build_block_tables(self, seqs, out_host):
         self.blocks.block_table_into(seqs, self.max_blocks_per_seq, out_host.data_ptr())
 
+    def _prefill_groups(self, sizes):
+        """Contiguous chunk ranges [(a, b), ...] of a prefill step, one per HIP stream of
+        ``LlamaModel.forward_overlapped``: split at the chunk boundary nearest to equal token counts
+        when the step is large enough that each half still runs its GEMMs at full MFMA rate."""
+        T, B = sum(sizes), len(sizes)
+        if self.prefill_streams < 2 or B < 2 or T < 2 * self.prefill_split_min:
+            return [(0, B)]
+        acc, best, cut = 0, None, 1
+        for i in range(1, B):
+            acc += sizes[i - 1]
+            d = abs(2 * acc - T)
+            if best is None or d < best:
+                best, cut = d, i
+        lo = sum(sizes[:cut])
+        if min(lo, T - lo) < self.prefill_split_min:
+            return [(0, B)]
+        return [(0, cut), (cut, B)]
+
     def _run_prefill(self, chunks):
         t0 = time.perf_counter()
         dev = self.device
@@ -387,10 +414,18 @@ class LLMEngine:
         bt = torch.zeros((B, self.max_blocks_per_seq), dtype=torch.int32)
         self._build_block_tables([r.seq for r, _, _ in chunks], bt)
         to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
-        meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
-                        cu_q=to(cu), max_q=max(n for _, _, n in chunks))
+        parts = []
+        for a, b in self._prefill_groups([n for _, _, n in chunks]):
+            t0_, t1_ = int(cu[a]), int(cu[b])
+            meta = AttnMeta(decode=False, positions=to(pos[t0_:t1_]), slots=to(slots[t0_:t1_]),
+                            block_tables=to(bt[a:b]), ctx_lens=to(ctx[a:b]), cu_q=to(cu[a:b + 1] - cu[a]),
+                            max_q=max(n for _, _, n in chunks[a:b]))
+            parts.append((to(ids[t0_:t1_]), meta))
         with self.timer.phase("prefill"):
-            hidden = self.model.forward(to(ids), meta, self.kv)
+            if len(parts) == 1:
+                hidden = self.model.forward(parts[0][0], parts[0][1], self.kv)
+            else:
+                hidden = self.model.forward_overlapped(parts, self.kv)
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
         self.stats["prefill_tokens"] += T
         self.stats["prefill_steps"] += 1

@@ -191,38 +191,83 @@ class LlamaModel:
         # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
         # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
         sk = self.use_skinny and meta.decode and T <= ops.SKINNY_MAX_M and x.is_cuda
-        slabs_ok = self.tp_size == 1  # under TP the partial sums go through the all-reduce as bf16
         residual = None
         for li, L in enumerate(self.layers):
-            if residual is None:
-                h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
-                residual = x
-            else:
-                h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
-            qkv = self._proj(h, L.qkv_w, sk, name="qkv", ws=L.qkv_ws)
-            q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv,
-                                  D)
-            if meta.decode:
-                a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
-                                     meta.workspace)
-            elif meta.n_decode:
-                a = self._mixed_attention(q, kv, li, meta)
-            else:
-                a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
-                                              meta.max_q, causal=True)
-            o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
-            h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
-            if sk and self.interleaved_mlp and L.gate_up_ws is not None:
-                act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU, nt=True,
-                                      cfg=self.STREAM_CFG_M64 if T <= 64 else self.STREAM_CFG_M128)
-            elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
-                act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
-            else:
-                gu = tuning.linear(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
-                act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
-            x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down", ws=L.down_ws))
+            x, residual = self._layer(li, L, x, residual, meta, kv, sk)
         out, _ = ops.rmsnorm(x, self.final_norm, cfg.eps, residual=residual)
         return out
+
+    def _layer(self, li: int, L: DecoderLayer, x, residual, meta: AttnMeta, kv: KVCache, sk: bool):
+        """One decoder layer: (layer input, residual stream) -> (next layer input, residual stream)."""
+        cfg, D, T = self.cfg, self.cfg.head_dim, meta.positions.numel()  # x may be [S, T, H] split-K slabs
+        slabs_ok = self.tp_size == 1  # under TP the partial sums go through the all-reduce as bf16
+        if residual is None:
+            h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
+            residual = x
+        else:
+            h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
+        qkv = self._proj(h, L.qkv_w, sk, name="qkv", ws=L.qkv_ws)
+        q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
+        if meta.decode:
+            a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
+                                 meta.workspace)
+        elif meta.n_decode:
+            a = self._mixed_attention(q, kv, li, meta)
+        else:
+            a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                          meta.max_q, causal=True)
+        o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
+        h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
+        if sk and self.interleaved_mlp and L.gate_up_ws is not None:
+            act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU, nt=True,
+                                  cfg=self.STREAM_CFG_M64 if T <= 64 else self.STREAM_CFG_M128)
+        elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
+            act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
+        else:
+            gu = tuning.linear(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
+            act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
+        x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down", ws=L.down_ws))
+        return x, residual
+
+    def forward_overlapped(self, parts, kv: KVCache) -> torch.Tensor:
+        """Prefill of independent sub-batches ``[(ids, meta), ...]`` (disjoint sequences) with each
+        sub-batch's layer stack on its own HIP stream, issued layer by layer in lock step.  One
+        sub-batch's memory-bound kernels (SiLU-mul, RMSNorm, RoPE/KV write, flash attention) then run
+        beside the other's compute-bound hipBLASLt GEMMs instead of after them.  Returns the final
+        hidden states of all sub-batches concatenated in order, on the current stream.  Callers
+        guarantee no sub-batch reads KV written by another in the same call (prefix blocks are only
+        shared once committed after a forward), and TP = 1 (RCCL ordering is per stream)."""
+        if len(parts) == 1 or not kv.k.is_cuda:
+            return torch.cat([self.forward(ids, meta, kv) for ids, meta in parts])
+        main = torch.cuda.current_stream(self.device)
+        side = getattr(self, "_side_streams", None)
+        if side is None or len(side) < len(parts) - 1:
+            side = self._side_streams = [torch.cuda.Stream(self.device) for _ in range(len(parts) - 1)]
+        streams = [main] + side[:len(parts) - 1]
+        ready = torch.cuda.Event()
+        ready.record(main)
+        state = []
+        for s, (ids, meta) in zip(streams, parts):
+            if s is not main:
+                s.wait_event(ready)
+                # inputs were allocated (and copied in) on the main stream: keep them alive for s
+                for t in (ids, meta.positions, meta.slots, meta.block_tables, meta.ctx_lens, meta.cu_q):
+                    t.record_stream(s)
+            with torch.cuda.stream(s):
+                state.append([ops.embed_gather(ids, self.embed), None])
+        for li, L in enumerate(self.layers):
+            for i, (s, (_, meta)) in enumerate(zip(streams, parts)):
+                with torch.cuda.stream(s):
+                    state[i] = list(self._layer(li, L, *state[i], meta, kv, False))
+        outs = []
+        for s, (x, residual) in zip(streams, state):
+            with torch.cuda.stream(s):
+                outs.append(ops.rmsnorm(x, self.final_norm, self.cfg.eps, residual=residual)[0])
+        for s, out in zip(streams, outs):
+            if s is not main:
+                main.wait_stream(s)
+                out.record_stream(main)
+        return torch.cat(outs)
 
     @staticmethod
     def _mixed_attention(q, kv: KVCache, li: int, meta: AttnMeta) -> torch.Tensor:

@@ -167,3 +167,55 @@ def test_engine_pipelined_decode_matches_synchronous_on_gpu():
         assert eng.stats["graph_replays"] > 0
         outs[pipe] = (sampled, free_run, stopped)
     assert outs[True] == outs[False]
+
+
+def test_overlapped_prefill_matches_single_forward():
+    """Prefill split into two sub-batches on two HIP streams (forward_overlapped) == one forward over
+    the whole step: final hidden states and the K/V written to the paged cache."""
+    cfg = decoder_config("tiny-llama")
+    w = {k: v.to(torch.bfloat16) for k, v in
+         random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True).items()}
+    model = LlamaModel(cfg, w, DEV, interleaved_mlp=True)
+    bs, nbp = 64, 8
+    gen = torch.Generator().manual_seed(1)
+    prompts = [torch.randint(0, 900, (int(n),), generator=gen).tolist() for n in (300, 170, 411, 96, 250)]
+    i32 = dict(dtype=torch.int32, device=DEV)
+
+    def meta_for(idx):
+        ps = [prompts[i] for i in idx]
+        bt = torch.stack([torch.arange(i * nbp, (i + 1) * nbp, **i32) for i in idx])
+        cu = torch.tensor([0] + [sum(len(p) for p in ps[:j + 1]) for j in range(len(ps))], **i32)
+        return (torch.tensor([t for p in ps for t in p], **i32),
+                AttnMeta(decode=False, positions=torch.cat([torch.arange(len(p), **i32) for p in ps]),
+                         slots=torch.cat([bt[j, 0].long() * bs + torch.arange(len(p), device=DEV)
+                                          for j, p in enumerate(ps)]),
+                         block_tables=bt, ctx_lens=torch.tensor([len(p) for p in ps], **i32), cu_q=cu,
+                         max_q=max(len(p) for p in ps)))
+
+    kv1 = KVCache(cfg.layers, len(prompts) * nbp, cfg.kv_heads, bs, cfg.head_dim, DEV)
+    kv2 = KVCache(cfg.layers, len(prompts) * nbp, cfg.kv_heads, bs, cfg.head_dim, DEV)
+    ids, meta = meta_for(range(5))
+    h1 = model.forward(ids, meta, kv1)
+    h2 = model.forward_overlapped([meta_for(range(2)), meta_for(range(2, 5))], kv2)
+    torch.cuda.synchronize()
+    assert h2.shape == h1.shape
+    torch.testing.assert_close(h2.float(), h1.float(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(kv2.k.float(), kv1.k.float(), rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(kv2.v.float(), kv1.v.float(), rtol=3e-2, atol=3e-2)
+    assert hasattr(model, "_side_streams")
+
+
+def test_engine_two_stream_prefill_on_gpu():
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+
+    eng = LLMEngine("tiny-llama", device=DEV, max_batch=16, block_size=64, num_blocks=128,
+                    max_prefill_tokens=4096, prefill_streams=2)
+    eng.prefill_split_min = 256
+    sp = SamplingParams(max_new_tokens=12, ignore_eos=True)
+    rids = [eng.add_request(list(range(10, 10 + 200 + 31 * i)), sp) for i in range(8)]
+    while eng.has_unfinished():
+        eng.step()
+    outs = [eng.pop_output(r) for r in rids]
+    assert hasattr(eng.model, "_side_streams")
+    assert all(len(o.token_ids) == 12 for o in outs)
+    assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
