@@ -72,6 +72,19 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   const int t = (int)(th / heads);
   const int half = D >> 1;
   const int i0 = c * 8;
+  // rotation and cache slot first (pos -> cos/sin is a dependent chain): their round trips overlap
+  // the slab loads instead of following them
+  float2 cs[8];
+  {
+    const float4* csp = reinterpret_cast<const float4*>(cos_sin + (size_t)positions[t] * half + i0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float4 v = csp[j];
+      cs[2 * j] = make_float2(v.x, v.y);
+      cs[2 * j + 1] = make_float2(v.z, v.w);
+    }
+  }
+  const int64_t slot = h >= Hq ? slots[t] : 0;
   float x1[8], x2[8];
   if (slabs) {
     // split-K slabs of the QKV projection: sum, then round like a bf16 GEMM output
@@ -122,7 +135,6 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     unpack8(*reinterpret_cast<const u32x4*>(src + i0 + half), x2);
   }
   if (h < Hq + Hkv) {
-    const float2* cs = cos_sin + (size_t)positions[t] * half + i0;
     float o1[8], o2[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -140,7 +152,6 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   if (h < Hq) {
     dst = q_out + ((size_t)t * Hq + h) * D;
   } else {
-    const int64_t slot = slots[t];
     if (slot < 0) return;
     const int64_t blk = slot / block_size, off = slot - blk * block_size;
     const int kh = (h < Hq + Hkv) ? h - Hq : h - Hq - Hkv;

@@ -58,91 +58,128 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, bf1
 
 // Same as rmsnorm_kernel but x arrives as S fp32 split-K slabs of the producing projection:
 // x = bf16(sum_s slabs[s]) (the rounding a bf16 GEMM output would have had).
+// Latency-bound at decode sizes (one row per workgroup, 128-256 rows): everything a thread reads --
+// residual, gain and the slab chunks of KG vectors at once -- is issued before the first add, so the
+// kernel waits out one memory round trip instead of one per slab group plus one for the gain after
+// the row reduction.  Out-of-range vectors load a clamped (valid) address and are masked.
 template <int NT, int VPT>
 __global__ __launch_bounds__(NT) void rmsnorm_slab_kernel(bf16* __restrict__ out, bf16* __restrict__ res_out,
                                                           const float* __restrict__ slabs, int S, long slab_stride,
                                                           const bf16* __restrict__ res_in, const bf16* __restrict__ w,
                                                           int cols, float eps) {
+  constexpr int KG = VPT < 2 ? VPT : 2;  // vectors whose slab loads are in flight together
   __shared__ float red[NT / 64];
   const size_t row = blockIdx.x;
   const int nvec = cols >> 3;
   const u32x4* rr = reinterpret_cast<const u32x4*>(res_in + row * cols);
-  float v[VPT][8];
-  float ss = 0.f;
+  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
+  int iv[VPT];
+  bool ok[VPT];
+  u32x4 graw[VPT], rraw[VPT];
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
     const int i = threadIdx.x + k * NT;
-    if (i < nvec) {
+    ok[k] = i < nvec;
+    iv[k] = ok[k] ? i : nvec - 1;
+    graw[k] = wr[iv[k]];
+    if (res_in) rraw[k] = rr[iv[k]];
+  }
+  float v[VPT][8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
-      const float* src = slabs + row * cols + (size_t)i * 8;
-      // eight slabs per round with all their loads issued before the adds (a plain runtime loop
-      // waits out one L2/HBM round trip per slab)
-      int sl = 0;
-      for (; sl + 8 <= S; sl += 8, src += 8 * slab_stride) {
-        f32x4 a[8], b[8];
+  for (int k = 0; k < VPT; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+  const float* base = slabs + row * cols;
+#pragma unroll
+  for (int k0 = 0; k0 < VPT; k0 += KG) {
+    int sl = 0;
+    for (; sl + 8 <= S; sl += 8) {
+      f32x4 a[KG][8], b[KG][8];
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          a[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride);
-          b[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride + 4);
+          const float* src = base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8;
+          a[kk][q] = *reinterpret_cast<const f32x4*>(src);
+          b[kk][q] = *reinterpret_cast<const f32x4*>(src + 4);
         }
+      __builtin_amdgcn_sched_barrier(0);  // keep every load of the round ahead of the adds
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
         for (int q = 0; q < 8; ++q)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[k][j] += a[q][j];
-            v[k][4 + j] += b[q][j];
+            v[k0 + kk][j] += a[kk][q][j];
+            v[k0 + kk][4 + j] += b[kk][q][j];
           }
-      }
-      for (; sl + 4 <= S; sl += 4, src += 4 * slab_stride) {
-        f32x4 a[4], b[4];
+    }
+    for (; sl + 4 <= S; sl += 4) {
+      f32x4 a[KG][4], b[KG][4];
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          a[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride);
-          b[q] = *reinterpret_cast<const f32x4*>(src + q * slab_stride + 4);
+          const float* src = base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8;
+          a[kk][q] = *reinterpret_cast<const f32x4*>(src);
+          b[kk][q] = *reinterpret_cast<const f32x4*>(src + 4);
         }
+      __builtin_amdgcn_sched_barrier(0);  // keep every load of the round ahead of the adds
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            v[k][j] += a[q][j];
-            v[k][4 + j] += b[q][j];
+            v[k0 + kk][j] += a[kk][q][j];
+            v[k0 + kk][4 + j] += b[kk][q][j];
           }
+    }
+    for (; sl < S; ++sl) {
+      f32x4 a[KG], b[KG];
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk) {
+        const float* src = base + (size_t)sl * slab_stride + (size_t)iv[k0 + kk] * 8;
+        a[kk] = *reinterpret_cast<const f32x4*>(src);
+        b[kk] = *reinterpret_cast<const f32x4*>(src + 4);
       }
-      for (; sl < S; ++sl, src += slab_stride) {
-        const f32x4 a = *reinterpret_cast<const f32x4*>(src), b = *reinterpret_cast<const f32x4*>(src + 4);
+#pragma unroll
+      for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[k][j] += a[j];
-          v[k][4 + j] += b[j];
+          v[k0 + kk][j] += a[kk][j];
+          v[k0 + kk][4 + j] += b[kk][j];
         }
-      }
+    }
+  }
+  float ss = 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j]));
-      if (res_in) {
-        float r[8];
-        unpack8(rr[i], r);
+  for (int k = 0; k < VPT; ++k) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + r[j]));
-        reinterpret_cast<u32x4*>(res_out + row * cols)[i] = pack8(v[k]);
-      }
+    for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j]));
+    if (res_in) {
+      float r[8];
+      unpack8(rraw[k], r);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = bf2f(f2bf(v[k][j] + r[j]));
+      if (ok[k]) reinterpret_cast<u32x4*>(res_out + row * cols)[iv[k]] = pack8(v[k]);
+    }
+    if (ok[k]) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) ss += v[k][j] * v[k][j];
     }
   }
   const float tot = block_sum<NT>(ss, red);
   const float inv = rsqrtf(tot / (float)cols + eps);
-  const u32x4* wr = reinterpret_cast<const u32x4*>(w);
   u32x4* orow = reinterpret_cast<u32x4*>(out + row * cols);
 #pragma unroll
   for (int k = 0; k < VPT; ++k) {
-    const int i = threadIdx.x + k * NT;
-    if (i < nvec) {
+    if (ok[k]) {
       float g[8], o[8];
-      unpack8(wr[i], g);
+      unpack8(graw[k], g);
 #pragma unroll
       for (int j = 0; j < 8; ++j) o[j] = v[k][j] * inv * g[j];
-      orow[i] = pack8(o);
+      orow[iv[k]] = pack8(o);
     }
   }
 }

@@ -1,0 +1,14 @@
+#!/bin/bash
+# norm slab / rope latency tweaks: full gpu suite, then the headline bench twice
+cd "$(dirname "$0")/.." || exit 1
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/s3b_tests.log 2>&1
+rc=$?; tail -1 gpurun_out/s3b_tests.log; [ $rc -eq 0 ] || exit $rc
+pp() { python -c "
+import sys,json; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); e=d['config']['engine_rank0']
+print(sys.argv[1], d['value'], d['p50_latency_ms'], 'prefill ms/batch', round(e['gpu_prefill_ms']/3,1), 'decode ms/step', round(e['gpu_decode_ms']/e['decode_steps'],3))" $1; }
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 > gpurun_out/s3b_b1.log 2>&1
+rc=$?; [ $rc -eq 0 ] || exit $rc; pp gpurun_out/s3b_b1.log
+timeout -k 10 400 python bench.py --steps 3 --warmup 1 > gpurun_out/s3b_b2.log 2>&1
+rc=$?; [ $rc -eq 0 ] || exit $rc; pp gpurun_out/s3b_b2.log
