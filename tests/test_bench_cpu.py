@@ -1,0 +1,53 @@
+"""The bench.py driver contract on CPU: one rank and two gloo ranks (the multi-GPU launch shape of
+``torch.distributed.run``) on the tiny model presets print exactly one JSON line with the required
+keys, the whole-job aggregate and the data-parallel config."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+TINY = ["--embed-model", "tiny-bert", "--llm-model", "tiny-llama", "--index-rows", "5000", "--batch", "4",
+        "--max-new-tokens", "6", "--steps", "1", "--warmup", "1"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def _check(d, n):
+    assert REQUIRED <= set(d)
+    assert d["n_gpus"] == n and d["steps"] == 1 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    c = d["config"]
+    assert c["parallelism"] == f"dp{n}" and c["global_batch"] == 4 * n
+    # whole-job aggregate: n replicas x batch 4 answered in the timed step
+    assert d["value"] == pytest.approx(4 * n / (d["ms_per_step"] / 1000.0), rel=0.02)
+    assert c["docs_per_prompt"] > 0
+
+
+def test_bench_single_rank():
+    _check(_run([sys.executable, "bench.py"] + TINY), 1)
+
+
+def test_bench_two_gloo_ranks():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + TINY
+    _check(_run(cmd), 2)
