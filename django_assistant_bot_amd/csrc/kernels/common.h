@@ -102,6 +102,88 @@ __device__ __forceinline__ float key_float(uint32_t k) {
   return __uint_as_float(u);
 }
 
+// One 8-dim chunk pair (dims i0..i0+7 and i0+D/2..) of head `h` of token `t` of a QKV projection,
+// with rotate-half RoPE applied when `rotate`: the shared body of rope_kv_kernel and of the fused
+// decode-attention prologue (bitwise the same result in both).  The projection is either bf16 rows
+// (`qkv`, row stride `ld`) or S fp32 split-K slabs (`slabs`, row stride `ld`, slab stride
+// `slab_stride`) summed in slab order and rounded like a bf16 GEMM output.  `cs` holds the 8
+// (cos, sin) pairs of the token's position for dims i0..i0+7.  U slabs' loads are in flight per
+// round (the per-element add order is slab order for any U).
+template <int U = 4>
+__device__ __forceinline__ void rope_chunk(const bf16* __restrict__ qkv, const float* __restrict__ slabs, int S,
+                                           long slab_stride, int ld, int t, int h, int D, int i0,
+                                           const float2 (&cs)[8], bool rotate, float (&x1)[8], float (&x2)[8]) {
+  const int half = D >> 1;
+  if (slabs) {
+    const float* src = slabs + (size_t)t * ld + (size_t)h * D;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
+    int sl = 0;
+    for (; sl + U <= S; sl += U, src += U * slab_stride) {
+      f32x4 a0[U], a1[U], b0[U], b1[U];
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const float* sq = src + q * slab_stride;
+        a0[q] = *reinterpret_cast<const f32x4*>(sq + i0);
+        a1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + 4);
+        b0[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half);
+        b1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half + 4);
+      }
+#pragma unroll
+      for (int q = 0; q < U; ++q)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          x1[j] += a0[q][j];
+          x1[4 + j] += a1[q][j];
+          x2[j] += b0[q][j];
+          x2[4 + j] += b1[q][j];
+        }
+    }
+    for (; sl < S; ++sl, src += slab_stride) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + i0), a1 = *reinterpret_cast<const f32x4*>(src + i0 + 4);
+      const f32x4 b0 = *reinterpret_cast<const f32x4*>(src + i0 + half);
+      const f32x4 b1 = *reinterpret_cast<const f32x4*>(src + i0 + half + 4);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        x1[j] += a0[j];
+        x1[4 + j] += a1[j];
+        x2[j] += b0[j];
+        x2[4 + j] += b1[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x1[j] = bf2f(f2bf(x1[j]));
+      x2[j] = bf2f(f2bf(x2[j]));
+    }
+  } else {
+    const bf16* src = qkv + (size_t)t * ld + (size_t)h * D;
+    unpack8(*reinterpret_cast<const u32x4*>(src + i0), x1);
+    unpack8(*reinterpret_cast<const u32x4*>(src + i0 + half), x2);
+  }
+  if (rotate) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float2 v = cs[j];
+      const float o1 = x1[j] * v.x - x2[j] * v.y;
+      const float o2 = x2[j] * v.x + x1[j] * v.y;
+      x1[j] = o1;
+      x2[j] = o2;
+    }
+  }
+}
+
+// The 8 (cos, sin) pairs of dims i0..i0+7 at position `pos` ([max_pos, D/2] float2 table).
+__device__ __forceinline__ void rope_cs(const float2* __restrict__ cos_sin, int pos, int half, int i0, float2 (&cs)[8]) {
+  const float4* csp = reinterpret_cast<const float4*>(cos_sin + (size_t)pos * half + i0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float4 v = csp[j];
+    cs[2 * j] = make_float2(v.x, v.y);
+    cs[2 * j + 1] = make_float2(v.z, v.w);
+  }
+}
+
 }  // namespace dab
 
 #define DAB_CHECK_LAUNCH() (hipGetLastError())

@@ -75,79 +75,10 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
   // rotation and cache slot first (pos -> cos/sin is a dependent chain): their round trips overlap
   // the slab loads instead of following them
   float2 cs[8];
-  {
-    const float4* csp = reinterpret_cast<const float4*>(cos_sin + (size_t)positions[t] * half + i0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float4 v = csp[j];
-      cs[2 * j] = make_float2(v.x, v.y);
-      cs[2 * j + 1] = make_float2(v.z, v.w);
-    }
-  }
+  rope_cs(cos_sin, positions[t], half, i0, cs);
   const int64_t slot = h >= Hq ? slots[t] : 0;
   float x1[8], x2[8];
-  if (slabs) {
-    // split-K slabs of the QKV projection: sum, then round like a bf16 GEMM output
-    const float* src = slabs + (size_t)t * ld + (size_t)h * D;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
-    int sl = 0;
-    for (; sl + 4 <= S; sl += 4, src += 4 * slab_stride) {  // four slabs' loads in flight per round
-      f32x4 a0[4], a1[4], b0[4], b1[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float* sq = src + q * slab_stride;
-        a0[q] = *reinterpret_cast<const f32x4*>(sq + i0);
-        a1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + 4);
-        b0[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half);
-        b1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half + 4);
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x1[j] += a0[q][j];
-          x1[4 + j] += a1[q][j];
-          x2[j] += b0[q][j];
-          x2[4 + j] += b1[q][j];
-        }
-    }
-    for (; sl < S; ++sl, src += slab_stride) {
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + i0), a1 = *reinterpret_cast<const f32x4*>(src + i0 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(src + i0 + half);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(src + i0 + half + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x1[j] += a0[j];
-        x1[4 + j] += a1[j];
-        x2[j] += b0[j];
-        x2[4 + j] += b1[j];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      x1[j] = bf2f(f2bf(x1[j]));
-      x2[j] = bf2f(f2bf(x2[j]));
-    }
-  } else {
-    const bf16* src = qkv + (size_t)t * ld + (size_t)h * D;
-    unpack8(*reinterpret_cast<const u32x4*>(src + i0), x1);
-    unpack8(*reinterpret_cast<const u32x4*>(src + i0 + half), x2);
-  }
-  if (h < Hq + Hkv) {
-    float o1[8], o2[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float2 v = cs[j];
-      o1[j] = x1[j] * v.x - x2[j] * v.y;
-      o2[j] = x2[j] * v.x + x1[j] * v.y;
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      x1[j] = o1[j];
-      x2[j] = o2[j];
-    }
-  }
+  rope_chunk(qkv, slabs, S, slab_stride, ld, t, h, D, i0, cs, h < Hq + Hkv, x1, x2);
   bf16* dst;
   if (h < Hq) {
     dst = q_out + ((size_t)t * Hq + h) * D;
