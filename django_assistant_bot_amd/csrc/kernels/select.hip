@@ -254,6 +254,14 @@ __global__ __launch_bounds__(SEL_NT) void topk_rows_kernel(const float* __restri
 // keeps only `rows` CUs busy and re-reads the row 5 times.
 
 constexpr int CH_NT = 256;
+constexpr int CH_FAST_MAXK = 64;   // threshold pre-filter for k <= this (sampling candidates)
+constexpr int CH_FAST_CAP = 512;   // survivors ranked in LDS; more fall back to the radix select
+
+struct ChunkFast {
+  u32x4 tmax[CH_NT / 4];
+  u32x4 kv[CH_FAST_CAP / 2];  // survivors as (key, index) pairs, two per 16 B
+  uint32_t n, thr;
+};
 
 template <int PT>
 __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restrict__ src, int src_bf16, long ld, int n,
@@ -262,6 +270,7 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
   __shared__ uint32_t hist[256];
   __shared__ uint32_t bc[2];
   __shared__ uint32_t cnt[2];
+  __shared__ ChunkFast fst;
   const int row = blockIdx.y, c = blockIdx.x, nchunks = gridDim.x;
   const int chunk = CH_NT * PT;
   const int start = c * chunk;
@@ -269,13 +278,119 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
   const int tid = threadIdx.x, lane = tid & 63;
   const float* sf = reinterpret_cast<const float*>(src) + (size_t)row * ld + start;
   const bf16* sb = reinterpret_cast<const bf16*>(src) + (size_t)row * ld + start;
+  // Each thread reads 16-B vectors (8 bf16 or 4 fp32 keys): key j of this thread is element
+  // idx_of(j) of the chunk.  Strided 2-4 B loads (one 128-256 B request per wave instruction) held
+  // the kernel to ~1 TB/s.
+  static_assert(CH_NT == 256 && PT % 8 == 0, "idx_of assumes 256 threads and whole 16-B vectors");
+  const int lg = src_bf16 ? 3 : 2;
+  auto idx_of = [&](int j) { return ((j >> lg) << (8 + lg)) + (tid << lg) + (j & ((1 << lg) - 1)); };
+  const bool vec_ok = ((reinterpret_cast<uintptr_t>(src_bf16 ? (const void*)sb : (const void*)sf)) & 15) == 0;
   uint32_t key[PT];
+  if (src_bf16) {
 #pragma unroll
-  for (int j = 0; j < PT; ++j) {
-    const int i = j * CH_NT + tid;
-    key[j] = i < len ? float_key(src_bf16 ? bf2f(sb[i]) : sf[i]) : 0u;
+    for (int v = 0; v < PT / 8; ++v) {
+      const int i0 = v * (CH_NT * 8) + tid * 8;
+      if (vec_ok && i0 + 8 <= len) {
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(sb + i0), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) key[8 * v + e] = float_key(f[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) key[8 * v + e] = i0 + e < len ? float_key(bf2f(sb[i0 + e])) : 0u;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int v = 0; v < PT / 4; ++v) {
+      const int i0 = v * (CH_NT * 4) + tid * 4;
+      if (vec_ok && i0 + 4 <= len) {
+        const f32x4 f = *reinterpret_cast<const f32x4*>(sf + i0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) key[4 * v + e] = float_key(f[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) key[4 * v + e] = i0 + e < len ? float_key(sf[i0 + e]) : 0u;
+      }
+    }
   }
   const int kk = min(k, len);
+  uint32_t* ok = cand_key + ((size_t)row * nchunks + c) * kc;
+  int* oi = cand_idx + ((size_t)row * nchunks + c) * kc;
+  if (kk <= CH_FAST_MAXK) {
+    // Threshold pre-filter (sampling: k = 64 of 8192 logits).  t = the kk-th largest of the 256
+    // per-thread maxima: at least kk keys are >= t (those maxima), so every top-kk key is >= t, and
+    // typically only a few hundred keys pass.  The survivors are compacted into LDS and ranked
+    // exactly (key desc, index asc): one pass over the registers instead of four histogram passes
+    // whose LDS atomics serialise on the handful of top-byte bins logits fall into.  Too many
+    // survivors (heavy ties) fall through to the radix select below.
+    uint32_t m = 0;
+#pragma unroll
+    for (int j = 0; j < PT; ++j)
+      if (idx_of(j) < len) m = max(m, key[j]);
+    reinterpret_cast<uint32_t*>(fst.tmax)[tid] = m;
+    if (tid == 0) fst.n = 0;
+    __syncthreads();
+    // rank of this thread's maximum (desc, thread index asc): 16-B broadcast reads, eight in flight
+    // (one dependent LDS round trip per element would cost ~7 us per workgroup)
+    int rank = 0;
+#pragma unroll 4
+    for (int j4 = 0; j4 < CH_NT / 4; ++j4) {
+      const u32x4 o4 = fst.tmax[j4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) rank += (o4[e] > m) || (o4[e] == m && 4 * j4 + e < tid);
+    }
+    if (rank == kk - 1) fst.thr = m;
+    __syncthreads();
+    const uint32_t t = fst.thr;
+#pragma unroll
+    for (int j = 0; j < PT; ++j) {
+      const int i = idx_of(j);
+      const int slot = wave_append(&fst.n, i < len && key[j] >= t);
+      if (slot >= 0 && slot < CH_FAST_CAP) {
+        uint32_t* e2 = reinterpret_cast<uint32_t*>(fst.kv) + 2 * slot;
+        e2[0] = key[j];
+        e2[1] = (uint32_t)(start + i);
+      }
+    }
+    __syncthreads();
+    const int ns = (int)fst.n;
+    if (ns <= CH_FAST_CAP) {
+      // pad to a multiple of 8 pairs with (key 0, index max): never ranked above a survivor
+      const int ns8 = min(CH_FAST_CAP, (ns + 7) & ~7);
+      if (tid < ns8 - ns) {
+        uint32_t* e2 = reinterpret_cast<uint32_t*>(fst.kv) + 2 * (ns + tid);
+        e2[0] = 0u;
+        e2[1] = 0xffffffffu;
+      }
+      __syncthreads();
+      for (int a = tid; a < ns; a += CH_NT) {
+        const uint32_t* ea = reinterpret_cast<const uint32_t*>(fst.kv) + 2 * a;
+        const uint32_t ka = ea[0], ia = ea[1];
+        int r = 0;
+        for (int u2 = 0; u2 < ns8 / 2; u2 += 4) {
+          u32x4 q[4];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) q[z] = fst.kv[u2 + z];
+#pragma unroll
+          for (int z = 0; z < 4; ++z) {
+            r += (q[z][0] > ka) || (q[z][0] == ka && q[z][1] < ia);
+            r += (q[z][2] > ka) || (q[z][2] == ka && q[z][3] < ia);
+          }
+        }
+        if (r < kk) {
+          ok[r] = ka;
+          oi[r] = (int)ia;
+        }
+      }
+      for (int i = kk + tid; i < kc; i += CH_NT) {
+        ok[i] = 0u;
+        oi[i] = -1;
+      }
+      return;
+    }
+    __syncthreads();  // uniform: every thread read the same count
+  }
   uint32_t prefix = 0, pmask = 0, need = (uint32_t)kk;
   for (int shift = 24; shift >= 0; shift -= 8) {
     for (int i = tid; i < 256; i += CH_NT) hist[i] = 0;
@@ -286,7 +401,7 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
     // logits, whose keys spread over a dozen top-byte bins)
 #pragma unroll
     for (int j = 0; j < PT; ++j) {
-      const int i = j * CH_NT + tid;
+      const int i = idx_of(j);
       const int bin = (i < len && (key[j] & pmask) == prefix) ? (int)((key[j] >> shift) & 255u) : -1;
       const int b0 = __builtin_amdgcn_readfirstlane(bin);
       if (__all(bin == b0)) {
@@ -335,11 +450,9 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
   }
   __syncthreads();
   const uint32_t n_gt = (uint32_t)kk - need;
-  uint32_t* ok = cand_key + ((size_t)row * nchunks + c) * kc;
-  int* oi = cand_idx + ((size_t)row * nchunks + c) * kc;
 #pragma unroll
   for (int j = 0; j < PT; ++j) {
-    const int i = j * CH_NT + tid;
+    const int i = idx_of(j);
     const bool valid = i < len;
     const int pg = wave_append(&cnt[0], valid && key[j] > prefix);
     if (pg >= 0) {

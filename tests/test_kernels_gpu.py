@@ -305,6 +305,24 @@ def test_topk_rows(n):
     assert i.dtype == torch.int64 and int(i.min()) >= 1000
 
 
+def test_topk_rows_ties_and_prefilter_fallback():
+    """Chunk top-k threshold pre-filter (k <= 64): exact values with ties at and above the cut,
+    and the radix fallback when too many keys tie with the threshold (all-equal rows)."""
+    n = 40000
+    s = torch.randn(6, n, device=DEV)
+    s[0, ::7] = 2.5                 # ~5.7k equal keys per row, above every other value
+    s[1] = 0.0                      # all equal: survivors overflow, radix fallback
+    s[2] = torch.randint(0, 3, (n,), device=DEV).float()  # three distinct values
+    s[3, 100:] = float("-inf")
+    s[4] = torch.round(s[4] * 4) / 4  # coarse grid: many ties at the k-th value
+    for k in (1, 7, 50, 64):
+        v, i = ops.topk_rows(s, k)
+        ev, _ = torch.topk(s, k, dim=-1)
+        assert torch.equal(v, ev), k
+        assert torch.equal(torch.gather(s, 1, i.long()), v), k
+        assert int(i.min()) >= 0 and len(set(i[5].tolist())) == k
+
+
 @pytest.mark.parametrize("fast", [False, True])
 def test_sampling_greedy_and_support(fast):
     V, R = 128256, 64
