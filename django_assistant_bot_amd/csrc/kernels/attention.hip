@@ -61,7 +61,9 @@ struct FlashParams {
 // grid is walked XCD-major: a (sequence, kv head)'s workgroups get ids that share blockIdx % 8 and
 // land on one XCD, whose L2 then serves the re-reads (round-robin dispatch puts block i on XCD i % 8).
 template <int D, bool CAUSAL, bool PAGED, int NW, int QT>
-__global__ __launch_bounds__(64 * NW) void flash_fwd_kernel(FlashParams p) {
+// (QT = 2 with 4 waves is held to 256 registers -- 2 waves per SIMD, no spills -- by the
+// launch bound; unbounded it took 294 and ran at 1 wave per SIMD.)
+__global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_fwd_kernel(FlashParams p) {
   constexpr int KT = 64;
   constexpr int NT = 64 * NW;
   constexpr int QB = 16 * QT * NW;
@@ -559,7 +561,8 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // Long D=128 sequences (Llama prefill): 128-query blocks of 8 waves x 16 queries halve the K/V
   // tile traffic per query (16x1024 causal: 298 -> 355 TFLOP/s).  DAB_FLASH_VARIANT selects for
   // A/B runs (benchmarks/kernel_bench.py attn): w4 = 64-query blocks everywhere, qt2 = 4 waves x 2
-  // sub-tiles of 16 (halves LDS reads per MFMA but drops to 1 wave/SIMD: 196 TFLOP/s), w8 = 8 waves
+  // sub-tiles of 16 (halves LDS reads per MFMA; 196 TFLOP/s at 1 wave/SIMD, 340-350 since it is
+  // held to 2 waves/SIMD -- still not above the default, so LDS reads are not the bound), w8 = 8 waves
   // also for D <= 64 (the encoder is 5 % slower that way).
   static const int variant = [] {
     const char* v = getenv("DAB_FLASH_VARIANT");
