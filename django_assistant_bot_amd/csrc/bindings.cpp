@@ -108,6 +108,15 @@ PYBIND11_MODULE(_native, m) {
                                      (const int*)ctx_k, batch, max_sq, Hq, Hkv, D, causal, paged, scale, ST(s)),
                 "flash_attention");
         });
+  // HIP stream restricted to a set of CUs (bit i of the mask words = CU i): lets a compute-bound
+  // workload run beside a bandwidth-bound one on disjoint CUs (benchmarks/overlap_probe.py).  The
+  // handle is wrapped by torch.cuda.ExternalStream; destroy it with destroy_stream.
+  m.def("create_cu_masked_stream", [](std::vector<uint32_t> mask) {
+    hipStream_t st = nullptr;
+    check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+    return reinterpret_cast<uintptr_t>(st);
+  });
+  m.def("destroy_stream", [](u s) { check(hipStreamDestroy(ST(s)), "hipStreamDestroy"); });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
                                      u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
                                      float scale, u s) {
