@@ -392,3 +392,31 @@ def test_index_threshold_search_overflow_falls_back():
     v, i, _ = idx.search(torch.ones(2, dim, device=DEV), 10)
     assert idx.stats["threshold_overflows"] == 1
     assert torch.allclose(v, torch.ones_like(v), atol=1e-2) and (i >= 0).all()
+
+
+def test_cu_masked_stream_runs_kernels():
+    """_native.create_cu_masked_stream: a stream restricted to a CU subset (contiguous low CUs
+    excluded) runs native kernels and library GEMMs with the same results (profiles/overlap_probe.md)."""
+    nat = ops.native()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (n_cu + 31) // 32
+    mask = [0] * words
+    for i in range(min(32, n_cu - 1), n_cu):
+        mask[i // 32] |= 1 << (i % 32)
+    h = nat.create_cu_masked_stream(mask)
+    try:
+        s = torch.cuda.ExternalStream(h)
+        x, w = bf(37, 4096), bf(4096)
+        a, b = bf(300, 512), bf(256, 512, scale=0.05)
+        exp_n, _ = ops.rmsnorm(x, w, 1e-5)
+        exp_g = a.float() @ b.float().t()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s):
+            got_n, _ = ops.rmsnorm(x, w, 1e-5)
+            got_g = ops.gemm_bt(a, b)
+        s.synchronize()
+        assert torch.equal(got_n, exp_n)
+        close(got_g, exp_g, atol=3e-2, rtol=2e-2)
+    finally:
+        torch.cuda.synchronize()
+        nat.destroy_stream(h)
