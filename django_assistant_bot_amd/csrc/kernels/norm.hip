@@ -400,6 +400,13 @@ int rmsnorm_slabs(void* out, void* res_out, const float* slabs, int S, long slab
                   const void* w, int rows, int cols, float eps, hipStream_t s) {
   if (rows <= 0) return 0;
   if (cols % 8 || cols > 16384 || S < 1 || slab_stride % 4) return hipErrorInvalidValue;
+  // 4096-wide rows (Llama-3-8B decode, 8 slabs): 512 threads x 1 vector instead of 256 x 2 -- twice
+  // the waves issuing the slab loads: 4.97 vs 5.52 us per call at 128 rows (benchmarks/slab_norm_bench.py)
+  if (cols / 8 > 256 && cols / 8 <= 512) {
+    hipLaunchKernelGGL((rmsnorm_slab_kernel<512, 1>), dim3(rows), dim3(512), 0, s, (bf16*)out, (bf16*)res_out, slabs,
+                       S, slab_stride, (const bf16*)res_in, (const bf16*)w, cols, eps);
+    return hipGetLastError();
+  }
   DAB_ROW_DISPATCH(rmsnorm_slab_kernel, rows, cols, s, (bf16*)out, (bf16*)res_out, slabs, S, slab_stride,
                    (const bf16*)res_in, (const bf16*)w, cols, eps);
   return hipGetLastError();
