@@ -131,6 +131,12 @@ PYBIND11_MODULE(_native, m) {
                        (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s)),
           "gemm_bt");
   });
+  m.def("gemm256_ok", &dab::gemm256_ok);
+  m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
+                      int epilogue, u s) {
+    check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s)),
+          "gemm256");
+  });
   m.def("gemm_score_candidates", [](u A, long lda, u B, long ldb, int M, int N, int K, u row_group, u q_group, u thr,
                                     u cnt, u cand_val, u cand_idx, int cap, u s) {
     check(dab::gemm_score_candidates(CVP(A), lda, CVP(B), ldb, M, N, K, reinterpret_cast<const int*>(row_group),

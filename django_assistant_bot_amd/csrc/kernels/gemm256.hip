@@ -1,0 +1,481 @@
+// Large-M bf16 GEMM  C[M,N] = A[M,K] . B[N,K]^T  (+bias, +GELU(erf), +residual, or fused SwiGLU)
+// for gfx950: the prefill / encoder projections (Llama-3 qkv / o / gate_up / down at M = 32k tokens,
+// bge qkv / o / up / down at M = 64k).  Replaces HF Linear in the reference
+// (ai/providers/transformers.py:57-66 generate, ai/embedders/transformers.py:18-22 encoder forward).
+//
+// Structure: the 256x256 "8-phase" schedule of cdna_hip_programming.md section 5 (T1-T5):
+//   * 512 threads = 8 waves; per K-tile (BK = 64) the block tile is cut into 2x2 quadrants of
+//     128x128 and every wave owns a 64x32 piece of EACH quadrant (waves 2 (M) x 4 (N) per quadrant),
+//     so one phase = one quadrant = 16 x v_mfma_f32_16x16x32_bf16 per wave, 4 phases per K-tile;
+//   * the A/B tiles are staged by LDS-DMA (buffer_load ... lds, 16 B per lane) in HALF-TILE pieces
+//     (128 rows x 64 k = 16 KB, two instructions per wave), one piece per phase, so the load stream
+//     is spread evenly under the MFMAs; 2 K-tile buffers = 128 KB of LDS (1 block per CU);
+//   * counted waits only: every phase waits `vmcnt(8)` (4 pieces stay in flight ACROSS barriers,
+//     each piece has 4 phases ~ 2k cycles to land), raw s_barrier (never __syncthreads, whose
+//     fence would drain the DMA), all LDS in ONE __shared__ array;
+//   * the two wave groups (wr = 0 / 1, one wave of each per SIMD) are staggered by one barrier so one
+//     group's MFMA cluster overlaps the other group's LDS reads + DMA issue (ping-pong);
+//     s_setprio(1) around each MFMA cluster keeps hipcc from moving MFMAs across the barriers (T5);
+//   * fragment registers: the A rows of the current quadrant row (32 VGPR) and BOTH B halves
+//     (2 x 16 VGPR), so a K-tile reads A0+B0 / B1 / A1 / - in its 4 phases (24 ds_read_b128, the
+//     minimum), and every staged piece is rewritten >= 2 phases after its last read (WAR rule with
+//     staggered groups) and waited >= 1 phase before its first read (RAW rule);
+//   * LDS rows are 128 B; the 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7): conflict-free
+//     for the 4 x 16-lane groups of ds_read_b128 (MI355X_MICROARCH.md section LDS).  LDS-DMA writes
+//     lane-linearly, so the swizzle is applied to the per-lane SOURCE address (rule 21);
+//   * buffer descriptors clamp the tile edges: rows >= M (or >= N) read zeros, no per-lane clamp;
+//   * bijective XCD-aware block remap (T1) + grouped tile order so the 32 tiles an XCD runs at once
+//     share A / B panels in that XCD's L2.
+#include "common.h"
+#include "launchers.h"
+
+#include <cstdlib>
+#include <type_traits>
+
+namespace dab {
+
+namespace {
+
+enum { G_NONE = 0, G_GELU = 1, G_SWIGLU = 2 };
+
+struct G256 {
+  const bf16* A;
+  const bf16* B;
+  bf16* C;
+  const bf16* bias;
+  const bf16* residual;
+  int M, N, K;
+  long lda, ldb, ldc, ldr;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int VMC>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(VMC >= 0 && VMC <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMC) : "memory");
+}
+
+constexpr int kEpiStores = 16;  // VMEM stores per wave in every epilogue variant
+
+__device__ __forceinline__ void bar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr int kBuf = 65536;   // one K-tile: A0 | A1 | B0 | B1, 16 KB each
+constexpr int kHalf = 16384;  // 128 rows x 128 B
+
+}  // namespace
+
+// grouped tile order: tile id -> (m0, n0), column-major inside groups of GM tile rows
+__device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int& m0, int& n0) {
+  constexpr int GM = 4;
+  const int per_group = GM * tiles_n;
+  const int grp = sid / per_group, first_m = grp * GM;
+  const int gsz = min(GM, tiles_m - first_m);
+  const int inner = sid - grp * per_group;
+  m0 = (first_m + inner % gsz) << 8;
+  n0 = (inner / gsz) << 8;
+}
+
+template <int EPI, bool BIAS, bool RES>
+__global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+
+  // Persistent: one workgroup per CU walks a strided list of tiles.  Blocks b and b+8 share an XCD,
+  // so the tile ids are split into 8 contiguous chunks (bijective for any count) and the nper
+  // workgroups of chunk x take ids cstart + l, cstart + l + nper, ... -> at any time the ~32
+  // workgroups of one XCD run consecutive (grouped) tiles that share A / B panels in its L2.
+  const int tiles_m = (p.M + 255) >> 8, tiles_n = p.N >> 8;
+  const int nwg = tiles_m * tiles_n;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int x = bid & 7, l = bid >> 3;
+  const int nper = (G >> 3) + (x < (G & 7) ? 1 : 0);
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int cstart = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+  const int cend = cstart + q8 + (x < r8 ? 1 : 0);
+  int sid = cstart + l;
+  if (sid >= cend) return;  // whole workgroup: uniform
+  int m0, n0;
+  tile_of(sid, tiles_m, tiles_n, m0, n0);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int li = lane & 15, g = lane >> 4;
+
+  // ---- LDS-DMA staging: piece j (0/1) of wave w = half-tile rows 8(8j + w) .. +7
+  const int sw = (4 * (w & 1) + (lane >> 4)) & 7;
+  const int cc = (lane & 7) ^ sw;  // global 16-B chunk this lane fetches
+  const int srow = 8 * w + (lane >> 3);
+  // whole row offsets in VOFFSET (the buffer range check sees them: rows >= M / N read zeros);
+  // the K offset goes in SOFFSET
+  const unsigned vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2), vA1 = vA0 + (unsigned)(64 * p.lda * 2);
+  const unsigned vA2 = vA0 + (unsigned)(128 * p.lda * 2), vA3 = vA0 + (unsigned)(192 * p.lda * 2);
+  const unsigned vB0 = (unsigned)((srow * p.ldb + 8 * cc) * 2), vB1 = vB0 + (unsigned)(64 * p.ldb * 2);
+  const unsigned vB2 = vB0 + (unsigned)(128 * p.ldb * 2), vB3 = vB0 + (unsigned)(192 * p.ldb * 2);
+  auto rsrc_a = [&](int mm) {
+    const long rows = min(256, p.M - mm);
+    return make_rsrc(p.A + (size_t)mm * p.lda, (unsigned)(((rows - 1) * p.lda + p.K) * 2));
+  };
+  auto rsrc_b = [&](int nn) {
+    const long rows = min(256, p.N - nn);
+    return make_rsrc(p.B + (size_t)nn * p.ldb, (unsigned)(((rows - 1) * p.ldb + p.K) * 2));
+  };
+  __amdgpu_buffer_rsrc_t rA = rsrc_a(m0), rB = rsrc_b(n0);
+
+  // slot: 0 = A rows 0-127, 1 = A rows 128-255, 2 = B rows 0-127, 3 = B rows 128-255
+  auto stage = [&](int buf, int slot, int kt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb) {
+    char* dst = smem + buf * kBuf + slot * kHalf + w * 1024;
+    const unsigned so = (unsigned)kt * 128u;
+    const __amdgpu_buffer_rsrc_t r = slot < 2 ? ra : rb;
+    const unsigned v0 = slot == 0 ? vA0 : slot == 1 ? vA2 : slot == 2 ? vB0 : vB2;
+    const unsigned v1 = slot == 0 ? vA1 : slot == 1 ? vA3 : slot == 2 ? vB1 : vB3;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, v0, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + 8192), 16, v1, so, 0, 0);
+  };
+
+  // ---- fragment reads (per-lane byte offsets inside a half-tile, k-steps 0 / 1)
+  const int swr = li >> 1;
+  const int rdA0 = (64 * wr + li) * 128 + 16 * (g ^ swr), rdA1 = (64 * wr + li) * 128 + 16 * ((4 + g) ^ swr);
+  const int rdB0 = (32 * wc + li) * 128 + 16 * (g ^ swr), rdB1 = (32 * wc + li) * 128 + 16 * ((4 + g) ^ swr);
+
+  bf16x8 af[4][2];
+  bf16x8 bfr[2][2][2];  // [jh][jn][ks]
+  f32x4 acc[2][2][4][2];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+
+#define G256_READ_A(BUF, IH)                                                                     \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+    const char* base = smem + (BUF) * kBuf + (IH) * kHalf + i * 2048;                            \
+    af[i][0] = *reinterpret_cast<const bf16x8*>(base + rdA0);                                    \
+    af[i][1] = *reinterpret_cast<const bf16x8*>(base + rdA1);                                    \
+  }
+#define G256_READ_B(BUF, JH)                                                                     \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
+    const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf + j * 2048;                \
+    bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                               \
+    bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                               \
+  }
+#define G256_MFMA(IH, JH)                                                                        \
+  __builtin_amdgcn_s_setprio(1);                                                                 \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                               \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+    acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                    \
+  __builtin_amdgcn_s_setprio(0);
+
+  const int T = p.K >> 6;  // K-tiles (even, >= 2)
+  const int iters = T >> 1;
+
+  // prologue (first tile only): K-tile 0 complete, K-tile 1's A0 / B0 in flight
+  stage(0, 0, 0, rA, rB);
+  stage(0, 2, 0, rA, rB);
+  stage(0, 3, 0, rA, rB);
+  stage(0, 1, 0, rA, rB);
+  stage(1, 0, 1, rA, rB);
+  stage(1, 2, 1, rA, rB);
+  wait_vm<8>();
+  bar();
+  if (wr == 1) bar();  // stagger group 1 by one barrier (ping-pong with group 0)
+
+  // One iteration = 8 phases = K-tiles e = 2it (buffer 0) and o = 2it + 1 (buffer 1).
+  // phase : quadrant reads  stage (buffer, slot, K-tile)  wait (for the next phase's reads)
+  //   1   : (0,0) A0 B0     (1, B1, o)                   vmcnt(8)  -> B1 e
+  //   2   : (0,1) B1        (1, A1, o)                   vmcnt(8)  -> A1 e
+  //   3   : (1,1) A1        (0, A0, e+2)                 -
+  //   4   : (1,0) -         (0, B0, e+2)                 vmcnt(8)  -> A0 B0 o
+  //   5   : (0,0) A0 B0     (0, B1, e+2)                 vmcnt(8)  -> B1 o
+  //   6   : (0,1) B1        (0, A1, e+2)                 vmcnt(8)  -> A1 o
+  //   7   : (1,1) A1        (1, A0, o+2)                 -
+  //   8   : (1,0) -         (1, B0, o+2)                 vmcnt(8)  -> A0 B0 e+2
+  // Every piece is restaged >= 2 phases after its last read.  In the last iteration of a tile the
+  // phase 3-8 pieces are the NEXT tile's K-tiles 0 / 1 (same buffers as e+2 / o+2), so the next
+  // tile starts without a prologue; after the last tile nothing is staged and the phase-4 wait
+  // drains everything (one vmcnt(0) per workgroup).  One copy of the body: the variants differ
+  // only in uniform (SGPR) values, which keeps hipcc's register allocation of the loop intact.
+  bool after_epi = false;
+  for (;;) {
+    const int nsid = sid + nper;
+    const bool more = nsid < cend;
+    int nm0 = m0, nn0 = n0;
+    if (more) tile_of(nsid, tiles_m, tiles_n, nm0, nn0);
+    const __amdgpu_buffer_rsrc_t nA = rsrc_a(nm0), nB = rsrc_b(nn0);
+    for (int it = 0; it < iters; ++it) {
+      const bool last = it == iters - 1;
+      const bool st = !last || more;  // stage phases 3-8
+      // first iteration after an epilogue: kEpiStores younger stores sit in the VM queue
+      const bool fe = after_epi && it == 0;
+      const int e = 2 * it, o = e + 1;
+      const int ke = last ? 0 : e + 2, ko = last ? 1 : o + 2;
+      const __amdgpu_buffer_rsrc_t sa = last ? nA : rA, sb = last ? nB : rB;
+      // phase 1
+      G256_READ_A(0, 0)
+      G256_READ_B(0, 0)
+      stage(1, 3, o, rA, rB);
+      if (fe) wait_vm<8 + kEpiStores>();
+      else wait_vm<8>();
+      bar();
+      G256_MFMA(0, 0)
+      bar();
+      // phase 2
+      G256_READ_B(0, 1)
+      stage(1, 1, o, rA, rB);
+      if (fe) wait_vm<8 + kEpiStores>();
+      else wait_vm<8>();
+      bar();
+      G256_MFMA(0, 1)
+      bar();
+      // phase 3
+      G256_READ_A(0, 1)
+      if (st) stage(0, 0, ke, sa, sb);
+      bar();
+      G256_MFMA(1, 1)
+      bar();
+      // phase 4
+      if (st) {
+        stage(0, 2, ke, sa, sb);
+        if (fe) wait_vm<8 + kEpiStores>();
+        else wait_vm<8>();
+      } else {
+        wait_vm<0>();
+      }
+      bar();
+      G256_MFMA(1, 0)
+      bar();
+      // phase 5
+      G256_READ_A(1, 0)
+      G256_READ_B(1, 0)
+      if (st) {
+        stage(0, 3, ke, sa, sb);
+        wait_vm<8>();
+      }
+      bar();
+      G256_MFMA(0, 0)
+      bar();
+      // phase 6
+      G256_READ_B(1, 1)
+      if (st) {
+        stage(0, 1, ke, sa, sb);
+        wait_vm<8>();
+      }
+      bar();
+      G256_MFMA(0, 1)
+      bar();
+      // phase 7
+      G256_READ_A(1, 1)
+      if (st) stage(1, 0, ko, sa, sb);
+      bar();
+      G256_MFMA(1, 1)
+      bar();
+      // phase 8
+      if (st) {
+        stage(1, 2, ko, sa, sb);
+        wait_vm<8>();
+      }
+      bar();
+      G256_MFMA(1, 0)
+      bar();
+    }
+
+    // ---- epilogue: acc[ih][jh][i][jn][r] = C[m0 + 128 ih + 64 wr + 16 i + li][n0 + 128 jh + 32 wc + 16 jn + 4 g + r]
+    // The next tile's first K-tiles are already in flight; the stores overlap them.  Exactly
+    // kEpiStores buffer stores per wave, unconditional (rows >= M fall outside the descriptor and
+    // are dropped), so the next tile's first waits can count past them (vmcnt(8 + kEpiStores)).
+    // The lane offsets go through an opaque asm so hipcc cannot hoist the epilogue's address
+    // arithmetic out of the tile loop (it would stay live across the K-loop and spill).
+    int e_li = li, e_g = g, e_wc = wc;
+    asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
+    const long c_rows = min(256, p.M - m0);
+    const __amdgpu_buffer_rsrc_t rC = make_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
+    if constexpr (EPI == G_SWIGLU) {
+      // weight rows interleaved in 16-row groups [gate 16 | up 16]: jn = 0 gate, jn = 1 up
+      float bg[2][4], bu[2][4];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int jh = 0; jh < 2; ++jh) {
+          const bf16* bp = p.bias + n0 + 128 * jh + 32 * e_wc + 4 * e_g;
+          const u32x2 gv = *reinterpret_cast<const u32x2*>(bp), uv = *reinterpret_cast<const u32x2*>(bp + 16);
+          bg[jh][0] = __uint_as_float(gv[0] << 16), bg[jh][1] = __uint_as_float(gv[0] & 0xffff0000u);
+          bg[jh][2] = __uint_as_float(gv[1] << 16), bg[jh][3] = __uint_as_float(gv[1] & 0xffff0000u);
+          bu[jh][0] = __uint_as_float(uv[0] << 16), bu[jh][1] = __uint_as_float(uv[0] & 0xffff0000u);
+          bu[jh][2] = __uint_as_float(uv[1] << 16), bu[jh][3] = __uint_as_float(uv[1] & 0xffff0000u);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mr = 128 * ih + 64 * wr + 16 * i + e_li;
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float gt = acc[ih][jh][i][0][r], up = acc[ih][jh][i][1][r];
+              if constexpr (BIAS) {
+                gt += bg[jh][r];
+                up += bu[jh][r];
+              }
+              o[r] = gt / (1.f + __expf(-gt)) * up;
+            }
+            u32x2 v;
+            v[0] = pack2bf(o[0], o[1]);
+            v[1] = pack2bf(o[2], o[3]);
+            const int oc = (n0 + 128 * jh) / 2 + 16 * e_wc + 4 * e_g;
+            __builtin_amdgcn_raw_buffer_store_b64(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, 0);
+          }
+        }
+    } else {
+      // v_permlane16_swap between the jn = 0 / 1 fragments: afterwards each lane holds 8 contiguous
+      // columns n0 + 128 jh + 32 wc + cq, cq = 16 (g & 1) + 8 (g >> 1) -> one 16-B store (T21 idea
+      // for the 16x16 layout: half the store instructions at equal bytes)
+      const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
+      float bv[2][8];
+      if constexpr (BIAS) {
+#pragma unroll
+        for (int jh = 0; jh < 2; ++jh) {
+          const u32x4 b4 = *reinterpret_cast<const u32x4*>(p.bias + n0 + 128 * jh + 32 * e_wc + cq);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            bv[jh][2 * q] = __uint_as_float(b4[q] << 16);
+            bv[jh][2 * q + 1] = __uint_as_float(b4[q] & 0xffff0000u);
+          }
+        }
+      }
+      __amdgpu_buffer_rsrc_t rR = rC;
+      if constexpr (RES) {
+        rR = make_rsrc(p.residual + (size_t)m0 * p.ldr, (unsigned)(c_rows * p.ldr * 2));
+      }
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mr = 128 * ih + 64 * wr + 16 * i + e_li;
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            float o[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[ih][jh][i][0][r]),
+                                                         __float_as_uint(acc[ih][jh][i][1][r]), false, false);
+              o[r] = __uint_as_float(sw[0]);
+              o[4 + r] = __uint_as_float(sw[1]);
+            }
+            const int nc = n0 + 128 * jh + 32 * e_wc + cq;
+            if constexpr (BIAS) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] += bv[jh][r];
+            }
+            if constexpr (EPI == G_GELU) {
+#pragma unroll
+              for (int r = 0; r < 8; ++r) o[r] = 0.5f * o[r] * (1.f + erff(o[r] * 0.70710678118654752f));
+            }
+            if constexpr (RES) {
+              const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(rR, (unsigned)((mr * p.ldr + nc) * 2), 0, 0);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                o[2 * q] += __uint_as_float(rv[q] << 16);
+                o[2 * q + 1] += __uint_as_float(rv[q] & 0xffff0000u);
+              }
+            }
+            u32x4 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
+            if constexpr (BIAS || RES) {
+              if (ih == 0 && i == 0 && jh == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
+          }
+        }
+    }
+    after_epi = true;
+    if (!more) break;
+    sid = nsid;
+    m0 = nm0;
+    n0 = nn0;
+    rA = nA;
+    rB = nB;
+    zero_acc();
+  }
+  if (wr == 0) bar();  // balance the stagger barrier
+#undef G256_READ_A
+#undef G256_READ_B
+#undef G256_MFMA
+}
+
+// Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.
+int gemm256_ok(int M, int N, int K, long lda, long ldb) {
+  if (M <= 0 || N <= 0 || N % 256 || K % 128 || K <= 0 || lda % 8 || ldb % 8) return 0;
+  if ((255L * lda + K) * 2 >= (1L << 31) || (255L * ldb + K) * 2 >= (1L << 31)) return 0;
+  if ((128L * lda) * 2 + (long)K * 2 >= (1L << 31) || (128L * ldb) * 2 + (long)K * 2 >= (1L << 31)) return 0;
+  return 1;
+}
+
+int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s) {
+  if (!gemm256_ok(M, N, K, lda, ldb)) return hipErrorInvalidValue;
+  if (epilogue == G_SWIGLU && residual) return hipErrorInvalidValue;
+  G256 p;
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.C = (bf16*)C;
+  p.bias = (const bf16*)bias;
+  p.residual = (const bf16*)residual;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.ldc = ldc;
+  p.ldr = ldr;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  // persistent: one workgroup (128 KB of LDS) per CU; DAB_GEMM256_PERSIST=0 launches one per tile
+  const char* pe = getenv("DAB_GEMM256_PERSIST");
+  const bool persist = !(pe && pe[0] == '0');
+  const int nwg = (persist && tiles > cus) ? cus : tiles;
+  const bool hb = bias != nullptr, hr = residual != nullptr;
+#define G256_LAUNCH(E, B, R) hipLaunchKernelGGL((gemm256_kernel<E, B, R>), dim3(nwg), dim3(512), 0, s, p)
+  switch (epilogue) {
+    case G_NONE:
+      if (hb && hr) G256_LAUNCH(G_NONE, true, true);
+      else if (hb) G256_LAUNCH(G_NONE, true, false);
+      else if (hr) G256_LAUNCH(G_NONE, false, true);
+      else G256_LAUNCH(G_NONE, false, false);
+      break;
+    case G_GELU:
+      if (hr) return hipErrorInvalidValue;
+      if (hb) G256_LAUNCH(G_GELU, true, false);
+      else G256_LAUNCH(G_GELU, false, false);
+      break;
+    case G_SWIGLU:
+      if (hr) return hipErrorInvalidValue;
+      if (hb) G256_LAUNCH(G_SWIGLU, true, false);
+      else G256_LAUNCH(G_SWIGLU, false, false);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+#undef G256_LAUNCH
+  return hipGetLastError();
+}
+
+}  // namespace dab

@@ -49,6 +49,12 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
             const uint32_t* allow, int allow_words, hipStream_t s);
 
+// gemm256.hip (large-M prefill / encoder GEMM, 256x256 8-phase schedule; epilogue 0 none, 1 GELU,
+// 2 SwiGLU on [gate 16 | up 16]-interleaved weight rows; bias / residual optional)
+int gemm256_ok(int M, int N, int K, long lda, long ldb);
+int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s);
+
 // skinny_gemm.hip (decode-sized M <= 64; S K-slices: S == 1 -> bf16 out with epilogue, S > 1 -> fp32
 // slabs [S][M][N] reduced by the consumer or by skinny_reduce)
 int skinny_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,

@@ -291,6 +291,20 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
 # GEMM
 
 
+GEMM256_MIN_M = int(os.environ.get("DAB_GEMM256_MIN_M", "1024"))
+
+
+def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
+    """Large-M shapes go to the 256x256 8-phase kernel (gemm256.hip); DAB_GEMM256=0 disables it,
+    =1 forces it for every eligible shape."""
+    mode = os.environ.get("DAB_GEMM256", "auto")
+    if mode == "0":
+        return False
+    if mode != "1" and M < GEMM256_MIN_M:
+        return False
+    return bool(native().gemm256_ok(M, N, K, lda, ldb))
+
+
 def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, row_group=None, q_group=None,
             allow=None, out=None):
     """C = A . B^T (+bias) (+act) (+residual) on MFMA; A [M, K], B [N, K] (K-contiguous rows)."""
@@ -327,6 +341,11 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     if out is None:
         out = torch.empty((M, n_out), dtype=dtype, device=A.device)
     expect(out.dtype == dtype and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output buffer")
+    if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU) and not out_f32 and row_group is None and q_group is None
+            and allow is None and use_gemm256(M, N, K, A.stride(0), B.stride(0))):
+        native().gemm256(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
+                         residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), stream(A))
+        return out
     native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
                      residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), int(out_f32),
                      ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A))

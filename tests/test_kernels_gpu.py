@@ -202,6 +202,44 @@ def test_gemm_big_tiles(M, N, K):
           atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 128), (300, 512, 256), (1000, 1024, 512), (4100, 768, 768),
+                                   (2048, 2304, 1024), (8192, 2304, 512), (20000, 1024, 128), (9000, 2048, 256)])
+def test_gemm256(M, N, K, monkeypatch):
+    """8-phase 256x256 kernel (gemm256.hip), forced for every eligible shape: ragged M, every epilogue,
+    and grids of more tiles than CUs (persistent workgroups, next-tile prefetch, counted waits past
+    the epilogue stores)."""
+    monkeypatch.setenv("DAB_GEMM256", "1")
+    assert ops.native().gemm256_ok(M, N, K, K, K)
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    bias, res = bf(N), bf(M, N)
+    close(ops.gemm_bt(A, B), ref.gemm_bt(A, B), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, bias, res), ref.gemm_bt(A, B, bias, res), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, bias, None, ops.EPI_GELU), ref.gemm_bt(A, B, bias, None, ops.EPI_GELU), atol=3e-2,
+          rtol=2e-2)
+    wg, wu = bf(N // 2, K, scale=0.05), bf(N // 2, K, scale=0.05)
+    w = ops.interleave_gate_up(wg, wu)
+    close(ops.gemm_bt(A, w, epilogue=ops.EPI_SWIGLU), ref.silu_mul(ref.gemm_bt(A, torch.cat([wg, wu], 0))),
+          atol=3e-2, rtol=3e-2)
+    bg, bu = bf(N // 2), bf(N // 2)
+    bw = ops.interleave_gate_up(bg[:, None], bu[:, None])[:, 0].contiguous()
+    close(ops.gemm_bt(A, w, bw, epilogue=ops.EPI_SWIGLU),
+          ref.silu_mul(ref.gemm_bt(A, torch.cat([wg, wu], 0), torch.cat([bg, bu]))), atol=3e-2, rtol=3e-2)
+    close(ops.gemm_bt(A, B, bias), ref.gemm_bt(A, B, bias), atol=3e-2, rtol=2e-2)
+    close(ops.gemm_bt(A, B, None, res), ref.gemm_bt(A, B, None, res), atol=3e-2, rtol=2e-2)
+
+
+def test_gemm256_exact_layout(monkeypatch):
+    """Small-integer operands (exact in bf16 and fp32): every output element must match exactly, so a
+    swapped row/column map or a misplaced K-slice cannot hide behind the tolerance."""
+    monkeypatch.setenv("DAB_GEMM256", "1")
+    M, N, K = 512, 512, 256
+    A = torch.randint(-3, 4, (M, K), device=DEV).to(torch.bfloat16)
+    B = torch.randint(-2, 3, (N, K), device=DEV).to(torch.bfloat16)
+    B[:, 0] += torch.arange(N, device=DEV).to(torch.bfloat16) % 7  # asymmetric in n
+    exp = A.float() @ B.float().t()
+    assert torch.equal(ops.gemm_bt(A, B).float(), exp.to(torch.bfloat16).float())
+
+
 def test_gemm_swiglu():
     M, F, K = 77, 256, 512
     x, wg, wu = bf(M, K), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
