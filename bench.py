@@ -317,7 +317,6 @@ def main():
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
             "graphs": llm.use_graphs,
-            "tuned_gemm_shapes": llm.tuned_gemms,
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
             "engine_rank0": eng,

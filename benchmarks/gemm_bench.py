@@ -65,12 +65,16 @@ def main():
     ap.add_argument("--shapes", default="llama,bge,square,edge")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
+    ap.add_argument("--only", default="", help="comma list of op names to run")
     ap.add_argument("--ab-persist", action="store_true", help="also time one-workgroup-per-tile launches")
     args = ap.parse_args()
     os.environ.setdefault("DAB_GEMM256", "1")
     torch.manual_seed(0)
     for group in args.shapes.split(","):
         for name, M, N, K, kind in SHAPES[group]:
+            if args.only and name not in args.only.split(","):
+                continue
             a = rand((M, K))
             w = rand((N, K), 0.05)
             b = rand((N,), 0.5)
@@ -82,6 +86,8 @@ def main():
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             nat, lib = [], []
             arms = [("nat", lambda: run_native(a, w, b, kind, out)), ("lib", lambda: run_lib(a, w, b, kind))]
+            if args.native_only:
+                arms = arms[:1]
             if args.ab_persist:
                 def nonp():
                     os.environ["DAB_GEMM256_PERSIST"] = "0"
@@ -103,6 +109,7 @@ def main():
                     {"nat": nat, "lib": lib, "np": npers}[arm].append(t)
             nat.sort()
             lib.sort()
+            lib = lib or [float("nan")]
             flop = 2.0 * M * N * K
             tn, tl = nat[len(nat) // 2], lib[len(lib) // 2]
             print(json.dumps({"op": name, "M": M, "N": N, "K": K, "epilogue": kind,

@@ -120,12 +120,6 @@ class LLMEngine:
             from ..parallel.custom_allreduce import maybe_create
 
             self.model.custom_ar = maybe_create(tp_group, self.device, tp_size)
-        self.tuned_gemms = 0
-        if self.device.type == "cuda" and os.environ.get("DAB_GEMM_TUNING", "1") != "0":
-            from ..ops import tuning
-
-            arch = torch.cuda.get_device_properties(self.device).gcnArchName.split(":")[0]
-            self.tuned_gemms = tuning.load(tuning.tuning_file(cfg.name, tp_size, arch))
         self.tokenizer = Tokenizer.for_decoder(cfg, checkpoint)
         self.max_batch = max_batch
         self.block_size = block_size

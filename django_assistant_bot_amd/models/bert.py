@@ -11,8 +11,6 @@ No padding tokens are ever computed: sequences are concatenated and delimited by
 """
 from __future__ import annotations
 
-import os
-
 from dataclasses import dataclass
 
 import torch
@@ -47,10 +45,6 @@ class BertEncoder:
         self.typ = w["type_emb"]
         self.eln_g = w["emb_ln_g"]
         self.eln_b = w["emb_ln_b"]
-        # up projection: hipBLASLt + a bias+GELU(erf) elementwise pass, or the native GEMM with the
-        # GELU in its epilogue (DAB_BERT_FUSED_UP=1).  At 64k tokens: 258 + ~150 us vs 532 us
-        # (erf in the tile epilogue does not overlap the MFMA loop; profiles/embed_study.md)
-        self.fused_up = os.environ.get("DAB_BERT_FUSED_UP", "0") == "1"
         self.layers = [
             EncoderLayer(*(w[f"l{i}.{n}"] for n in ("qkv_w", "qkv_b", "o_w", "o_b", "ln1_g", "ln1_b", "i_w", "i_b",
                                                     "d_w", "d_b", "ln2_g", "ln2_b")))
@@ -68,8 +62,8 @@ class BertEncoder:
         T = ids.numel()
         x = ops.bert_embed(ids, pos_ids, None, self.word, self.pos, self.typ, self.eln_g, self.eln_b, cfg.eps)
         for L in self.layers:
-            # plain projections on hipBLASLt (bias in its epilogue); residual adds fused into the native
-            # LayerNorm; the up projection: see ``fused_up``
+            # every projection on the native MFMA GEMM (gemm256 at >= 1024 tokens) with the bias (and
+            # the up projection's GELU) in its epilogue; residual adds fused into the LayerNorm
             qkv = ops.linear(x, L.qkv_w, L.qkv_b)
             q = qkv[:, :H].view(T, nh, D)
             k = qkv[:, H:2 * H].view(T, nh, D)
@@ -77,10 +71,7 @@ class BertEncoder:
             a = ops.flash_attention_packed(q, k, v, cu_seqlens, cu_seqlens, max_seqlen, causal=False)
             h = ops.linear(a.view(T, H), L.o_w, L.o_b)
             x = ops.layernorm(h, L.ln1_g, L.ln1_b, cfg.eps, residual=x)
-            if self.fused_up:
-                f = ops.linear(x, L.i_w, L.i_b, act="gelu")  # native MFMA GEMM, bias+GELU(erf) epilogue
-            else:
-                f = ops.gelu(ops.linear(x, L.i_w), L.i_b)  # hipBLASLt + one bias+GELU(erf) pass
+            f = ops.linear(x, L.i_w, L.i_b, act="gelu")  # bias + GELU(erf) epilogue
             h = ops.linear(f, L.d_w, L.d_b)
             x = ops.layernorm(h, L.ln2_g, L.ln2_b, cfg.eps, residual=x)
         return x

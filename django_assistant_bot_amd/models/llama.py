@@ -22,7 +22,6 @@ import torch
 
 from .. import ops
 from ..ops import reference as ref
-from ..ops import tuning
 from .configs import DecoderConfig
 
 
@@ -106,6 +105,7 @@ class LlamaModel:
         # 39.7 -> 29.2, gate_up 51.8 + 5.1 (SiLU) -> 53.0 with SwiGLU fused, at M = 128
         # (profiles/decode_stream_gemm.md).  DAB_DECODE_GEMM=skinny keeps the split-K kernel above.
         self.stream = False
+        self.lm_head_ws = None
         if (os.environ.get("DAB_DECODE_GEMM", "stream") == "stream" and self.device.type == "cuda"
                 and self.use_skinny):
             self.stream = self._make_stream_copies()
@@ -136,16 +136,21 @@ class LlamaModel:
         return w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
 
     def _make_stream_copies(self) -> bool:
-        """Shuffled decode copies of the projection weights when they fit comfortably (each copy is
+        """Shuffled decode copies of the projection weights (and of the LM head, which decode and
+        the prefill last-token logits stream at M <= 128) when they fit comfortably (each copy is
         the size of the weights; the KV pool is sized from what is left)."""
         names = ("qkv", "o", "gate_up", "down") if self.interleaved_mlp else ("qkv", "o", "down")
         mats = [(L, n) for L in self.layers for n in names if self._stream_ok(getattr(L, f"{n}_w"))]
         extra = sum(getattr(L, f"{n}_w").numel() * 2 for L, n in mats)
+        head = self._stream_ok(self.lm_head)
+        extra += self.lm_head.numel() * 2 if head else 0
         free, _ = torch.cuda.mem_get_info(self.device)
         if not mats or extra > 0.4 * free:
             return False
         for L, n in mats:
             setattr(L, f"{n}_ws", ops.shuffle_weights(getattr(L, f"{n}_w")))
+        if head:
+            self.lm_head_ws = ops.shuffle_weights(self.lm_head)
         return True
 
     @staticmethod
@@ -169,14 +174,15 @@ class LlamaModel:
 
     def _proj(self, x, w, sk: bool, allow_slabs: bool = True, name: str = "", ws=None):
         """Projection of the decode (``sk``: weight-streaming kernel, fp32 split-K slabs when the
-        consumer can sum them) or prefill path (hipBLASLt)."""
+        consumer can sum them) or prefill path (native MFMA GEMM: the 256x256 8-phase kernel for
+        large token counts, ``gemm256.hip``)."""
         if sk and ws is not None:
             cfg = self.STREAM_CFG_M64 if x.shape[0] <= 64 else self.STREAM_CFG_M128
             s = self._stream_splits(w.shape[0], w.shape[1])
             out = ops.stream_gemm(x, ws, splits=s, cfg=cfg, nt=True)
             return ops.skinny_reduce(out) if (s > 1 and not allow_slabs) else out
         if not sk or name not in self.skinny_for:
-            return tuning.linear(x, w) if x.is_cuda else ops.linear(x, w)
+            return ops.gemm_bt(x, w) if x.is_cuda else ops.linear(x, w)
         s = self._splits(w)
         if s > 1 and not allow_slabs:
             return ops.skinny_reduce(ops.skinny_gemm(x, w, splits=s))
@@ -223,8 +229,10 @@ class LlamaModel:
                                   cfg=self.STREAM_CFG_M64 if T <= 64 else self.STREAM_CFG_M128)
         elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
             act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
+        elif self.interleaved_mlp and h.is_cuda:
+            act = ops.gemm_bt(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)  # SwiGLU in the GEMM epilogue
         else:
-            gu = tuning.linear(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
+            gu = ops.gemm_bt(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
             act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down", ws=L.down_ws))
         return x, residual
@@ -292,8 +300,15 @@ class LlamaModel:
         return a
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
-        """[n, H] -> [n, V] logits (bf16 GEMM; the sampler reads bf16 or fp32)."""
-        if ("lm_head" in self.skinny_for and h.is_cuda and h.shape[0] <= ops.SKINNY_MAX_M
-                and self.lm_head.shape[0] % 64 == 0):
+        """[n, H] -> [n, V] logits (bf16; the sampler reads bf16 or fp32).  Up to 128 rows (decode
+        steps, prefill last tokens) stream the shuffled LM-head copy through ``stream_gemm``;
+        larger batches run the native MFMA GEMM."""
+        if not h.is_cuda:
+            return ops.linear(h, self.lm_head)
+        n = h.shape[0]
+        if self.lm_head_ws is not None and n <= 128:
+            cfg = self.STREAM_CFG_M64 if n <= 64 else self.STREAM_CFG_M128
+            return ops.stream_gemm(h, self.lm_head_ws, cfg=cfg, nt=True)
+        if "lm_head" in self.skinny_for and n <= ops.SKINNY_MAX_M and self.lm_head.shape[0] % 64 == 0:
             return ops.skinny_gemm(h, self.lm_head)
-        return tuning.linear(h, self.lm_head) if h.is_cuda else ops.linear(h, self.lm_head)
+        return ops.gemm_bt(h, self.lm_head)

@@ -589,16 +589,34 @@ def topk_rows(scores, k, index_base=0, want_global=False):
     return vals, idx
 
 
-def linear(x, w, b=None, residual=None, act=None, use_native=False):
-    """y = x W^T (+b) (+act) (+residual).  Fused epilogues run on the native MFMA GEMM; a plain
-    projection may run on hipBLASLt through torch (vendor library GEMM)."""
-    if not x.is_cuda:
-        epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]
-        return ref.gemm_bt(x, w, b, residual, epi)
-    if act is None and residual is None and not use_native:
-        return F.linear(x, w, b)
+def linear(x, w, b=None, residual=None, act=None):
+    """y = x W^T (+b) (+act) (+residual) on the native MFMA GEMMs (``gemm_bt``: the 256x256 8-phase
+    kernel for large token counts, the 128x128 kernel otherwise), epilogues fused.  Shapes the
+    kernels cannot take (K % 64, N % 4) fall back to torch with a one-time warning."""
     epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]
-    x2 = x.reshape(-1, x.shape[-1])
+    if not x.is_cuda:
+        return ref.gemm_bt(x, w, b, residual, epi)
+    K, N = x.shape[-1], w.shape[0]
+    if K % 64 or N % 4 or (epi == EPI_SWIGLU and N % 32):
+        _warn_once(f"linear: K={K} N={N} not supported by the native GEMM; torch fallback")
+        y = F.linear(x, w, b)
+        if act == "gelu":
+            y = F.gelu(y)
+        elif act == "swiglu":
+            y = silu_mul(y, interleaved=True)
+        return y + residual if residual is not None else y
+    x2 = x.reshape(-1, K)
     r2 = residual.reshape(x2.shape[0], -1) if residual is not None else None
     y = gemm_bt(x2, w, b, r2, epi)
     return y.view(*x.shape[:-1], y.shape[-1])
+
+
+_WARNED: set = set()
+
+
+def _warn_once(msg: str) -> None:
+    if msg not in _WARNED:
+        _WARNED.add(msg)
+        import logging
+
+        logging.getLogger(__name__).warning(msg)
