@@ -203,13 +203,22 @@ class DjangoIngestRepository(IngestRepository):
         model = self._model(kind)
         for r, v in zip(rows, vectors):
             r.embedding = list(v)
-        await sync_to_async(model.objects.bulk_update)(rows, fields=["embedding"])
+
+        def save():
+            from assistant.storage.index import get_index_service
+
+            model.objects.bulk_update(rows, fields=["embedding"])
+            get_index_service().upsert_objects(model, rows, "embedding")  # bulk_update fires no signals
+        await sync_to_async(save)()
 
     async def nearest_earlier_question(self, document, embedding):
         from assistant.rag.services.search_service import embedding_search_questions
         from assistant.storage.models import Question
 
-        hits = await embedding_search_questions(embedding, Question.objects.filter(document__id__lt=document.id), n=1)
+        from assistant.storage.index import with_index_filter
+
+        qs = with_index_filter(Question.objects.filter(document__id__lt=document.id), doc_lt=document.id)
+        hits = await embedding_search_questions(embedding, qs, n=1)
         return (hits[0], float(hits[0].distance)) if hits else None
 
     async def delete_question(self, question):
@@ -224,8 +233,12 @@ class DjangoIngestRepository(IngestRepository):
         from assistant.storage.models import WikiDocumentProcessing
 
         def run():
+            from assistant.storage.index import get_index_service
+
             with transaction.atomic():
                 processing.status = WikiDocumentProcessing.Status.COMPLETED
                 processing.save(update_fields=["status"])
                 processing.wiki_document.processing.exclude(id=processing.id).delete()
+            # the wiki's rows now match the COMPLETED filter: re-mirror their group bit
+            get_index_service().refresh_wiki(processing.wiki_document_id)
         await sync_to_async(run)()

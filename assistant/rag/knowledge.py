@@ -23,6 +23,11 @@ from typing import Dict, List, Optional, Sequence, Tuple
 from assistant.rag.aggregation import aggregate_documents
 from assistant.utils.sync import sync_to_async
 
+try:
+    import torch
+except ImportError:  # pragma: no cover - the memory knowledge base needs torch; Django paths do not
+    torch = None
+
 
 @dataclasses.dataclass
 class Topic:
@@ -148,8 +153,12 @@ class MemoryKnowledgeBase(KnowledgeBase):
         return self._search(embedding, n)
 
     async def search_documents(self, query, embedding, max_scores_n, top_n):
-        hits = self._search(embedding, max_scores_n * top_n * 10)
-        ranked = aggregate_documents([h.distance for h in hits], [h.document_id for h in hits], max_scores_n, top_n)
+        # broad search: (similarity, document) of the k nearest questions in ONE device->host copy,
+        # then the native per-document aggregation -- no per-hit Python objects
+        sims, ids, docs = self.index.search([list(embedding)], max_scores_n * top_n * 10)
+        sd = torch.stack([sims[0].double(), docs[0].double()]).cpu().numpy()
+        live = ids[0].cpu().numpy() >= 0 if sims.is_cuda else ids[0].numpy() >= 0
+        ranked = aggregate_documents(1.0 - sd[0][live], sd[1][live].astype("int64"), max_scores_n, top_n)
         return [(self.documents[d], s) for d, s in ranked if d in self.documents]
 
     async def get_document(self, doc_id):
@@ -166,9 +175,11 @@ class DjangoKnowledgeBase(KnowledgeBase):
         self.bot = bot
 
     def _completed_questions(self):
+        from assistant.storage.index import with_index_filter
         from assistant.storage.models import Question, WikiDocumentProcessing
-        return Question.objects.filter(document__wiki__bot=self.bot,
-                                       document__wiki__processing__status=WikiDocumentProcessing.Status.COMPLETED)
+        qs = Question.objects.filter(document__wiki__bot=self.bot,
+                                     document__wiki__processing__status=WikiDocumentProcessing.Status.COMPLETED)
+        return with_index_filter(qs, bot=self.bot, completed=True)  # one group compare in the index
 
     async def topics(self, examples_per_topic: int = 2) -> List[Topic]:
         from assistant.storage.models import Question, WikiDocument, WikiDocumentProcessing

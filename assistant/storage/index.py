@@ -39,25 +39,115 @@ def _key(model, field: str) -> str:
     return f"{model._meta.label_lower}.{field}"
 
 
+def row_group(bot_id, completed) -> np.ndarray:
+    """Row group the index kernels filter on: ``bot_id * 2 + completed`` (completed = the row's wiki
+    has a COMPLETED processing run), so the reference's hot filter ``document__wiki__bot=B,
+    document__wiki__processing__status=COMPLETED`` (steps/embeddings.py:26-29) is ONE group compare
+    in the score epilogue -- no pk list, no mask."""
+    b = np.asarray(bot_id, dtype=np.int64)
+    return (b * 2 + np.asarray(completed, dtype=np.int64)).astype(np.int32)
+
+
+def _completed_wikis() -> set:
+    from assistant.storage.models import WikiDocumentProcessing
+
+    return set(WikiDocumentProcessing.objects.filter(status=WikiDocumentProcessing.Status.COMPLETED)
+               .values_list("wiki_document_id", flat=True))
+
+
 def _meta_values(model, field, qs=None):
     """(ids, doc_ids, groups, vectors) of the rows with a non-null vector."""
     qs = model.objects.all() if qs is None else qs
     if model._meta.label_lower == "assistant_storage.document":
-        rows = qs.exclude(**{f"{field}__isnull": True}).values_list("id", "id", "wiki__bot_id", field)
+        rows = qs.exclude(**{f"{field}__isnull": True}).values_list("id", "id", "wiki__bot_id", "wiki_id", field)
     else:
         rows = qs.exclude(**{f"{field}__isnull": True}).values_list("id", "document_id", "document__wiki__bot_id",
-                                                                     field)
-    ids, docs, groups, vecs = [], [], [], []
-    for i, d, g, v in rows.iterator(chunk_size=4096):
+                                                                     "document__wiki_id", field)
+    ids, docs, bots, wikis, vecs = [], [], [], [], []
+    for i, d, b, w, v in rows.iterator(chunk_size=4096):
         if v is None:
             continue
         ids.append(i)
         docs.append(d if d is not None else -1)
-        groups.append(g if g is not None else 0)
+        bots.append(b if b is not None else 0)
+        wikis.append(w if w is not None else -1)
         vecs.append(np.asarray(v, dtype=np.float32))
     dim = len(vecs[0]) if vecs else 0
-    return (np.asarray(ids, dtype=np.int64), np.asarray(docs, dtype=np.int64), np.asarray(groups, dtype=np.int32),
+    done = np.isin(np.asarray(wikis, dtype=np.int64), np.fromiter(_completed_wikis(), dtype=np.int64)) if ids else []
+    return (np.asarray(ids, dtype=np.int64), np.asarray(docs, dtype=np.int64), row_group(bots, done),
             np.stack(vecs) if vecs else np.zeros((0, dim), dtype=np.float32))
+
+
+# ------------------------------------------------------------------------------ QuerySet filter shapes
+
+class IndexFilter:
+    """A QuerySet filter the index evaluates itself: ``group`` (bot * 2 + completed), ``doc_lt``
+    (document id bound), or ``all``.  ``None`` from ``index_filter_of`` = generic (pk allow-list)."""
+
+    def __init__(self, group=None, doc_lt=None):
+        self.group, self.doc_lt = group, doc_lt
+
+    def __repr__(self):
+        return f"IndexFilter(group={self.group}, doc_lt={self.doc_lt})"
+
+
+HINT_ATTR = "_dab_index_filter"
+
+
+def with_index_filter(qs, *, bot=None, completed=None, doc_lt=None):
+    """Attach the filter the QuerySet encodes so the index can evaluate it without touching the DB.
+    Used by the framework's own call sites; foreign QuerySets are recognised by ``index_filter_of``."""
+    if bot is not None and completed:
+        setattr(qs, HINT_ATTR, IndexFilter(group=int(row_group(getattr(bot, "pk", bot), 1))))
+    elif doc_lt is not None and bot is None and completed is None:
+        setattr(qs, HINT_ATTR, IndexFilter(doc_lt=int(doc_lt)))
+    return qs
+
+
+def index_filter_of(qs):
+    """IndexFilter for the two QuerySet shapes the framework searches with (reference
+    steps/embeddings.py:26-29 and processing steps/questions.py:121-126), IndexFilter() for an
+    unfiltered QuerySet, None for anything else."""
+    hint = getattr(qs, HINT_ATTR, None)
+    if hint is not None:
+        return hint
+    where = qs.query.where
+    if not where:
+        return IndexFilter()
+    try:
+        return _recognise(qs, where)
+    except Exception:  # unknown Django internals / lookups: generic path
+        return None
+
+
+def _recognise(qs, where):
+    if where.negated or where.connector != "AND" or qs.query.low_mark or qs.query.high_mark is not None:
+        return None
+    bot = completed = doc_lt = None
+    for child in where.children:
+        if not hasattr(child, "lhs") or not hasattr(child, "rhs"):
+            return None
+        target = getattr(child.lhs, "target", None)
+        if target is None:
+            return None
+        label, name, lookup = target.model._meta.label_lower, target.name, child.lookup_name
+        rhs = getattr(child.rhs, "pk", child.rhs)
+        if label == "assistant_storage.wikidocument" and name == "bot" and lookup == "exact":
+            bot = int(rhs)
+        elif (label == "assistant_storage.wikidocumentprocessing" and name == "status" and lookup == "exact"
+              and rhs == "completed"):
+            completed = True
+        elif ((label == "assistant_storage.document" and name == "id")
+              or (label in ("assistant_storage.question", "assistant_storage.sentence") and name == "document")) \
+                and lookup == "lt":
+            doc_lt = int(rhs)
+        else:
+            return None
+    if bot is not None and completed and doc_lt is None:
+        return IndexFilter(group=int(row_group(bot, 1)))
+    if doc_lt is not None and bot is None and completed is None:
+        return IndexFilter(doc_lt=doc_lt)
+    return None
 
 
 class _EngineBackend:
@@ -83,13 +173,14 @@ class _EngineBackend:
         if name in self._idx:
             self._idx[name].remove(ids)
 
-    def search(self, name, q, n, allowed, group):
+    def search(self, name, q, n, allowed, group, doc_lt=None):
         idx = self._idx.get(name)
         if idx is None or len(idx) == 0:
             return [], []
         sims, ids, _ = idx.search(np.asarray(q, dtype=np.float32)[None], min(n, 1024),
                                   q_groups=None if group is None else [group],
-                                  allowed=None if allowed is None else [set(allowed)])
+                                  allowed=None if allowed is None else [allowed],
+                                  doc_lt=None if doc_lt is None else [doc_lt])
         sims, ids = sims[0].float().cpu().numpy(), ids[0].cpu().numpy()
         keep = ids >= 0
         return ids[keep].tolist(), (1.0 - sims[keep]).tolist()
@@ -120,10 +211,11 @@ class _GPUServiceBackend:
     def remove(self, name, ids):
         self._post(f"/index/{name}/delete", {"ids": list(map(int, ids))})
 
-    def search(self, name, q, n, allowed, group):
+    def search(self, name, q, n, allowed, group, doc_lt=None):
         r = self._post(f"/index/{name}/search", {"queries": [list(map(float, q))], "k": int(n),
                                                  "groups": None if group is None else [int(group)],
-                                                 "allowed": None if allowed is None else [list(map(int, allowed))]})
+                                                 "allowed": None if allowed is None else [list(map(int, allowed))],
+                                                 "doc_lt": None if doc_lt is None else [int(doc_lt)]})
         return r["ids"][0], r["distances"][0]
 
 
@@ -131,6 +223,7 @@ class IndexService:
     def __init__(self, backend: str | None = None):
         self.backend_name = backend or settings.get("VECTOR_INDEX_BACKEND", None) or self._default_backend()
         self._lock = threading.RLock()
+        self.stats = {"fast": 0, "generic": 0}
         if self.backend_name == "engine":
             self._be = _EngineBackend()
         elif self.backend_name == "gpu_service":
@@ -189,6 +282,23 @@ class IndexService:
         with self._lock:
             self._be.upsert(name, ids, vecs, docs, groups)
 
+    def refresh_wiki(self, wiki_id):
+        """Re-mirror every searchable row of one wiki (finalize flips its completed bit and deletes the
+        older runs' rows through the cascade)."""
+        if self._be is None:
+            return
+        from assistant.storage.models import Document, Question, Sentence
+
+        for model, field, flt in ((Question, "embedding", "document__wiki_id"),
+                                  (Sentence, "embedding", "document__wiki_id"),
+                                  (Document, "content_embedding", "wiki_id")):
+            name = _key(model, field)
+            if not self._be.loaded(name):
+                continue
+            ids, docs, groups, vecs = _meta_values(model, field, model.objects.filter(**{flt: wiki_id}))
+            with self._lock:
+                self._be.upsert(name, ids, vecs, docs, groups)
+
     def remove(self, model, ids, field="embedding"):
         if self._be is None:
             return
@@ -199,18 +309,26 @@ class IndexService:
 
     # ---------------------------------------------------------------- search
     def search(self, qs, query_embedding, n: int, field: str = "embedding"):
-        """Exact cosine search restricted to the QuerySet -> [(pk, distance)] ascending distance."""
+        """Exact cosine search restricted to the QuerySet -> [(pk, distance)] ascending distance.
+
+        The framework's two filter shapes (bot + COMPLETED, document id bound) and unfiltered
+        QuerySets are evaluated inside the index (group compare / device mask; the group form keeps
+        the threshold-search kernel); any other filter becomes a pk allow-list fetched with one
+        ``values_list`` and mapped to rows vectorised."""
         model = qs.model
         q = np.asarray(query_embedding, dtype=np.float32)
         if self._be is None:
             return self._db_search(qs, q, n, field)
         self.ensure_loaded(model, field)
+        flt = index_filter_of(qs)
         allowed = None
-        if qs.query.where:  # any filter -> exact allow-list (unfiltered QuerySets scan everything)
-            allowed = list(qs.values_list("pk", flat=True))
-            if not allowed:
+        if flt is None:
+            allowed = np.fromiter(qs.values_list("pk", flat=True), dtype=np.int64)
+            if not len(allowed):
                 return []
-        ids, dist = self._be.search(_key(model, field), q, n, allowed, None)
+            flt = IndexFilter()
+        self.stats["fast" if allowed is None else "generic"] += 1
+        ids, dist = self._be.search(_key(model, field), q, n, allowed, flt.group, flt.doc_lt)
         return list(zip(ids, dist))
 
     @staticmethod

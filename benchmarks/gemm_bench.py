@@ -67,6 +67,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
     ap.add_argument("--only", default="", help="comma list of op names to run")
+    ap.add_argument("--gm", default="", help="comma list of tile-group sizes to A/B (DAB_GEMM256_GM)")
     ap.add_argument("--ab-persist", action="store_true", help="also time one-workgroup-per-tile launches")
     args = ap.parse_args()
     os.environ.setdefault("DAB_GEMM256", "1")
@@ -88,6 +89,14 @@ def main():
             arms = [("nat", lambda: run_native(a, w, b, kind, out)), ("lib", lambda: run_lib(a, w, b, kind))]
             if args.native_only:
                 arms = arms[:1]
+            for gm in [int(x) for x in args.gm.split(",") if x]:
+                def gm_arm(gm=gm):
+                    os.environ["DAB_GEMM256_GM"] = str(gm)
+                    try:
+                        run_native(a, w, b, kind, out)
+                    finally:
+                        os.environ.pop("DAB_GEMM256_GM", None)
+                arms.append((f"gm{gm}", gm_arm))
             if args.ab_persist:
                 def nonp():
                     os.environ["DAB_GEMM256_PERSIST"] = "0"
@@ -97,6 +106,7 @@ def main():
                         os.environ["DAB_GEMM256_PERSIST"] = "1"
                 arms.append(("np", nonp))
             npers = []
+            extra = {}
             for _ in range(args.rounds):
                 for arm, fn in arms:
                     fn()
@@ -106,7 +116,8 @@ def main():
                     ev[1].record()
                     torch.cuda.synchronize()
                     t = ev[0].elapsed_time(ev[1]) / args.iters * 1e3
-                    {"nat": nat, "lib": lib, "np": npers}[arm].append(t)
+                    extra.setdefault(arm, []).append(t) if arm not in ("nat", "lib", "np") else \
+                        {"nat": nat, "lib": lib, "np": npers}[arm].append(t)
             nat.sort()
             lib.sort()
             lib = lib or [float("nan")]
@@ -118,7 +129,8 @@ def main():
                               "native_tflops": round(flop / tn / 1e6, 1), "lib_tflops": round(flop / tl / 1e6, 1),
                               "speedup": round(tl / tn, 3), "max_abs_err": round(err, 5),
                               "ref_max": round(scale, 3), "ok": err <= 0.02 * max(scale, 1.0),
-                              **({"nonpersist_us": round(sorted(npers)[len(npers) // 2], 1)} if npers else {})}),
+                              **({"nonpersist_us": round(sorted(npers)[len(npers) // 2], 1)} if npers else {}),
+                              **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()}}),
                   flush=True)
             del a, w, b, out
             torch.cuda.empty_cache()

@@ -46,6 +46,7 @@ struct G256 {
   const bf16* residual;
   int M, N, K;
   long lda, ldb, ldc, ldr;
+  int gm;  // tile rows per group of the grouped tile order
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -74,8 +75,7 @@ constexpr int kHalf = 16384;  // 128 rows x 128 B
 }  // namespace
 
 // grouped tile order: tile id -> (m0, n0), column-major inside groups of GM tile rows
-__device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int& m0, int& n0) {
-  constexpr int GM = 4;
+__device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int GM, int& m0, int& n0) {
   const int per_group = GM * tiles_n;
   const int grp = sid / per_group, first_m = grp * GM;
   const int gsz = min(GM, tiles_m - first_m);
@@ -103,7 +103,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   int sid = cstart + l;
   if (sid >= cend) return;  // whole workgroup: uniform
   int m0, n0;
-  tile_of(sid, tiles_m, tiles_n, m0, n0);
+  tile_of(sid, tiles_m, tiles_n, p.gm, m0, n0);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -215,7 +215,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     const int nsid = sid + nper;
     const bool more = nsid < cend;
     int nm0 = m0, nn0 = n0;
-    if (more) tile_of(nsid, tiles_m, tiles_n, nm0, nn0);
+    if (more) tile_of(nsid, tiles_m, tiles_n, p.gm, nm0, nn0);
     const __amdgpu_buffer_rsrc_t nA = rsrc_a(nm0), nB = rsrc_b(nn0);
     for (int it = 0; it < iters; ++it) {
       const bool last = it == iters - 1;
@@ -450,6 +450,9 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = ((M + 255) / 256) * (N / 256);
   // persistent: one workgroup (128 KB of LDS) per CU; DAB_GEMM256_PERSIST=0 launches one per tile
+  const char* ge = getenv("DAB_GEMM256_GM");
+  p.gm = ge ? atoi(ge) : 4;
+  if (p.gm < 1) p.gm = 1;
   const char* pe = getenv("DAB_GEMM256_PERSIST");
   const bool persist = !(pe && pe[0] == '0');
   const int nwg = (persist && tiles > cus) ? cus : tiles;

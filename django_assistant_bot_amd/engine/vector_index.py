@@ -31,6 +31,7 @@ class VectorIndex:
         self.stats = {"threshold_searches": 0, "threshold_overflows": 0}
         self.vecs = self.row_ids = self.row_docs = self.row_group = None
         self._row_of: dict[int, int] = {}
+        self._sorted = None  # lazily built (sorted ids, rows) for vectorised id -> row lookups
         self._dead = 0
         self._grow(max(64, capacity))
 
@@ -75,6 +76,7 @@ class VectorIndex:
         if (grp < 0).any():
             raise ValueError("groups must be >= 0 (negative marks deleted rows)")
         idl = ids.tolist()
+        self._sorted = None
         if len(set(idl)) == n and not (self._row_of.keys() & set(idl)):
             # bulk insert of new ids (ingest): C-speed bookkeeping, contiguous rows
             if self.n + n > self._cap:
@@ -113,6 +115,7 @@ class VectorIndex:
     def remove(self, ids) -> int:
         rows = [self._row_of.pop(int(x)) for x in np.asarray(ids).reshape(-1).tolist() if int(x) in self._row_of]
         if rows:
+            self._sorted = None
             r = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
             self.row_group[r] = -1
             self.row_ids[r] = -1
@@ -133,33 +136,75 @@ class VectorIndex:
         self._dead = 0
         ids = self.row_ids[:m].cpu().numpy()
         self._row_of = {int(x): i for i, x in enumerate(ids.tolist())}
+        self._sorted = None
 
     # ------------------------------------------------------------------ search
-    def allow_mask(self, allowed: list) -> torch.Tensor:
-        """Per-query allowed item-id sets -> int32 bitmask [q, ceil(n/32)] over rows."""
+    def rows_of(self, ids) -> np.ndarray:
+        """Row index of each live item id (ids that are not in the index are dropped).  Vectorised
+        through a sorted (id, row) table rebuilt lazily after upserts / deletes."""
+        ids = np.asarray(ids, dtype=np.int64).reshape(-1)
+        if self._sorted is None:
+            keys = np.fromiter(self._row_of.keys(), dtype=np.int64, count=len(self._row_of))
+            vals = np.fromiter(self._row_of.values(), dtype=np.int64, count=len(self._row_of))
+            order = np.argsort(keys, kind="stable")
+            self._sorted = (keys[order], vals[order])
+        keys, vals = self._sorted
+        if not len(keys) or not len(ids):
+            return np.zeros(0, dtype=np.int64)
+        pos = np.searchsorted(keys, ids)
+        pos = np.minimum(pos, len(keys) - 1)
+        hit = keys[pos] == ids
+        return vals[pos[hit]]
+
+    def _pack_rows(self, row_mask: torch.Tensor) -> torch.Tensor:
+        """bool [q, words*32] row mask (device) -> int32 bitmask [q, words] for the score epilogue."""
+        q, nb = row_mask.shape
+        w = row_mask.view(q, nb // 32, 32).to(torch.int64) << torch.arange(32, device=row_mask.device)
+        packed = w.sum(-1)
+        packed = packed - (packed >= (1 << 31)).to(torch.int64) * (1 << 32)
+        return packed.to(torch.int32).contiguous()
+
+    def allow_mask(self, allowed) -> torch.Tensor:
+        """Per-query allowed item ids (sets, lists or int arrays) -> int32 bitmask [q, ceil(n/32)] over
+        rows, built on the device (no per-id Python loop)."""
         words = (self.n + 31) // 32
-        m = np.zeros((len(allowed), words * 32), dtype=bool)
+        m = torch.zeros((len(allowed), words * 32), dtype=torch.bool, device=self.device)
         for qi, ids in enumerate(allowed):
-            rows = [self._row_of[i] for i in ids if i in self._row_of]
-            m[qi, rows] = True
-        bits = m.reshape(len(allowed), words, 32).astype(np.uint64) << np.arange(32, dtype=np.uint64)
-        packed = bits.sum(-1).astype(np.uint32).view(np.int32)
-        return torch.from_numpy(np.ascontiguousarray(packed)).to(self.device)
+            ids = np.fromiter(ids, dtype=np.int64) if isinstance(ids, (set, frozenset)) else ids
+            rows = self.rows_of(ids)
+            if len(rows):
+                m[qi, torch.from_numpy(rows).to(self.device)] = True
+        return self._pack_rows(m)
+
+    def doc_lt_mask(self, limits) -> torch.Tensor:
+        """Rows whose document id is < limits[q] (the ingest dedup filter ``document__id__lt``),
+        bitmask built from the row metadata on the device."""
+        words = (self.n + 31) // 32
+        lim = torch.as_tensor(np.asarray(limits, dtype=np.int64), device=self.device)[:, None]
+        m = torch.zeros((len(limits), words * 32), dtype=torch.bool, device=self.device)
+        m[:, : self.n] = self.row_docs[None, : self.n] < lim
+        return self._pack_rows(m)
 
     @torch.inference_mode()
-    def scores(self, queries: torch.Tensor, q_groups=None, allowed=None) -> torch.Tensor:
-        """fp32 cosine similarities [q, n] (-inf for filtered / deleted rows)."""
+    def scores(self, queries: torch.Tensor, q_groups=None, allowed=None, doc_lt=None) -> torch.Tensor:
+        """fp32 cosine similarities [q, n] (-inf for filtered / deleted rows).  Filters: ``q_groups``
+        (per-query row group, e.g. bot + status bit), ``allowed`` (per-query item ids), ``doc_lt``
+        (per-query document-id bound); masks are ANDed."""
         q = F.normalize(torch.as_tensor(queries).to(self.device, torch.float32), dim=-1).to(self.dtype)
         qg = None if q_groups is None else torch.as_tensor(q_groups, dtype=torch.int32).to(self.device)
         allow = None if allowed is None else self.allow_mask(allowed)
+        if doc_lt is not None:
+            dm = self.doc_lt_mask(doc_lt)
+            allow = dm if allow is None else allow & dm
         n = max(self.n, 4)
         n = (n + 3) // 4 * 4
         return ops.gemm_bt(q, self.vecs[:n], epilogue=ops.EPI_SCORES, out_f32=True, row_group=self.row_group[:n],
                            q_group=qg, allow=allow)
 
     @torch.inference_mode()
-    def search(self, queries, k: int, q_groups=None, allowed=None):
-        """-> (similarity [q, k] fp32 desc, item ids [q, k] int64 (-1 = none), doc ids [q, k] int64)."""
+    def search(self, queries, k: int, q_groups=None, allowed=None, doc_lt=None):
+        """-> (similarity [q, k] fp32 desc, item ids [q, k] int64 (-1 = none), doc ids [q, k] int64).
+        Group-only filters keep the exact threshold path (no score matrix) on large indexes."""
         queries = torch.as_tensor(queries)
         if queries.ndim == 1:
             queries = queries[None]
@@ -168,13 +213,13 @@ class VectorIndex:
             z = torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=self.device)
             return torch.full((nq, max(k, 0)), float("-inf"), device=self.device), z, z.clone()
         got = None
-        if (self.device.type == "cuda" and allowed is None and self.n >= self.threshold_min_rows
+        if (self.device.type == "cuda" and allowed is None and doc_lt is None and self.n >= self.threshold_min_rows
                 and k <= 1024 and self.threshold_search):
             got = self._threshold_search(queries, k, q_groups)
         if got is not None:
             vals, rows = got
         else:
-            s = self.scores(queries, q_groups, allowed)
+            s = self.scores(queries, q_groups, allowed, doc_lt)
             kk = min(k, s.shape[1], 1024)
             vals, rows = ops.topk_rows(s, kk)
         rows = rows.long()
@@ -236,5 +281,6 @@ class VectorIndex:
         idx.row_group[:n] = st["group"].to(idx.device)
         idx.n = n
         idx._row_of = {int(x): i for i, x in enumerate(st["ids"].tolist()) if x >= 0}
+        idx._sorted = None
         idx._dead = n - len(idx._row_of)
         return idx

@@ -69,6 +69,7 @@ class SearchRequest(BaseModel):
     k: int = 10
     groups: Optional[List[int]] = None
     allowed: Optional[List[List[int]]] = None
+    doc_lt: Optional[List[int]] = None
 
 
 embedders: Dict[str, object] = {}
@@ -178,7 +179,8 @@ async def index_search(name: str, request: SearchRequest):
         return {"ids": [[] for _ in range(nq)], "distances": [[] for _ in range(nq)],
                 "doc_ids": [[] for _ in range(nq)]}
     with _index_lock:
-        sims, ids, docs = idx.search(request.queries, request.k, q_groups=request.groups, allowed=request.allowed)
+        sims, ids, docs = idx.search(request.queries, request.k, q_groups=request.groups, allowed=request.allowed,
+                                     doc_lt=request.doc_lt)
     out_ids, out_d, out_docs = [], [], []
     for s, i, d in zip(sims.tolist(), ids.tolist(), docs.tolist()):
         keep = [j for j, x in enumerate(i) if x >= 0]

@@ -1,0 +1,181 @@
+"""Filtered exact search: the index-side filters (group = bot*2 + completed, document-id bound,
+vectorised pk allow-lists) against a brute-force oracle, and the ORM bridge's QuerySet-shape
+recognition (reference steps/embeddings.py:26-29, processing steps/questions.py:121-126)."""
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from assistant.storage import index as index_mod
+from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+N, DIM = 3000, 64
+
+
+@pytest.fixture(scope="module")
+def data():
+    rng = np.random.default_rng(0)
+    vecs = rng.standard_normal((N, DIM)).astype(np.float32)
+    ids = rng.permutation(10 * N)[:N].astype(np.int64) + 5
+    docs = rng.integers(0, 400, N).astype(np.int64)
+    bots = rng.integers(1, 4, N)
+    done = rng.integers(0, 2, N)
+    groups = index_mod.row_group(bots, done)
+    return vecs, ids, docs, groups
+
+
+def oracle(vecs, ids, q, k, keep):
+    vn = vecs / np.linalg.norm(vecs, axis=1, keepdims=True)
+    qn = q / np.linalg.norm(q)
+    s = (torch.from_numpy(vn).to(torch.bfloat16).float().numpy() @
+         torch.from_numpy(qn).to(torch.bfloat16).float().numpy())
+    s = np.where(keep, s, -np.inf)
+    order = np.argsort(-s, kind="stable")[:k]
+    order = order[np.isfinite(s[order])]
+    return set(ids[order].tolist()), s[order]
+
+
+def build(data):
+    vecs, ids, docs, groups = data
+    idx = VectorIndex(DIM, device="cpu")
+    idx.add(ids, vecs, doc_ids=docs, groups=groups)
+    return idx
+
+
+def check(idx, data, q, k, keep, **kw):
+    vecs, ids, _, _ = data
+    sims, got, _ = idx.search(q[None], k, **kw)
+    got_ids = [i for i in got[0].tolist() if i >= 0]
+    exp_ids, exp_s = oracle(vecs, ids, q, k, keep)
+    assert len(got_ids) == len(exp_ids)
+    # ties at the k-th score may swap members: compare scores, and ids away from the boundary
+    np.testing.assert_allclose(np.sort(sims[0][: len(got_ids)].numpy())[::-1], np.sort(exp_s)[::-1], atol=1e-5)
+    assert len(set(got_ids) ^ exp_ids) <= 2
+
+
+@pytest.mark.parametrize("k", [1, 5, 250])
+def test_group_filter_matches_oracle(data, k):
+    idx = build(data)
+    q = np.random.default_rng(k).standard_normal(DIM).astype(np.float32)
+    g = int(index_mod.row_group(2, 1))
+    check(idx, data, q, k, data[3] == g, q_groups=[g])
+
+
+@pytest.mark.parametrize("bound", [0, 37, 200, 10_000])
+def test_doc_lt_filter_matches_oracle(data, bound):
+    idx = build(data)
+    q = np.random.default_rng(bound).standard_normal(DIM).astype(np.float32)
+    check(idx, data, q, 7, data[2] < bound, doc_lt=[bound])
+
+
+def test_allow_list_array_and_set_match_oracle(data):
+    idx = build(data)
+    rng = np.random.default_rng(3)
+    allowed = rng.choice(data[1], 500, replace=False)
+    keep = np.isin(data[1], allowed)
+    q = rng.standard_normal(DIM).astype(np.float32)
+    check(idx, data, q, 20, keep, allowed=[allowed])
+    check(idx, data, q, 20, keep, allowed=[set(allowed.tolist()) | {-99, 10 ** 9}])  # unknown ids ignored
+
+
+def test_filters_compose_and_survive_deletes(data):
+    idx = build(data)
+    vecs, ids, docs, groups = data
+    dead = ids[::7]
+    idx.remove(dead)
+    g = int(index_mod.row_group(1, 0))
+    keep = (groups == g) & (docs < 250) & ~np.isin(ids, dead)
+    q = np.random.default_rng(9).standard_normal(DIM).astype(np.float32)
+    check(idx, data, q, 50, keep, q_groups=[g], doc_lt=[250])
+    idx.compact()
+    check(idx, data, q, 50, keep, q_groups=[g], doc_lt=[250])
+
+
+def test_rows_of_is_vectorised_and_tracks_upserts(data):
+    idx = build(data)
+    ids = data[1]
+    rows = idx.rows_of(ids[:10])
+    assert rows.tolist() == [idx._row_of[int(i)] for i in ids[:10]]
+    idx.add([123456789], np.ones((1, DIM), np.float32), doc_ids=[1], groups=[0])
+    assert idx.rows_of([123456789]).tolist() == [idx._row_of[123456789]]
+    idx.remove([123456789])
+    assert idx.rows_of([123456789]).size == 0
+
+
+# ------------------------------------------------------------------ ORM bridge with stub QuerySets
+
+class _Meta:
+    def __init__(self, label):
+        self.label_lower = label
+
+
+def _field(label, name):
+    return types.SimpleNamespace(model=types.SimpleNamespace(_meta=_Meta(label)), name=name)
+
+
+def _lookup(label, name, lookup, rhs):
+    return types.SimpleNamespace(lhs=types.SimpleNamespace(target=_field(label, name)), lookup_name=lookup, rhs=rhs)
+
+
+class _Where(list):
+    negated = False
+    connector = "AND"
+
+    @property
+    def children(self):
+        return list(self)
+
+
+class StubQS:
+    def __init__(self, children, pks=()):
+        self.model = types.SimpleNamespace(_meta=_Meta("assistant_storage.question"))
+        self.query = types.SimpleNamespace(where=_Where(children), low_mark=0, high_mark=None)
+        self._pks = list(pks)
+        self.values_list_calls = 0
+
+    def values_list(self, *a, **kw):
+        self.values_list_calls += 1
+        return list(self._pks)
+
+
+def test_recognises_the_two_framework_filter_shapes():
+    bot = types.SimpleNamespace(pk=3)
+    hot = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot),
+                  _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed")])
+    f = index_mod.index_filter_of(hot)
+    assert f.group == int(index_mod.row_group(3, 1)) and f.doc_lt is None
+    dedup = StubQS([_lookup("assistant_storage.question", "document", "lt", 41)])
+    assert index_mod.index_filter_of(dedup).doc_lt == 41
+    assert index_mod.index_filter_of(StubQS([])).group is None
+    other = StubQS([_lookup("assistant_storage.question", "text", "icontains", "x")])
+    assert index_mod.index_filter_of(other) is None
+    mixed = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", 3)])  # bot without status
+    assert index_mod.index_filter_of(mixed) is None
+
+
+def test_hint_wins_over_recognition():
+    qs = index_mod.with_index_filter(StubQS([_lookup("x", "y", "exact", 1)]), bot=5, completed=True)
+    assert index_mod.index_filter_of(qs).group == int(index_mod.row_group(5, 1))
+
+
+def test_service_fast_and_generic_paths_equal_oracle(data, monkeypatch):
+    vecs, ids, docs, groups = data
+    svc = index_mod.IndexService(backend="engine")
+    svc._be.upsert("assistant_storage.question.embedding", ids, vecs, docs, groups)
+    monkeypatch.setattr(svc, "ensure_loaded", lambda *a: None)
+    q = np.random.default_rng(5).standard_normal(DIM).astype(np.float32)
+    bot = 2
+    hot = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot),
+                  _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed")])
+    got = svc.search(hot, q, 250)
+    assert hot.values_list_calls == 0 and svc.stats["fast"] == 1
+    exp, _ = oracle(vecs, ids, q, 250, groups == index_mod.row_group(bot, 1))
+    assert len(set(p for p, _ in got) ^ exp) <= 2
+    assert all(a[1] <= b[1] + 1e-6 for a, b in zip(got, got[1:]))  # ascending distance
+    # generic filter: one values_list, same answer as the oracle over the pk set
+    allowed = ids[groups == index_mod.row_group(bot, 1)]
+    gen = StubQS([_lookup("assistant_storage.question", "text", "icontains", "x")], pks=allowed.tolist())
+    got2 = svc.search(gen, q, 250)
+    assert gen.values_list_calls == 1 and svc.stats["generic"] == 1
+    assert [p for p, _ in got2] == [p for p, _ in got]
