@@ -20,7 +20,7 @@ Two load shapes (``--mode``):
     the load is in steady state; one "step" = C completed questions (warmup steps are not timed).
     The index is replicated per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
   * ``batch`` (default) -- one step = a batch of C questions answered together (retrieve all,
-    prefill all, decode all); the index is sharded across the ranks with an all-gather merge.
+    prefill all, decode all); the index is sharded across the ranks (queries all-gathered, partial top-k routed back with all_to_all).
     Measured at C=128 on one MI355X: batch 32.5 q/s p50 3.9 s; serve 30.3 q/s p50 4.2 s (mixed
     2048) -- large-M prefill GEMMs run at ~1.6 PFLOP/s, so mixing decode rows into smaller prefill
     chunks costs more than it saves (profiles/serving_mixed_steps.md).
@@ -313,7 +313,7 @@ def main():
                      if args.qps > 0 else
                      f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"),
             "index_rows": n_rows,
-            "index": "replicated per GPU" if serve else "sharded (all-gather merge)",
+            "index": "replicated per GPU" if serve else "sharded (all_to_all merge)",
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
             "graphs": llm.use_graphs,

@@ -1,13 +1,13 @@
 #!/usr/bin/env python
 """BASELINE config 3: in-HBM cosine top-k index sharded across the GPUs of a node, partial top-k
-merged with RCCL all-gather (the pgvector replacement).
+merged over RCCL (the pgvector replacement).
 
 Rows are owned by ``id % world``.  Each rank holds ``rows / world`` bf16 vectors.  A search of a
 query batch:
 
 1. all-gathers the queries;
 2. each rank runs the fused score GEMM + radix top-k on its shard;
-3. all-gathers the packed (score, id, doc) partials and merges.
+3. routes each rank's packed (score, id, doc) partials back to it with all_to_all (12 B per hit) and merges.
 
 ``ShardedIndex.search`` is the same path ``bench.py`` and the RAG pipeline use.
 
@@ -75,7 +75,7 @@ def main():
                         "scan_TBps": round(args.rows * args.dim * 2 / per_call / 1e12, 2)})
         assert ids.shape == (B, args.k)
     if R == 0:
-        print(json.dumps({"metric": "sharded in-HBM cosine top-k (RCCL all-gather merge)", "n_gpus": W,
+        print(json.dumps({"metric": "sharded in-HBM cosine top-k (RCCL all_to_all merge)", "n_gpus": W,
                           "rows": args.rows, "dim": args.dim, "k": args.k, "dtype": "bf16", "data": "synthetic",
                           "results": results}), flush=True)
     pdist.shutdown()

@@ -49,7 +49,10 @@ def embed_corpus(engine, text_of: Callable[[int], str], n: int, rank: int = 0, w
         v = engine.embed_tokens(np.asarray(flat), np.asarray(offs), out_dtype=torch.float32)
         if index is not None:
             target = getattr(index, "local", index)  # ShardedIndex -> its local VectorIndex (we own these ids)
-            target.add(part, v, doc_ids=None if doc_of is None else doc_of(part))
+            docs = None if doc_of is None else doc_of(part)
+            if hasattr(index, "_note_keys"):
+                index._note_keys(part, docs)
+            target.add(part, v, doc_ids=docs)
         if keep is not None or gather:
             out_vecs.append(v)
     if pool:

@@ -1,16 +1,18 @@
-"""Vector index sharded across the GPUs of a node; partial top-k merged with all-gather over xGMI.
+"""Vector index sharded across the GPUs of a node; partial top-k merged over RCCL / xGMI.
 
 Row ownership: ``owner(id) = id % world``, so ingest on any rank routes each vector to the rank that
-stores it and deletes need no broadcast.  A search batch of every rank is answered in three steps:
+stores it and deletes need no broadcast.  Two search collectives:
 
-  1. all-gather the query embeddings of all ranks (each rank scans its shard for ALL queries, so the
-     per-GPU scan work stays constant as the node grows -- weak scaling);
-  2. local fused score GEMM + exact top-k on the shard (``VectorIndex.search``);
-  3. all-gather the packed partial results ([queries, k] x {similarity, id, doc}) and merge each
-     rank's own queries with the top-k kernel over the W*k candidates.
+* ``search`` -- every rank brings its own query batch (DP replicas of the RAG pipeline):
+  all-gather the queries, scan the local shard for all of them, ``all_to_all`` each rank's partial
+  top-k back to that rank only, merge W x k candidates with the top-k kernel.
+* ``search_replicated`` -- every rank already holds the same batch (gpu_service's node group gets
+  it with the control broadcast): scan, ``gather`` the partials to the serving rank, merge there.
 
-Messages are tiny (k = 250 -> ~6 KB per query per rank): the collectives are latency-bound, one
-all-gather each, which RCCL issues over the fully connected xGMI links.
+Partials travel as (fp32 score bits, int32 id, int32 doc) = 12 B per hit (24 B only if an id
+outgrows int32).  At k = 250 that is 3 KB per query per rank: the collectives are latency-bound
+single calls over the fully connected xGMI links.  Reference counterpart: the per-query pgvector
+scan + Python aggregation of /root/reference/assistant/rag/services/search_service.py:129-152,185-196.
 """
 from __future__ import annotations
 
@@ -31,6 +33,8 @@ class ShardedIndex:
         self.local = VectorIndex(dim, device, capacity, dtype)
         self.device = self.local.device
         self.dim = dim
+        self._max_key = 0  # largest id / doc id stored here: picks the 12 B or 24 B partial packing
+        self.stats = {"merge_bytes_recv": 0}
 
     def owner(self, ids: np.ndarray) -> np.ndarray:
         return np.asarray(ids, dtype=np.int64) % self.world
@@ -45,8 +49,15 @@ class ShardedIndex:
         v = torch.as_tensor(vectors)[torch.from_numpy(sel)] if len(sel) != len(ids) else vectors
         d = None if doc_ids is None else np.asarray(doc_ids)[sel]
         g = None if groups is None else np.asarray(groups)[sel]
+        self._note_keys(ids[sel], d)
         self.local.add(ids[sel], v, d, g)
         return int(mine.sum())
+
+    def _note_keys(self, ids, docs=None) -> None:
+        if len(ids):
+            self._max_key = max(self._max_key, int(np.max(ids)))
+        if docs is not None and len(docs):
+            self._max_key = max(self._max_key, int(np.max(docs)))
 
     # ------------------------------------------------------------------ snapshots
     def save(self, directory: str) -> str:
@@ -86,8 +97,9 @@ class ShardedIndex:
                 if not mine.any():
                     continue
                 sel = torch.nonzero(live).view(-1)[torch.from_numpy(np.nonzero(mine)[0])]
-                idx.local.add(ids_np[mine], f.get_tensor("vecs")[sel], f.get_tensor("docs")[sel].numpy(),
-                              f.get_tensor("group")[sel].numpy())
+                docs_np = f.get_tensor("docs")[sel].numpy()
+                idx._note_keys(ids_np[mine], docs_np)
+                idx.local.add(ids_np[mine], f.get_tensor("vecs")[sel], docs_np, f.get_tensor("group")[sel].numpy())
         return idx
 
     def remove(self, ids) -> int:
@@ -104,9 +116,43 @@ class ShardedIndex:
     def _comm_device(self):
         return self.device if (self.distributed and dist.get_backend(self.group) == "nccl") else torch.device("cpu")
 
+    # ------------------------------------------------------------------ search
+    def _pack(self, sims, ids, docs, k: int, wide: bool) -> torch.Tensor:
+        """Partial top-k -> [q, k, 3] (score bits, id, doc): 12 B per hit as int32, 24 B only when an
+        id does not fit in int32."""
+        if sims.shape[1] < k:  # shard smaller than k: pad with empty hits
+            pad = k - sims.shape[1]
+            sims = torch.cat([sims, torch.full((sims.shape[0], pad), float("-inf"), device=sims.device)], 1)
+            ids = torch.cat([ids, torch.full((ids.shape[0], pad), -1, dtype=ids.dtype, device=ids.device)], 1)
+            docs = torch.cat([docs, torch.full((docs.shape[0], pad), -1, dtype=docs.dtype, device=docs.device)], 1)
+        dt = torch.int64 if wide else torch.int32
+        return torch.stack([sims.contiguous().view(torch.int32).to(dt), ids.to(dt), docs.to(dt)], -1)
+
+    def _merge(self, cand: torch.Tensor, k: int):
+        """cand [q, W*k, 3] packed partials of the same queries -> merged exact top-k."""
+        cand = cand.to(self.device)
+        cs = cand[..., 0].to(torch.int32).view(torch.float32).contiguous()
+        kk = min(k, cs.shape[1], 1024)
+        vals, pos = ops.topk_rows(cs, kk)
+        pos = pos.long()
+        out_ids = torch.gather(cand[..., 1], 1, pos).long()
+        out_docs = torch.gather(cand[..., 2], 1, pos).long()
+        dead = torch.isinf(vals)
+        return vals, out_ids.masked_fill(dead, -1), out_docs.masked_fill(dead, -1)
+
+    def _wide(self) -> bool:
+        return self._max_key >= 2 ** 31
+
     @torch.inference_mode()
     def search(self, queries, k: int, q_groups=None):
-        """Collective: every rank of the group must call it (with its own, possibly empty, batch)."""
+        """Collective: every rank of the group calls it with its OWN (possibly empty) batch.
+
+        1. all-gather the query batches (each rank scans its shard for every query of the node:
+           per-GPU scan work is fixed as the node grows -- weak scaling);
+        2. local exact top-k on the shard for all of them;
+        3. ``all_to_all``: the partial top-k of rank r's queries goes to rank r only (W x less
+           traffic than all-gathering every partial), packed in 12 B per hit;
+        4. each rank merges the W partial lists of its own queries with the top-k kernel."""
         q = torch.as_tensor(queries).to(self.device, torch.float32)
         if q.ndim == 1:
             q = q[None]
@@ -114,41 +160,64 @@ class ShardedIndex:
             return self.local.search(q, k, q_groups)
         cdev = self._comm_device()
         nq = q.shape[0]
-        # 1. gather every rank's queries (padded to the largest batch)
-        counts = [torch.zeros(1, dtype=torch.int64, device=cdev) for _ in range(self.world)]
-        dist.all_gather(counts, torch.tensor([nq], dtype=torch.int64, device=cdev), group=self.group)
-        counts = [int(c.item()) for c in counts]
+        meta = torch.tensor([nq, int(self._wide())], dtype=torch.int64, device=cdev)
+        metas = [torch.zeros_like(meta) for _ in range(self.world)]
+        dist.all_gather(metas, meta, group=self.group)
+        counts = [int(m[0]) for m in metas]
+        wide = any(int(m[1]) for m in metas)
         mx = max(counts)
         if mx == 0:
             z = torch.full((0, k), -1, dtype=torch.int64, device=self.device)
             return torch.full((0, k), float("-inf"), device=self.device), z, z.clone()
-        qg = torch.full((mx,), -1, dtype=torch.int32)
-        if q_groups is not None:
-            qg[:nq] = torch.as_tensor(q_groups, dtype=torch.int32)
+        # 1. queries (+ their group in the last column), padded to the largest batch for all_gather
         qpad = torch.zeros((mx, self.dim + 1), dtype=torch.float32, device=cdev)
         qpad[:nq, : self.dim] = q.to(cdev)
-        qpad[:, self.dim] = qg.to(cdev).float()
+        qpad[:, self.dim] = -1.0
+        if q_groups is not None:
+            qpad[:nq, self.dim] = torch.as_tensor(q_groups, dtype=torch.float32).to(cdev)
         allq = [torch.empty_like(qpad) for _ in range(self.world)]
         dist.all_gather(allq, qpad, group=self.group)
-        allq = torch.cat(allq, 0).to(self.device)
-        # 2. local exact top-k for every query of the node
-        kk = k
-        sims, ids, docs = self.local.search(allq[:, : self.dim], kk, allq[:, self.dim].to(torch.int32))
-        if sims.shape[1] < k:  # shard smaller than k: pad
-            pad = k - sims.shape[1]
-            sims = torch.cat([sims, torch.full((sims.shape[0], pad), float("-inf"), device=self.device)], 1)
-            ids = torch.cat([ids, torch.full((ids.shape[0], pad), -1, dtype=torch.int64, device=self.device)], 1)
-            docs = torch.cat([docs, torch.full((docs.shape[0], pad), -1, dtype=torch.int64, device=self.device)], 1)
-        packed = torch.stack([sims.view(torch.int32).to(torch.int64), ids, docs], -1).to(cdev)  # [W*mx, k, 3]
-        # 3. gather partials, merge own queries
-        parts = [torch.empty_like(packed) for _ in range(self.world)]
-        dist.all_gather(parts, packed, group=self.group)
-        mine = torch.stack([p[self.rank * mx: self.rank * mx + nq] for p in parts], 1).to(self.device)  # [nq, W, k, 3]
-        cand = mine.reshape(nq, self.world * k, 3)
-        cs = cand[..., 0].to(torch.int32).view(torch.float32).contiguous()
-        kk = min(k, cs.shape[1], 1024)
-        vals, pos = ops.topk_rows(cs, kk)
-        pos = pos.long()
-        out_ids = torch.gather(cand[..., 1], 1, pos)
-        out_docs = torch.gather(cand[..., 2], 1, pos)
-        return vals, out_ids, out_docs
+        allq = torch.cat([a[:c] for a, c in zip(allq, counts)], 0).to(self.device)  # real rows only
+        # 2. local partial top-k for every query of the node
+        sims, ids, docs = self.local.search(allq[:, : self.dim], k, allq[:, self.dim].to(torch.int32))
+        packed = self._pack(sims, ids, docs, k, wide).to(cdev)  # [sum(counts), k, 3]
+        # 3. route each rank's partials to that rank
+        recv = torch.empty((self.world * nq, k, 3), dtype=packed.dtype, device=cdev)
+        dist.all_to_all_single(recv, packed, output_split_sizes=[nq] * self.world, input_split_sizes=counts,
+                               group=self.group)
+        self.stats["merge_bytes_recv"] = recv.numel() * recv.element_size()
+        # 4. merge [nq, W*k] candidates
+        cand = recv.view(self.world, nq, k, 3).permute(1, 0, 2, 3).reshape(nq, self.world * k, 3)
+        return self._merge(cand, k)
+
+    @torch.inference_mode()
+    def search_replicated(self, queries, k: int, q_groups=None, allowed=None, doc_lt=None, dst: int = 0):
+        """Collective for a batch every rank already holds (gpu_service: the request arrives with the
+        control broadcast).  Each rank scans its shard with the full filter set (``allowed`` ids /
+        ``doc_lt`` bounds are resolved against the local rows), the partials are gathered to ``dst``
+        and merged there.  Returns the result on ``dst`` and None elsewhere."""
+        q = torch.as_tensor(queries).to(self.device, torch.float32)
+        if q.ndim == 1:
+            q = q[None]
+        if not self.distributed or self.world == 1:
+            return self.local.search(q, k, q_groups, allowed=allowed, doc_lt=doc_lt)
+        nq = q.shape[0]
+        cdev = self._comm_device()
+        flag = torch.tensor([int(self._wide())], dtype=torch.int64, device=cdev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        wide = bool(flag.item())
+        if len(self.local):
+            sims, ids, docs = self.local.search(q, k, q_groups, allowed=allowed, doc_lt=doc_lt)
+        else:
+            sims = torch.full((nq, 0), float("-inf"), device=self.device)
+            ids = docs = torch.full((nq, 0), -1, dtype=torch.int64, device=self.device)
+        packed = self._pack(sims, ids, docs, k, wide).to(cdev)
+        me = dist.get_rank(self.group) if self.group is not None else self.rank
+        parts = [torch.empty_like(packed) for _ in range(self.world)] if me == dst else None
+        gdst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
+        dist.gather(packed, parts, dst=gdst, group=self.group)
+        if me != dst:
+            return None
+        self.stats["merge_bytes_recv"] = sum(p.numel() * p.element_size() for p in parts)
+        cand = torch.stack(parts, 1).reshape(nq, self.world * k, 3)
+        return self._merge(cand, k)

@@ -20,13 +20,13 @@ def _free_port():
     return p
 
 
-def _run(fn, *args):
+def _run(fn, *args, world=WORLD):
     port = _free_port()
-    mp.spawn(_entry, args=(fn, port) + args, nprocs=WORLD, join=True)
+    mp.spawn(_entry, args=(fn, port, world) + args, nprocs=world, join=True)
 
 
-def _entry(rank, fn, port, *args):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(WORLD), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+def _entry(rank, fn, port, world, *args):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     torch.set_num_threads(1)
     from django_assistant_bot_amd.parallel import dist as pdist
@@ -99,6 +99,65 @@ def test_sharded_index_matches_single_index(tmp_path):
     for r in range(WORLD):
         res = torch.load(out + f".{r}", weights_only=True)
         assert res["ids_equal"] and res["docs_equal"] and res["sims_err"] < 1e-5
+
+
+def _index_merge_body(info, out_path):
+    """all_to_all merge at world W: uneven per-rank batches (one rank empty), group filters, and
+    the replicated (serving) search with allow-lists / doc bounds gathered to rank 0."""
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    W = info.world_size
+    g = torch.Generator().manual_seed(5)
+    n, dim, k = 2000, 32, 40
+    vecs = torch.randn(n, dim, generator=g)
+    ids = np.arange(7, 7 + n) * 3
+    docs = ids // 11
+    groups = ((ids // 3) % 3).astype(np.int32)
+    idx = ShardedIndex(dim, "cpu")
+    idx.add(ids, vecs, doc_ids=docs, groups=groups)
+    single = VectorIndex(dim, "cpu")
+    single.add(ids, vecs, doc_ids=docs, groups=groups)
+    nq = 0 if info.rank == 1 else 2 + info.rank
+    q = torch.randn(nq, dim, generator=torch.Generator().manual_seed(70 + info.rank))
+    qg = [r % 3 for r in range(nq)]
+    res = {}
+    sims, got_ids, got_docs = idx.search(q, k, q_groups=qg)
+    res["nq"] = nq
+    if nq:
+        es, eids, edocs = single.search(q, k, q_groups=qg)
+        res["own_equal"] = bool(torch.equal(got_ids, eids) and torch.equal(got_docs, edocs))
+        res["own_err"] = float((sims - es).nan_to_num(0.0).abs().max())
+    res["bytes"] = idx.stats["merge_bytes_recv"]
+    # serving path: the same batch on every rank, filters resolved per shard
+    qs = torch.randn(3, dim, generator=torch.Generator().manual_seed(99))
+    allowed = [ids[::2].tolist(), ids[:300].tolist(), ids.tolist()]
+    doc_lt = [10 ** 9, 10 ** 9, int(docs[n // 2])]
+    out = idx.search_replicated(qs, k, q_groups=None, allowed=allowed, doc_lt=doc_lt)
+    if info.rank == 0:
+        es, eids, edocs = single.search(qs, k, allowed=allowed, doc_lt=doc_lt)
+        res["rep_equal"] = bool(torch.equal(out[1], eids) and torch.equal(out[2], edocs))
+        res["rep_err"] = float((out[0] - es).nan_to_num(0.0).abs().max())
+    else:
+        res["rep_none"] = out is None
+    torch.save(res, out_path + f".{info.rank}")
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_sharded_index_all_to_all_merge(tmp_path, world):
+    out = str(tmp_path / "merge.pt")
+    _run(_index_merge_body, out, world=world)
+    k = 40
+    for r in range(world):
+        res = torch.load(out + f".{r}", weights_only=True)
+        if res["nq"]:
+            assert res["own_equal"] and res["own_err"] < 1e-5
+        # each rank receives only the partials of its own queries: W x nq x k x 12 B
+        assert res["bytes"] == world * res["nq"] * k * 12
+        if r == 0:
+            assert res["rep_equal"] and res["rep_err"] < 1e-5
+        else:
+            assert res["rep_none"]
 
 
 def _dp_embed_body(info, out_path):
