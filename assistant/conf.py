@@ -28,11 +28,13 @@ DEFAULTS: dict[str, Any] = {
     "DEBUG": False,
     # engine settings
     "GPU_SERVICE_DEVICES": None,
-    "EMBED_DP": 1,
+    # gpu_service node mode (gpu_service/node_main.py): ranks holding an encoder replica / an index
+    # shard (0 = every GPU of the node) and the generator's tensor-parallel degree
+    "EMBED_DP": 0,
     "GEN_TP": 1,
     "KV_BLOCK_SIZE": 64,
     "MAX_BATCH_TOKENS": 65536,
-    "INDEX_SHARDS": 1,
+    "INDEX_SHARDS": 0,
     "INDEX_DTYPE": "bfloat16",
     "ENGINE_RANDOM_WEIGHTS": True,
 }

@@ -84,6 +84,11 @@ DECODERS = {
     "tiny-llama": DecoderConfig("tiny-llama", vocab_size=1024, hidden=256, layers=2, heads=4, kv_heads=2,
                                 intermediate=512, max_position=2048, bos_id=1000, eos_ids=(1001,), rope_scaling=None,
                                 rope_theta=10000.0),
+    # the Llama-3-70B head layout (64 query heads over 8 KV heads) at toy width: at TP=8 every rank
+    # holds exactly one KV head and 8 query heads, like 70B on 8 GPUs (CPU multi-rank tests)
+    "tiny-llama-70b-layout": DecoderConfig("tiny-llama-70b-layout", vocab_size=1024, hidden=1024, layers=2, heads=64,
+                                           kv_heads=8, intermediate=1024, max_position=2048, bos_id=1000,
+                                           eos_ids=(1001,), rope_scaling=None, rope_theta=10000.0),
 }
 
 _ALIASES = {

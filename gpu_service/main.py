@@ -9,9 +9,17 @@ Endpoints (request/response shapes of the reference where it had them):
   GET  /health                  loaded models, device
   GET  /metrics                 Prometheus text (engine counters, queue depths, HBM use)
 
-Requests from all concurrent callers share the engine's batches (EmbedWorker / LLMWorker), so the
-service is one process per GPU (gunicorn_conf.py maps worker i -> device i).  Model names are
-case-insensitive; unknown model -> 400; engine errors -> 500.
+Requests from all concurrent callers share the engine's batches (EmbedWorker / LLMWorker).  Two
+deployments:
+
+* one process per GPU under gunicorn (``gunicorn_conf.py``): independent replicas for /embeddings/
+  and /dialog/; /index/* needs a single worker (409 otherwise -- replicas would hold different indexes);
+* node mode (``python -m torch.distributed.run --nproc-per-node N -m gpu_service.node_main``): one
+  process group over the node's GPUs -- sharded index, DP embeddings, TP / replicated generators
+  (``django_assistant_bot_amd.parallel.node``).  The handlers below are the same; ``index_backend``
+  and the engine workers are swapped for the node facades.
+
+Model names are case-insensitive; unknown model -> 400; engine errors -> 500.
 """
 from __future__ import annotations
 
@@ -25,6 +33,7 @@ from typing import Dict, List, Optional
 
 from fastapi import FastAPI, HTTPException
 from fastapi.responses import PlainTextResponse
+from starlette.concurrency import run_in_threadpool
 from pydantic import BaseModel
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -75,7 +84,6 @@ class SearchRequest(BaseModel):
 embedders: Dict[str, object] = {}
 providers: Dict[str, object] = {}
 indexes: Dict[str, object] = {}
-_index_lock = threading.Lock()
 
 
 def load_models(embedder_names, provider_names):
@@ -132,55 +140,99 @@ async def get_response(request: DialogRequest):
         raise HTTPException(status_code=500, detail=str(e))
 
 
-def _index(name: str, dim: Optional[int] = None, create: bool = False):
-    with _index_lock:
-        idx = indexes.get(name)
-        if idx is None and create:
-            from django_assistant_bot_amd.engine.serving import engine_device
-            from django_assistant_bot_amd.engine.vector_index import VectorIndex
+class LocalIndexes:
+    """Single-process ``/index/*`` backend: one ``VectorIndex`` per name on this process's GPU.
+    (Node mode replaces it with ``NodeIndexes``: one index sharded over the node's GPUs.)"""
 
-            import torch
+    def __init__(self, store: Dict[str, object]):
+        self.indexes = store
+        self._lock = threading.Lock()
 
-            from django_assistant_bot_amd.engine.serving import setting
+    def dim(self, name: str):
+        idx = self.indexes.get(name)
+        return None if idx is None else idx.dim
 
-            dtype = getattr(torch, str(setting("INDEX_DTYPE", "bfloat16")))
-            idx = indexes[name] = VectorIndex(dim, device=engine_device(), dtype=dtype)
-        return idx
+    def upsert(self, name, ids, vectors, doc_ids=None, groups=None) -> int:
+        with self._lock:
+            idx = self.indexes.get(name)
+            if idx is None:
+                import torch
+
+                from django_assistant_bot_amd.engine.serving import engine_device, setting
+                from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+                dtype = getattr(torch, str(setting("INDEX_DTYPE", "bfloat16")))
+                idx = self.indexes[name] = VectorIndex(len(vectors[0]), device=engine_device(), dtype=dtype)
+            idx.add(ids, vectors, doc_ids=doc_ids, groups=groups)
+            return len(idx)
+
+    def delete(self, name, ids) -> int:
+        with self._lock:
+            idx = self.indexes.get(name)
+            return 0 if idx is None else idx.remove(ids)
+
+    def size(self, name) -> int:
+        idx = self.indexes.get(name)
+        return 0 if idx is None else len(idx)
+
+    def search(self, name, queries, k, groups=None, allowed=None, doc_lt=None):
+        with self._lock:
+            idx = self.indexes.get(name)
+            if idx is None or len(idx) == 0:
+                return None
+            return idx.search(queries, k, q_groups=groups, allowed=allowed, doc_lt=doc_lt)
+
+    def sizes(self) -> dict:
+        return {k: len(v) for k, v in self.indexes.items()}
+
+
+index_backend = LocalIndexes(indexes)
+
+
+def _workers_share_nothing() -> bool:
+    """gunicorn with several workers = independent replicas: an index would differ per worker."""
+    return int(os.environ.get("GPU_SERVICE_WORKERS", "1")) > 1 and isinstance(index_backend, LocalIndexes)
+
+
+def _index_guard():
+    if _workers_share_nothing():
+        raise HTTPException(status_code=409, detail="/index/* needs one index: run gpu_service.node_main "
+                                                    "(one process group over the node's GPUs) or one worker")
 
 
 @app.post("/index/{name}/upsert")
 async def index_upsert(name: str, request: UpsertRequest):
+    _index_guard()
     if len(request.ids) != len(request.vectors):
         raise HTTPException(status_code=400, detail="ids and vectors differ in length")
     if not request.ids:
-        return {"count": len(indexes[name]) if name in indexes else 0}
-    idx = _index(name, dim=len(request.vectors[0]), create=True)
-    if len(request.vectors[0]) != idx.dim:
-        raise HTTPException(status_code=400, detail=f"index {name} has dim {idx.dim}")
-    with _index_lock:
-        idx.add(request.ids, request.vectors, doc_ids=request.doc_ids, groups=request.groups)
-        return {"count": len(idx)}
+        return {"count": index_backend.size(name)}
+    dim = index_backend.dim(name)
+    if dim is not None and len(request.vectors[0]) != dim:
+        raise HTTPException(status_code=400, detail=f"index {name} has dim {dim}")
+    n = await run_in_threadpool(index_backend.upsert, name, request.ids, request.vectors, request.doc_ids,
+                                request.groups)
+    return {"count": n}
 
 
 @app.post("/index/{name}/delete")
 async def index_delete(name: str, request: DeleteRequest):
-    idx = _index(name)
-    if idx is None:
-        return {"removed": 0}
-    with _index_lock:
-        return {"removed": idx.remove(request.ids)}
+    _index_guard()
+    return {"removed": await run_in_threadpool(index_backend.delete, name, request.ids)}
 
 
 @app.post("/index/{name}/search")
 async def index_search(name: str, request: SearchRequest):
-    idx = _index(name)
+    _index_guard()
     nq = len(request.queries)
-    if idx is None or len(idx) == 0 or nq == 0:
+    got = None
+    if nq:
+        got = await run_in_threadpool(index_backend.search, name, request.queries, request.k, request.groups,
+                                      request.allowed, request.doc_lt)
+    if got is None:
         return {"ids": [[] for _ in range(nq)], "distances": [[] for _ in range(nq)],
                 "doc_ids": [[] for _ in range(nq)]}
-    with _index_lock:
-        sims, ids, docs = idx.search(request.queries, request.k, q_groups=request.groups, allowed=request.allowed,
-                                     doc_lt=request.doc_lt)
+    sims, ids, docs = got
     out_ids, out_d, out_docs = [], [], []
     for s, i, d in zip(sims.tolist(), ids.tolist(), docs.tolist()):
         keep = [j for j, x in enumerate(i) if x >= 0]
@@ -201,7 +253,7 @@ async def health():
     h = engine_health()
     body = {"status": "ok" if h["healthy"] else "unhealthy", "device": str(engine_device()),
             "embedders": sorted(embedders), "providers": sorted(providers),
-            "indexes": {k: len(v) for k, v in indexes.items()}, **({} if h["healthy"] else h)}
+            "indexes": index_backend.sizes(), **({} if h["healthy"] else h)}
     return JSONResponse(body, status_code=200 if h["healthy"] else 503)
 
 
@@ -223,5 +275,5 @@ async def metrics():
 
     lines: list = []
     _flatten("dab", engine_metrics(), lines)
-    lines += [f'dab_index_rows{{index="{k}"}} {float(len(v))}' for k, v in indexes.items()]
+    lines += [f'dab_index_rows{{index="{k}"}} {float(v)}' for k, v in index_backend.sizes().items()]
     return "\n".join(lines) + "\n"

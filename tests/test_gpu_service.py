@@ -60,3 +60,31 @@ def test_health_and_metrics(client):
     m = client.get("/metrics").text
     assert 'dab_embedder_requests{model="tiny-bert"}' in m
     assert 'dab_provider_requests{model="tiny-llama"}' in m
+
+
+def test_gunicorn_device_mapping_survives_respawn(monkeypatch):
+    """A respawned worker takes the GPU its predecessor left (reference gunicorn_conf.py ran every
+    worker on one device; worker.age-based mapping drifted after restarts)."""
+    from types import SimpleNamespace
+
+    from gpu_service import gunicorn_conf as gc
+
+    monkeypatch.setattr(gc, "devices", 4)
+    live = {}
+    for pid in range(4):
+        w = SimpleNamespace()
+        gc.pre_fork(SimpleNamespace(WORKERS=live), w)
+        live[pid] = w
+    assert sorted(w.dab_device for w in live.values()) == [0, 1, 2, 3]
+    dead = live.pop(2)
+    w = SimpleNamespace()
+    gc.pre_fork(SimpleNamespace(WORKERS=live), w)
+    assert w.dab_device == dead.dab_device
+    assert gc.pick_device([SimpleNamespace(dab_device=d) for d in (0, 1, 2, 3)], 4) == 0  # oversubscribed
+    assert gc.pick_device([SimpleNamespace(dab_device=d) for d in (0, 2)], 4) == 1
+
+
+def test_index_refused_with_independent_workers(client, monkeypatch):
+    monkeypatch.setenv("GPU_SERVICE_WORKERS", "2")
+    r = client.post("/index/q/search", json={"queries": [[1.0, 0.0, 0.0, 0.0]], "k": 1})
+    assert r.status_code == 409
