@@ -35,11 +35,11 @@ PYBIND11_MODULE(_native, m) {
                                long spin_limit, u s) {
     check(dab::custom_allreduce(bases, rank, VP(data), nbytes, half_bytes, spin_limit, ST(s)), "custom_allreduce");
   });
-  m.def("allreduce_buffer_alloc", [](long bytes) {
+  m.def("allreduce_buffer_alloc", [](long bytes, bool uncached) {
     uintptr_t p = 0;
-    check(dab::allreduce_buffer_alloc(bytes, &p), "allreduce_buffer_alloc");
+    check(dab::allreduce_buffer_alloc(bytes, uncached ? 1 : 0, &p), "allreduce_buffer_alloc");
     return p;
-  });
+  }, py::arg("bytes"), py::arg("uncached") = true);
   m.def("allreduce_buffer_free", [](u ptr) { check(dab::allreduce_buffer_free(ptr), "allreduce_buffer_free"); });
   m.def("ipc_get_handle", [](u ptr) {
     std::string h;

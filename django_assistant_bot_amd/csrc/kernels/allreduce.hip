@@ -136,9 +136,16 @@ int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, 
 
 // ---- IPC buffer management (host) ------------------------------------------------------------
 
-int allreduce_buffer_alloc(long bytes, uintptr_t* out) {
+// uncached = fine-grained, uncached device memory (hipDeviceMallocUncached): every load and store of
+// the signal flags and staging halves goes to HBM, never to a (remote) L2 line that a peer on another
+// GPU could leave stale.  The release/acquire system-scope atomics and __threadfence_system order the
+// accesses; uncached memory is what makes them coherent ACROSS xGMI (coarse-grained hipMalloc memory
+// is coherent only at kernel boundaries for peer accesses).  Peers read it over xGMI either way, so
+// the cost is the local staging write, which is tiny.
+int allreduce_buffer_alloc(long bytes, int uncached, uintptr_t* out) {
   void* ptr = nullptr;
-  hipError_t err = hipMalloc(&ptr, (size_t)bytes);
+  hipError_t err = uncached ? hipExtMallocWithFlags(&ptr, (size_t)bytes, hipDeviceMallocUncached)
+                            : hipMalloc(&ptr, (size_t)bytes);
   if (err != hipSuccess) return err;
   err = hipMemset(ptr, 0, (size_t)bytes);
   if (err != hipSuccess) {

@@ -93,7 +93,7 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
 size_t allreduce_signal_bytes();
 int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, long nbytes, long half_bytes,
                      long spin_limit, hipStream_t s);
-int allreduce_buffer_alloc(long bytes, uintptr_t* out);
+int allreduce_buffer_alloc(long bytes, int uncached, uintptr_t* out);
 int allreduce_buffer_free(uintptr_t ptr);
 int ipc_get_handle(uintptr_t ptr, std::string* handle);
 int ipc_open_handle(const std::string& handle, uintptr_t* out);

@@ -8,8 +8,9 @@ takes 2(W-1) serial steps over 2 of the links.  Larger messages (prefill) fall b
     ar.all_reduce(x)                         # in place; x bf16, contiguous, <= max_bytes
     ar.close()
 
-The buffers come from hipMalloc, outside the torch caching allocator, so IPC handles cover the
-whole allocation.  Each rank has one buffer: a signal area plus two staging halves of
+The buffers come from ``hipExtMallocWithFlags(..., hipDeviceMallocUncached)`` (fine-grained,
+uncached: flag and staging accesses are coherent across xGMI, not only at kernel boundaries),
+outside the torch caching allocator, so IPC handles cover the whole allocation.  Each rank has one buffer: a signal area plus two staging halves of
 ``max_bytes``.  The kernel's epochs live on the device, so calls can be captured in HIP graphs.
 A peer that never arrives makes the kernel set an error flag instead of hanging;
 ``check_error`` raises it on the host.
@@ -30,7 +31,7 @@ class CustomAllReduceError(RuntimeError):
 
 class CustomAllReduce:
     def __init__(self, group=None, device=None, max_bytes: int = 8 << 20, spin_limit: int = 1 << 24,
-                 exchange_group=None):
+                 exchange_group=None, uncached: bool = True):
         """``group``: the ranks that reduce together.  ``exchange_group``: where the IPC handles
         travel; it defaults to ``group`` and may be a gloo group."""
         self.group = group
@@ -45,7 +46,7 @@ class CustomAllReduce:
         self._n = n
         sig = n.allreduce_signal_bytes()
         with torch.cuda.device(self.device):
-            self.base = n.allreduce_buffer_alloc(sig + 2 * self.max_bytes)
+            self.base = n.allreduce_buffer_alloc(sig + 2 * self.max_bytes, uncached)
             handle = n.ipc_get_handle(self.base)
             handles = [None] * self.world
             if self.world > 1:
@@ -91,7 +92,6 @@ class CustomAllReduce:
             if r != self.rank:
                 self._n.ipc_close_handle(b)
         self._n.allreduce_buffer_free(self.base)
-
 
 
 def maybe_create(group, device, world: int):

@@ -91,7 +91,9 @@ class Node:
         self.rank, self.world = info.rank, info.world_size
         self.device = info.device
         assert plan.world == self.world, "plan built for another world size"
-        self.ctrl = ctrl if ctrl is not None else control_group(list(range(self.world)))
+        if ctrl is None and self.world > 1:
+            ctrl = control_group(list(range(self.world)))
+        self.ctrl = ctrl
         self.tp_group, self.tp_rank, self.replica = pdist.tp_groups(plan.gen_tp)
         self.index_group = _subgroup(plan.index_shards, self.world)
         self.embed_group = _subgroup(plan.embed_dp, self.world)
@@ -155,6 +157,8 @@ class Node:
 
     # ------------------------------------------------------------------ ops (run on every rank)
     def _cdev(self, group):
+        if self.world == 1:
+            return self.device
         return self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
 
     def _index(self, name: str, dim: int | None = None):

@@ -32,7 +32,7 @@ def _expected(world, n, salt):
     return acc.to(torch.bfloat16)
 
 
-def _body(rank, world, port, out_dir):
+def _body(rank, world, port, out_dir, uncached=True):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
@@ -41,7 +41,7 @@ def _body(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    ar = CustomAllReduce(None, dev, max_bytes=4 << 20, spin_limit=1 << 22)
+    ar = CustomAllReduce(None, dev, max_bytes=4 << 20, spin_limit=1 << 22, uncached=uncached)
     errors = []
     try:
         sizes = [8, 64, 4096 + 8, 1 << 16, (4 << 20) // 2, 3000 * 8, 8]  # elements (x2 bytes)
@@ -87,11 +87,12 @@ def _body(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_one_shot_allreduce_multi_process(world, tmp_path):
+@pytest.mark.parametrize("world,uncached", [(2, True), (4, True), (8, True), (2, False)])
+def test_one_shot_allreduce_multi_process(world, uncached, tmp_path):
+    """world 8 = the TP-8 group of a 70B node (here 8 processes on one device)."""
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_body, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_body, args=(r, world, port, str(tmp_path), uncached)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -458,3 +458,35 @@ def test_cu_masked_stream_runs_kernels():
     finally:
         torch.cuda.synchronize()
         nat.destroy_stream(h)
+
+
+@pytest.mark.parametrize("ctx,qlen", [([4096, 6000], [512, 1024]), ([8192], [8192]), ([8192, 5000], [1, 700])])
+def test_flash_paged_prefill_long_context_llama_heads(ctx, qlen):
+    """Llama-3-8B head layout (Hq 32, Hkv 8, D 128) at 4K-8K context: chunked prefill (q = the last
+    qlen positions of ctx) and a full 8K prompt, against the fp32 reference."""
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    nb = sum(math.ceil(c / bs) for c in ctx) + 4
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, nb)
+    q = bf(sum(qlen), Hq, D)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(qlen), causal=True)
+    exp = ref.flash_attention_paged(q, kc, vc, bt, cu, ctxt, True, 1 / math.sqrt(D))
+    close(out, exp)
+
+
+@pytest.mark.parametrize("part", [512, 2048])
+@pytest.mark.parametrize("split", [False, True])
+def test_paged_decode_8k_context(part, split):
+    """Decode at the engine's full 8192-token context (max_position of Llama-3), with the split-K
+    partition sizes the engine uses (512 for small batches, 2048 at RAG batch sizes)."""
+    ctx = [8192, 8191, 5000, 4097, 2048, 1]
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    nb = sum(math.ceil(c / bs) for c in ctx) + 4
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, nb)
+    q = bf(len(ctx), Hq, D)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    ws = ops.DecodeWorkspace(len(ctx), Hq, D, math.ceil(8192 / part), DEV) if split else None
+    out = ops.paged_decode(q, kc, vc, bt, ctxt, part, ws)
+    exp = ref.paged_decode(q, kc, vc, bt, ctxt, 1 / math.sqrt(D))
+    close(out, exp)

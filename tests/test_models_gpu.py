@@ -219,3 +219,49 @@ def test_engine_two_stream_prefill_on_gpu():
     assert hasattr(eng.model, "_side_streams")
     assert all(len(o.token_ids) == 12 for o in outs)
     assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
+
+
+def test_bert_encoder_bge_base_matches_hf_bertmodel(tmp_path):
+    """BertEncoder at the bge-base shape on the native kernels (bf16) vs the HF ``BertModel`` the
+    reference embedder runs (/root/reference/assistant/ai/embedders/transformers.py:18-25: fp32,
+    one text at a time, mean over all tokens) and vs this repo's fp32 CPU reference path, on
+    variable-length sequences up to 512 tokens: pooled cosine >= 0.999."""
+    transformers = pytest.importorskip("transformers")
+    from safetensors.torch import save_file
+
+    from django_assistant_bot_amd.models.bert import BertEncoder, pack_sequences
+    from django_assistant_bot_amd.models.configs import encoder_config
+    from django_assistant_bot_amd.models.weights import load_encoder_checkpoint
+
+    cfg = encoder_config("bge-base-en")
+    hc = transformers.BertConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, num_hidden_layers=cfg.layers,
+                                 num_attention_heads=cfg.heads, intermediate_size=cfg.intermediate,
+                                 max_position_embeddings=cfg.max_position, type_vocab_size=cfg.type_vocab,
+                                 layer_norm_eps=cfg.eps, hidden_act="gelu")
+    torch.manual_seed(0)
+    hf = transformers.BertModel(hc, add_pooling_layer=False).eval()
+    # give LayerNorms / biases non-trivial values so every fused epilogue is exercised
+    with torch.no_grad():
+        for name, p in hf.named_parameters():
+            if name.endswith("bias"):
+                p.normal_(0, 0.02)
+            elif "LayerNorm.weight" in name:
+                p.uniform_(0.8, 1.2)
+    save_file({k: v.contiguous() for k, v in hf.state_dict().items()}, str(tmp_path / "model.safetensors"))
+    gen = torch.Generator().manual_seed(1)
+    lens = [512, 1, 37, 200, 511, 64, 300, 2, 129]
+    seqs = [torch.randint(1000, cfg.vocab_size, (n,), generator=gen).tolist() for n in lens]
+    enc = BertEncoder(cfg, load_encoder_checkpoint(str(tmp_path), cfg, dtype=torch.bfloat16), DEV)
+    ids, pos, cu, mx = pack_sequences(seqs, DEV)
+    got = enc.encode(ids, pos, cu, mx, normalize=False).float().cpu()
+    hf = hf.to(DEV)
+    with torch.no_grad():
+        want = torch.stack([hf(input_ids=torch.tensor([s], device=DEV)).last_hidden_state[0].mean(0)
+                            for s in seqs]).float().cpu()
+    cos = torch.nn.functional.cosine_similarity(got, want, dim=-1)
+    assert cos.min().item() >= 0.999, cos
+    ref_enc = BertEncoder(cfg, load_encoder_checkpoint(str(tmp_path), cfg, dtype=torch.float32), "cpu")
+    ids, pos, cu, mx = pack_sequences(seqs, "cpu")
+    ref_out = ref_enc.encode(ids, pos, cu, mx, normalize=False).float()
+    assert torch.nn.functional.cosine_similarity(ref_out, want, dim=-1).min().item() >= 0.9999
+    assert torch.nn.functional.cosine_similarity(got, ref_out, dim=-1).min().item() >= 0.999

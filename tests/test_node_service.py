@@ -152,3 +152,52 @@ def test_node_service_matches_single_process(tmp_path, world, plan_kw):
     replicas = world // plan_kw.get("gen_tp", 1)
     assert len(res["placed"]) == replicas and (replicas == 1 or min(res["placed"]) > 0)
     assert res["health_indexes"] == {"q": 390} and res["metrics_ok"]
+
+
+@pytest.mark.gpu
+def test_node_service_on_gpu(monkeypatch):
+    """Node mode on the box's GPU (world 1): the same facades serve index, embeddings and dialog from
+    the native kernels; results equal the plain engines on the same device."""
+    from fastapi import FastAPI
+    from fastapi.testclient import TestClient
+
+    from django_assistant_bot_amd.engine import serving
+    from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+    from django_assistant_bot_amd.parallel.node import NodePlan
+    from gpu_service import main as svc
+    from gpu_service import node_main
+
+    for k, v in dict(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0").items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setattr(serving, "_llm", {})
+    monkeypatch.setattr(serving, "_emb", {})
+    monkeypatch.setattr(svc, "embedders", {})
+    monkeypatch.setattr(svc, "providers", {})
+    monkeypatch.setattr(svc, "index_backend", svc.index_backend)
+    node = node_main.setup(embedders=["tiny-bert"], providers=["tiny-llama"], plan=NodePlan(1), device_type="cuda")
+    try:
+        app = FastAPI()
+        for r in svc.app.routes:
+            app.router.routes.append(r)
+        c = TestClient(app)
+        g = torch.Generator().manual_seed(2)
+        ids = np.arange(3000)
+        vecs = torch.randn(3000, 64, generator=g)
+        assert c.post("/index/n/upsert", json={"ids": ids.tolist(), "vectors": vecs.tolist(),
+                                               "doc_ids": (ids // 10).tolist()}).json()["count"] == 3000
+        q = torch.randn(4, 64, generator=g)
+        got = c.post("/index/n/search", json={"queries": q.tolist(), "k": 20}).json()
+        single = VectorIndex(64, "cuda")
+        single.add(ids, vecs, doc_ids=ids // 10)
+        assert got["ids"] == single.search(q, 20)[1].tolist()
+        texts = [f"sentence {i} " * (i % 9 + 1) for i in range(40)]
+        emb = np.asarray(c.post("/embeddings/", json={"model": "tiny-bert", "texts": texts}).json()["embeddings"])
+        ref = EmbeddingEngine("tiny-bert", "cuda", seed=0).embed(texts).float().cpu().numpy()
+        assert np.abs(emb - ref).max() < 1e-3
+        r = c.post("/dialog/", json={"model": "tiny-llama", "messages": [{"role": "user", "content": "hi"}],
+                                     "max_tokens": 7}).json()["response"]
+        assert 0 < r["usage"]["completion_tokens"] <= 7
+        assert node.llms["tiny-llama"].stats["decode_steps"] > 0
+    finally:
+        node_main.teardown(node)
