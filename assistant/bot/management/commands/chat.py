@@ -1,5 +1,6 @@
 """Interactive console chat with a bot, stored in the database like any platform
-(reference bot/management/commands/chat.py).  ``--memory`` runs without touching the database."""
+(reference bot/management/commands/chat.py).  ``--memory`` runs without touching the database.  Like the
+reference, the chat restarts when a source file changes (``--noreload`` disables it)."""
 import asyncio
 import json
 import logging
@@ -43,8 +44,16 @@ class Command(BaseCommand):
         parser.add_argument("bot_codename")
         parser.add_argument("--memory", action="store_true", help="in-memory dialog (no database writes)")
         parser.add_argument("--history", default=HISTORY_FILE_NAME)
+        parser.add_argument("--noreload", action="store_true", help="do not restart on code changes")
 
     def handle(self, *args, **opts):
+        if opts["noreload"]:
+            return self._chat(opts)
+        from assistant.utils.autoreload import run_with_reloader
+
+        run_with_reloader(self._chat, opts)
+
+    def _chat(self, opts):
         logging.getLogger().setLevel(logging.WARNING)
         codename = opts["bot_codename"]
         platform = ConsolePlatform(opts["history"])

@@ -1,7 +1,8 @@
 """Run a bot in Telegram long-polling mode (reference bot/management/commands/telegram_poll.py).
 
 Uses ``getUpdates`` of the raw Bot API client (no python-telegram-bot).  Each update is stored like a
-webhook update and answered through ``answer_task`` -- inline with ``--sync``, else via Celery."""
+webhook update and answered through ``answer_task`` -- inline with ``--sync``, else via Celery.
+``--dev`` restarts the poller when a source file changes (``assistant.utils.autoreload``)."""
 import asyncio
 import logging
 from datetime import timedelta
@@ -25,8 +26,18 @@ class Command(BaseCommand):
         parser.add_argument("bot_codename")
         parser.add_argument("--sync", action="store_true", help="answer inline instead of through Celery")
         parser.add_argument("--timeout", type=int, default=30, help="long-poll timeout (s)")
+        parser.add_argument("--dev", action="store_true", help="development mode: auto-reload on code changes")
 
     def handle(self, *args, **opts):
+        if opts["dev"]:
+            from assistant.utils.autoreload import run_with_reloader
+
+            logger.info("development mode: auto-reload enabled")
+            run_with_reloader(self._run, opts)
+        else:
+            self._run(opts)
+
+    def _run(self, opts):
         try:
             asyncio.run(self._poll(opts["bot_codename"], opts["sync"], opts["timeout"]))
         except KeyboardInterrupt:

@@ -4,7 +4,7 @@ from django.db import migrations, models
 
 class Migration(migrations.Migration):
     initial = True
-    dependencies = [("assistant_bot", "0001_initial")]
+    dependencies = [("assistant_bot", "0006_botuser_phone_number_instance_is_unavailable")]
 
     operations = [
         migrations.CreateModel(

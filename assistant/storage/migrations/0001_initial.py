@@ -7,7 +7,9 @@ import assistant.storage.fields
 
 class Migration(migrations.Migration):
     """Knowledge-base schema.  Vectors use the portable VectorField (pgvector type on PostgreSQL when
-    pgvector is installed, float32 bytes elsewhere); no HNSW index -- search runs in the HBM index."""
+    pgvector is installed, float32 bytes elsewhere); no HNSW index -- search runs in the HBM index.
+    Document.content_embedding and the WikiDocument verbose names follow in 0002 (the reference's
+    migration names, so a database it created continues from its own history)."""
 
     initial = True
 
@@ -20,12 +22,12 @@ class Migration(migrations.Migration):
             name="WikiDocument",
             fields=[
                 ("id", models.BigAutoField(auto_created=True, primary_key=True, serialize=False, verbose_name="ID")),
-                ("url", models.URLField(blank=True, null=True, verbose_name="URL")),
-                ("title", models.TextField(blank=True, verbose_name="Заголовок")),
-                ("description", models.TextField(blank=True, default="", verbose_name="Описание")),
-                ("content", models.TextField(blank=True, default="", verbose_name="Содержание")),
-                ("created_at", models.DateTimeField(auto_now_add=True, verbose_name="Дата создания")),
-                ("updated_at", models.DateTimeField(auto_now=True, verbose_name="Дата обновления")),
+                ("url", models.URLField(blank=True, null=True)),
+                ("title", models.TextField(blank=True)),
+                ("description", models.TextField(blank=True, default="")),
+                ("content", models.TextField(blank=True, default="")),
+                ("created_at", models.DateTimeField(auto_now_add=True)),
+                ("updated_at", models.DateTimeField(auto_now=True)),
                 ("lft", models.PositiveIntegerField(editable=False)),
                 ("rght", models.PositiveIntegerField(editable=False)),
                 ("tree_id", models.PositiveIntegerField(db_index=True, editable=False)),
@@ -55,7 +57,6 @@ class Migration(migrations.Migration):
                 ("name", models.TextField()),
                 ("description", models.TextField(blank=True, default="")),
                 ("content", models.TextField(blank=True, default="")),
-                ("content_embedding", assistant.storage.fields.VectorField(blank=True, dimensions=768, null=True)),
                 ("processing", models.ForeignKey(blank=True, null=True, on_delete=django.db.models.deletion.CASCADE,
                                                  related_name="documents",
                                                  to="assistant_storage.wikidocumentprocessing")),

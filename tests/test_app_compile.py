@@ -16,7 +16,7 @@ def test_compiles(path):
 
 
 DJANGO_FREE = [
-    "assistant.conf", "assistant.utils.sync", "assistant.utils.tasks", "assistant.utils.language",
+    "assistant.conf", "assistant.utils.sync", "assistant.utils.autoreload", "assistant.utils.tasks", "assistant.utils.language",
     "assistant.utils.fuzzy", "assistant.utils.repeat_until", "assistant.ai.services.ai_service",
     "assistant.bot.domain", "assistant.bot.assistant_bot", "assistant.bot.store", "assistant.bot.session",
     "assistant.bot.selfplay", "assistant.bot.tasks", "assistant.bot.services.answer_service",
