@@ -36,6 +36,11 @@ def _check(d, n):
     assert d["n_gpus"] == n and d["steps"] == 1 and d["warmup"] == 1
     assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "bf16"
     assert d["value"] > 0 and d["ms_per_step"] > 0
+    # the fast JSON steps (classify + known question) reported next to the unchanged headline
+    assert d["fast_steps_s"] > 0 and 0 < d["full_pipeline_qps"] < d["value"]
+    assert d["full_pipeline_p50_latency_ms"] > d["p50_latency_ms"]
+    f = d["config"]["fast_steps"]
+    assert f["batch"] == 4 and f["classify_prompt_tokens"] > 100 and f["known_question_prompt_tokens"] > 50
     c = d["config"]
     assert c["parallelism"] == f"dp{n}" and c["global_batch"] == 4 * n
     # whole-job aggregate: n replicas x batch 4 answered in the timed step
