@@ -238,9 +238,15 @@ def get_embed_worker(model: str, **engine_kwargs) -> EmbedWorker:
         return w
 
 
+_node = None  # the gpu_service node (parallel.node.Node) when running in node mode
+
+
 def health() -> dict:
-    """Worker health for gpu_service /health (unhealthy after a sticky device fault)."""
+    """Worker health for gpu_service /health (unhealthy after a sticky device fault, or when the
+    node's process group broke)."""
     bad = {k: w.last_error for k, w in _llm.items() if not w.healthy}
+    if _node is not None and not _node.healthy:
+        bad["node"] = _node.last_error
     return {"healthy": not bad, "unhealthy_workers": bad}
 
 

@@ -52,6 +52,14 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
+        attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT")
+        if attempt is not None and os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True":
+            # restarted by torch.distributed.run after a rank fault: the agent's store outlives the
+            # failed group, so every key of this attempt (group addresses, RCCL unique ids) gets its
+            # own prefix instead of meeting the dead group's entries
+            base = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]), world, False,
+                                 timeout=datetime.timedelta(seconds=timeout_s))
+            kw["store"] = dist.PrefixStore(f"dab/attempt_{attempt}", base)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return DistInfo(rank, world, local, device, backend if world > 1 else "none")

@@ -43,6 +43,11 @@ import torch.distributed as dist
 logger = logging.getLogger(__name__)
 
 
+class NodeFault(RuntimeError):
+    """A node command failed: a rank died or a collective broke.  The group is unusable until the
+    launcher restarts it (new process group, new RCCL communicators)."""
+
+
 @dataclass
 class NodePlan:
     world: int
@@ -105,6 +110,8 @@ class Node:
         self._lock = threading.RLock()
         self._stopped = False
         self.commands = 0
+        self.healthy = True
+        self.last_error = ""
         from ..engine.embedding_engine import EmbeddingEngine
         from ..engine.llm_engine import LLMEngine
 
@@ -127,10 +134,20 @@ class Node:
         with self._lock:
             if self._stopped:
                 raise RuntimeError("node service is shut down")
-            if self.world > 1:
-                dist.broadcast_object_list([(op, payload)], src=0, group=self.ctrl)
-            self.commands += 1
-            return self.execute(op, payload)
+            if not self.healthy:
+                raise NodeFault(f"node group is broken ({self.last_error}); waiting for the restart")
+            try:
+                if self.world > 1:
+                    dist.broadcast_object_list([(op, payload)], src=0, group=self.ctrl)
+                self.commands += 1
+                return self.execute(op, payload)
+            except Exception as exc:
+                # A dead peer surfaces here: the control broadcast or a collective inside the op fails.
+                # Results of a half-run command cannot be trusted on any rank, so the group is over.
+                self.healthy = False
+                self.last_error = f"{op}: {type(exc).__name__}: {exc}"
+                logger.error("node command failed, group marked broken: %s", self.last_error)
+                raise NodeFault(self.last_error) from exc
 
     def follow(self) -> int:
         """Ranks 1..W-1: run commands until ``stop``.  Returns the number of commands run.  A command
@@ -142,7 +159,11 @@ class Node:
             op, payload = box[0]
             if op == "stop":
                 return n
-            self.execute(op, payload)
+            try:
+                self.execute(op, payload)
+            except Exception:
+                logger.exception("rank %d: node command %s failed; leaving the group", self.rank, op)
+                raise
             n += 1
 
     def shutdown(self) -> None:
@@ -154,6 +175,11 @@ class Node:
 
     def execute(self, op: str, payload):
         return getattr(self, "_op_" + op)(payload)
+
+    def _op_fault(self, rank):
+        """Fault injection (tests): the given rank fails inside a command."""
+        if self.rank == rank:
+            raise RuntimeError(f"injected fault on rank {rank}")
 
     # ------------------------------------------------------------------ ops (run on every rank)
     def _cdev(self, group):
@@ -336,7 +362,11 @@ class NodeLLM:
 
     def fail_all(self) -> list[int]:
         ids = list(self._where)
-        self.node.command("llm_fail", self.name)
+        if self.node.healthy:  # a broken group is restarted as a whole; nothing to clean up remotely
+            try:
+                self.node.command("llm_fail", self.name)
+            except NodeFault:
+                pass
         self._pending.clear()
         self._where.clear()
         self._deadline.clear()

@@ -56,6 +56,7 @@ def setup(embedders=None, providers=None, plan=None, max_batch=None, checkpoint=
     providers = registry.provider_models if providers is None else providers
     node = Node(info, plan, embedders, providers, seed=seed,
                 llm_kwargs=_llm_kwargs(info.device.type, max_batch, checkpoint), llm_weights=llm_weights)
+    serving._node = node
     if info.rank == 0:
         for name in node.llms:
             serving._llm[name] = serving.LLMWorker(NodeLLM(node, name))
@@ -65,6 +66,25 @@ def setup(embedders=None, providers=None, plan=None, max_batch=None, checkpoint=
         svc.load_models(embedders, providers)  # providers / embedders pick up the node workers
     logger.info("rank %d: node plan %s (tp group rank %d, replica %d)", info.rank, plan, node.tp_rank, node.replica)
     return node
+
+
+def exit_on_fault(node, grace_s: float = 2.0, poll_s: float = 0.5, exit=None):
+    """Rank 0 watchdog: once the group is broken (a rank died, a collective failed), keep answering
+    /health with 503 for ``grace_s`` and then leave with status 1, so ``torch.distributed.run
+    --max-restarts`` restarts every rank with a fresh process group (new RCCL communicators)."""
+    import threading
+    import time
+
+    def watch():
+        while node.healthy:
+            time.sleep(poll_s)
+        logger.error("node group broken (%s); exiting for a restart", node.last_error)
+        time.sleep(grace_s)
+        (exit or os._exit)(1)
+
+    t = threading.Thread(target=watch, name="node-watchdog", daemon=True)
+    t.start()
+    return t
 
 
 def teardown(node) -> None:
@@ -100,6 +120,7 @@ def main(argv=None) -> int:
 
     from gpu_service.main import app
 
+    exit_on_fault(node)
     try:
         uvicorn.run(app, host=a.host, port=a.port, log_level="info")
     finally:

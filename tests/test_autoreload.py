@@ -31,7 +31,7 @@ def test_reloader_restarts_child_on_source_change(tmp_path):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     p = subprocess.Popen([sys.executable, str(script)], cwd=root,
-                         env={**os.environ, "PYTHONPATH": root})
+                         env={**os.environ, "PYTHONPATH": root, "PYTHONDONTWRITEBYTECODE": "1"})
     try:
         t0 = time.time()
         while not (log.exists() and log.read_text().count("start") >= 1):
