@@ -1,0 +1,91 @@
+"""Paged decode attention at the headline decode shape: 128 sequences with mixed context lengths
+(the bench's ~1.0-1.5k tokens), Llama-3-8B heads (32 q / 8 kv, D 128), block size 64, shuffled block
+tables.  Compares dispatch orders (batch order vs longest-first) and partition sizes; uniform
+contexts of the same mean give the no-imbalance reference.  Graph-timed: N launches captured in one
+HIP graph, replayed; K/V rotate over several copies so the 650 MB working set stays cold as in the
+model (where 16 GB of weights stream between two layers' attention).
+
+    python benchmarks/decode_attn_bench.py [--batch 128] [--copies 3]
+"""
+import argparse
+import json
+import math
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from django_assistant_bot_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--copies", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=12)
+    a = ap.parse_args()
+    Hq, Hkv, D, bs, B = 32, 8, 128, 64, a.batch
+    g = torch.Generator().manual_seed(0)
+    for dist_name in ("mixed", "uniform"):
+        if dist_name == "mixed":
+            ctx_h = torch.randint(950, 1450, (B,), generator=g)
+        else:
+            ctx_h = torch.full((B,), 1200)
+        nbs = [math.ceil(int(c) / bs) for c in ctx_h]
+        nb = sum(nbs)
+        caches = []
+        for _ in range(a.copies):
+            kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+            caches.append((kc, torch.randn_like(kc)))
+        perm = torch.randperm(nb, generator=g)
+        bt = torch.zeros((B, max(nbs)), dtype=torch.int32)
+        o = 0
+        for i, n in enumerate(nbs):
+            bt[i, :n] = perm[o:o + n].to(torch.int32)
+            o += n
+        bt = bt.cuda()
+        ctx = ctx_h.to(torch.int32).cuda()
+        q = torch.randn(B, Hq, D, device="cuda").to(torch.bfloat16)
+        longest = torch.argsort(ctx_h, descending=True).to(torch.int32).cuda()
+        byts = 2.0 * float(ctx_h.sum()) * Hkv * D * 2
+        res = {"op": "paged-decode", "ctx": dist_name, "B": B, "mean_ctx": int(ctx_h.float().mean()),
+               "GB": round(byts / 1e9, 3)}
+        ref = None
+        for part in (2048, 1024, 512):
+            ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / part), "cuda")
+            for oname, order in (("batch", None), ("longest", longest)):
+                outs = []
+
+                def run():
+                    for kc, vc in caches:
+                        outs.append(ops.paged_decode(q, kc, vc, bt, ctx, part, ws, order=order))
+                run()
+                torch.cuda.synchronize()
+                if ref is None:
+                    ref = outs[0].float()
+                err = (outs[0].float() - ref).abs().max().item()
+                outs.clear()
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    for _ in range(a.iters):
+                        run()
+                torch.cuda.synchronize()
+                graph.replay()
+                torch.cuda.synchronize()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                graph.replay()
+                e.record()
+                torch.cuda.synchronize()
+                t = s.elapsed_time(e) / 1e3 / (a.iters * a.copies)
+                res[f"p{part}_{oname}_us"] = round(t * 1e6, 1)
+                res[f"p{part}_{oname}_tbps"] = round(byts / t / 1e12, 2)
+                res[f"p{part}_{oname}_err"] = round(err, 4)
+                del graph, outs
+        print(json.dumps(res), flush=True)
+        del caches
+
+
+if __name__ == "__main__":
+    main()

@@ -119,12 +119,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("destroy_stream", [](u s) { check(hipStreamDestroy(ST(s)), "hipStreamDestroy"); });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
                                      u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
-                                     float scale, u s) {
+                                     float scale, u s, u order) {
     check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
                                       (float*)po, (float*)pm, (float*)pl, (int*)cnt, batch, Hq, Hkv, D, part_size,
-                                      max_parts, scale, ST(s)),
+                                      max_parts, scale, ST(s), (const int*)order),
           "paged_decode_attention");
-  });
+  }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("max_blocks"), py::arg("bs"), py::arg("ctx"),
+     py::arg("out"), py::arg("po"), py::arg("pm"), py::arg("pl"), py::arg("cnt"), py::arg("batch"), py::arg("Hq"),
+     py::arg("Hkv"), py::arg("D"), py::arg("part_size"), py::arg("max_parts"), py::arg("scale"), py::arg("s"),
+     py::arg("order") = 0);
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,

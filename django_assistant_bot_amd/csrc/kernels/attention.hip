@@ -290,6 +290,7 @@ struct DecodeParams {
   float* part_m;
   float* part_l;
   int* counters;  // [B * Hkv] partition arrivals (zero between launches; the last arriver resets)
+  const int* order;  // optional [B] sequence visit order (longest first: see paged_decode_attention)
   int Hq, Hkv, part_size, max_parts;
   float scale_log2;
 };
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
   for (int item = blockIdx.x; item < total_items; item += gridDim.x) {
     const int part = item / BH;
     const int bh = item - part * BH;
-    const int hk = bh % p.Hkv, b = bh / p.Hkv;
+    const int hk = bh % p.Hkv, b = p.order ? p.order[bh / p.Hkv] : bh / p.Hkv;
     const int ctx = p.ctx_lens[b];
     const int k_begin = part * p.part_size;
     if (k_begin >= ctx) continue;
@@ -499,9 +500,10 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (tid == 0) {
-        const int prev = __hip_atomic_fetch_add(p.counters + bh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int ci = b * p.Hkv + hk;
+        const int prev = __hip_atomic_fetch_add(p.counters + ci, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int last = prev == np - 1;
-        if (last) __hip_atomic_store(p.counters + bh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (last) __hip_atomic_store(p.counters + ci, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         *last_flag = last;
       }
       __syncthreads();
@@ -605,10 +607,16 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   return hipGetLastError();
 }
 
+// The workgroups of a launch are dispatched in blockIdx order as CU slots free up; at RAG batch sizes
+// every CU runs about two (sequence, kv head) items one after the other, so with sequences of mixed
+// length the launch ends when the unluckiest slot has run two long ones.  ``order`` (optional, a
+// permutation of the batch, longest context first, built on the host with the step's inputs) makes
+// the dispatch longest-processing-time-first: the long items start in the first round, the short
+// ones fill in behind them.
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
-                           int part_size, int max_parts, float scale, hipStream_t s) {
+                           int part_size, int max_parts, float scale, hipStream_t s, const int* order) {
   if (batch <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1 || block_size % 32) return hipErrorInvalidValue;
   if (max_parts > 1 && !counters) return hipErrorInvalidValue;
@@ -625,6 +633,7 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_m = part_m;
   prm.part_l = part_l;
   prm.counters = counters;
+  prm.order = order;
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.part_size = part_size;

@@ -42,7 +42,8 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
-                           int part_size, int max_parts, float scale, hipStream_t s);
+                           int part_size, int max_parts, float scale, hipStream_t s,
+                           const int* order = nullptr);
 
 // gemm.hip
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,

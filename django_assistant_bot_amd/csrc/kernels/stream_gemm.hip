@@ -21,6 +21,7 @@
 // [gate | up] weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue
 // (rmsnorm / rope+KV write) or by skinny_reduce.  Block -> (tile, slice) keeps a tile's slices on
 // one XCD (bijective remap, slice-minor).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -40,7 +41,8 @@ struct StreamParams {
   const bf16* residual;
   long ldr;
   int M, N, K, S, kc;
-  int epi;  // 0 none, 2 swiglu
+  int epi;       // 0 none, 2 swiglu
+  int slab_wt;   // split-K slabs stored write-through (sc1)
 };
 
 constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2;
@@ -243,6 +245,20 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
   constexpr int NT = 64 * (NWC + NL);
   if (p.S > 1) {
     float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
+    if (p.slab_wt) {
+      // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
+      // instead of sitting dirty until the kernel-end write-back, which the next kernel's start
+      // would wait for (MI355X_MICROARCH.md price list: +2.8-3.8 us behind 12.6-16.8 MB of fp32
+      // partials); the consumer reads them once from the Infinity Cache either way
+      const auto srd = __builtin_amdgcn_make_buffer_rsrc(slab + n0, 0, (p.M - 1) * p.N * 4 + BN * 4, 0x00020000);
+      for (int e = tid; e < MP * (BN / 4); e += NT) {
+        const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
+        if (m < p.M)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile4(m, c4)), srd, (m * p.N + c4) * 4, 0,
+                                                 16);
+      }
+      return;
+    }
     for (int e = tid; e < MP * (BN / 4); e += NT) {
       const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
       if (m < p.M) *reinterpret_cast<f32x4*>(slab + (size_t)m * p.N + n0 + c4) = tile4(m, c4);
@@ -371,6 +387,11 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   p.S = S;
   p.kc = K / S;
   p.epi = epilogue;
+  static const int slab_wt = [] {
+    const char* v = getenv("DAB_SLAB_WT");
+    return v == nullptr ? 1 : atoi(v);
+  }();
+  p.slab_wt = slab_wt;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();
 }

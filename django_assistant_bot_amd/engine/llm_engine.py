@@ -178,6 +178,8 @@ class LLMEngine:
         self._d_topp = torch.ones(mb, dtype=torch.float32, device=dev)
         self._d_cnt = torch.zeros(mb, dtype=torch.int64, device=dev)
         self._d_tokens = torch.zeros(mb, dtype=torch.int32, device=dev)
+        self._d_order = torch.arange(mb, dtype=torch.int32, device=dev)  # decode attention dispatch order
+        self.lpt_order = os.environ.get("DAB_DECODE_ORDER", "1") == "1"
         pin = self.is_gpu
         mk = lambda *a, **k: torch.zeros(*a, **k, pin_memory=pin)  # noqa: E731
         self._h_ids = mk(mb, dtype=torch.int32)
@@ -190,6 +192,7 @@ class LLMEngine:
         self._h_topp = mk(mb, dtype=torch.float32)
         self._h_cnt = mk(mb, dtype=torch.int64)
         self._h_tokens = mk(mb, dtype=torch.int32)
+        self._h_order = mk(mb, dtype=torch.int32)
         # pipelined decode (``_step_pipelined``): step t+1 is launched before step t's tokens are read,
         # its input ids copied on the device from step t's sampled tokens, so the host's per-step
         # bookkeeping overlaps the GPU instead of idling it.  Two alternating host buffer sets: the
@@ -199,7 +202,7 @@ class LLMEngine:
         self.pipeline_decode = bool(pipeline_decode) and tp_size == 1
         self._h_alt = {k: mk(*(getattr(self, k).shape,), dtype=getattr(self, k).dtype)
                        for k in ("_h_ids", "_h_pos", "_h_slots", "_h_ctx", "_h_bt", "_h_temp", "_h_topk", "_h_topp",
-                                 "_h_cnt", "_h_tokens")}
+                                 "_h_cnt", "_h_tokens", "_h_order")}
         self._inflight = None  # launched decode step whose tokens are not consumed yet
         max_parts = math.ceil(self.max_model_len / part_size)
         self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
@@ -647,9 +650,10 @@ class LLMEngine:
             self._h_topk[B:Bp] = 1
             self._h_topp[B:Bp] = 1.0
             self._h_cnt[B:Bp] = 0
+        self._fill_order(Bp)
         pairs = [(self._d_pos, self._h_pos), (self._d_slots, self._h_slots), (self._d_ctx, self._h_ctx),
                  (self._d_temp, self._h_temp), (self._d_topk, self._h_topk), (self._d_topp, self._h_topp),
-                 (self._d_cnt, self._h_cnt), (self._d_bt, self._h_bt)]
+                 (self._d_cnt, self._h_cnt), (self._d_bt, self._h_bt), (self._d_order, self._h_order)]
         if src_rows is None:
             pairs.append((self._d_ids, self._h_ids))
         else:
@@ -743,9 +747,10 @@ class LLMEngine:
             self._h_topk[B:Bp] = 1
             self._h_topp[B:Bp] = 1.0
             self._h_cnt[B:Bp] = 0
+        self._fill_order(Bp)
         for d, h in ((self._d_ids, self._h_ids), (self._d_pos, self._h_pos), (self._d_slots, self._h_slots),
                      (self._d_ctx, self._h_ctx), (self._d_temp, self._h_temp), (self._d_topk, self._h_topk),
-                     (self._d_topp, self._h_topp), (self._d_cnt, self._h_cnt)):
+                     (self._d_topp, self._h_topp), (self._d_cnt, self._h_cnt), (self._d_order, self._h_order)):
             d[:Bp].copy_(h[:Bp], non_blocking=True)
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
         t1 = time.perf_counter()
@@ -776,6 +781,15 @@ class LLMEngine:
         self.stats["decode_host_s"] = self.stats.get("decode_host_s", 0.0) + (t1 - t0) + (t3 - t2)
         self.stats["decode_gpu_wait_s"] = self.stats.get("decode_gpu_wait_s", 0.0) + (t2 - t1)
 
+    def _fill_order(self, Bp: int) -> None:
+        """Host: the decode attention's dispatch order for this step, longest context first (LPT
+        balance of the two workgroup rounds per CU; benchmarks/decode_attn_bench.py)."""
+        if not self.lpt_order:
+            self._h_order[:Bp] = torch.arange(Bp, dtype=torch.int32)
+            return
+        ctx = self._h_ctx[:Bp].numpy()
+        self._h_order[:Bp] = torch.from_numpy(np.argsort(-ctx, kind="stable").astype(np.int32))
+
     def _decode_part(self, Bp: int) -> int:
         """Decode attention key partition for a step of Bp sequences: long partitions once the
         (sequence, kv head) pairs alone cover every CU twice over (512 pairs on 256 CUs)."""
@@ -785,7 +799,7 @@ class LLMEngine:
     def _decode_body(self, Bp: int):
         meta = AttnMeta(decode=True, positions=self._d_pos[:Bp], slots=self._d_slots[:Bp],
                         block_tables=self._d_bt[:Bp], ctx_lens=self._d_ctx[:Bp], workspace=self._workspace,
-                        part_size=self._decode_part(Bp))
+                        part_size=self._decode_part(Bp), order=self._d_order[:Bp] if self.is_gpu else None)
         h = self.model.forward(self._d_ids[:Bp], meta, self.kv)
         logits = self.model.logits(h)
         if self.is_gpu:

@@ -58,6 +58,7 @@ class AttnMeta:
     n_decode: int = 0
     dec_block_tables: torch.Tensor | None = None
     dec_ctx_lens: torch.Tensor | None = None
+    order: torch.Tensor | None = None  # int32 [B] decode attention dispatch order (longest context first)
 
 
 class KVCache:
@@ -216,7 +217,7 @@ class LlamaModel:
         q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
         if meta.decode:
             a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
-                                 meta.workspace)
+                                 meta.workspace, order=meta.order)
         elif meta.n_decode:
             a = self._mixed_attention(q, kv, li, meta)
         else:

@@ -257,8 +257,10 @@ class DecodeWorkspace:
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
-                 scale=None, out=None):
-    """q [B, Hq, D] (one new token per sequence) over the paged caches."""
+                 scale=None, out=None, order=None):
+    """q [B, Hq, D] (one new token per sequence) over the paged caches.  ``order`` (int32 [B], a
+    permutation of the batch) is the order the (sequence, kv head) items are dispatched in: longest
+    context first balances the two rounds of workgroups every CU runs at RAG batch sizes."""
     B, Hq, D = q.shape
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if not q.is_cuda:
@@ -281,9 +283,12 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
                "decode workspace too small")
         ws_o, ws_m, ws_l, ws_c = workspace.o, workspace.m, workspace.l, workspace.cnt
     out = torch.empty_like(q) if out is None else out
+    if order is not None:
+        _i32(order)
+        expect(order.is_cuda and order.numel() >= B, "decode order must hold the batch")
     native().paged_decode_attention(ptr(q), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
                                     ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
-                                    D, int(part_size), int(max_parts), float(scale), stream(q))
+                                    D, int(part_size), int(max_parts), float(scale), stream(q), ptr(order))
     return out
 
 

@@ -490,3 +490,6 @@ def test_paged_decode_8k_context(part, split):
     out = ops.paged_decode(q, kc, vc, bt, ctxt, part, ws)
     exp = ref.paged_decode(q, kc, vc, bt, ctxt, 1 / math.sqrt(D))
     close(out, exp)
+    # longest-first dispatch order: same result (each item writes its own sequence's rows)
+    order = torch.argsort(ctxt, descending=True).to(torch.int32)
+    assert torch.equal(ops.paged_decode(q, kc, vc, bt, ctxt, part, ws, order=order), out)
