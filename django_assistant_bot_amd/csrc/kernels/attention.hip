@@ -16,6 +16,8 @@
 //
 // Reference behaviour replaced: HF BertSelfAttention (ai/embedders/transformers.py:18-22) and the
 // HF Llama attention inside model.generate (ai/providers/transformers.py:57-66).
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -295,7 +297,7 @@ struct DecodeParams {
   float scale_log2;
 };
 
-template <int D>
+template <int D, bool KV_NT>
 __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, int total_items) {
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
@@ -357,8 +359,8 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
       const auto vd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), 0, bytes, 0x00020000);
 #pragma unroll
       for (int c = 0; c < CH; ++c) {
-        kr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(kd, lane * 16, c * 1024, 0));
-        vr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vd, lane * 16, c * 1024, 0));
+        kr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(kd, lane * 16, c * 1024, KV_NT ? 2 : 0));
+        vr[c] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(vd, lane * 16, c * 1024, KV_NT ? 2 : 0));
       }
     };
     auto stage = [&](const u32x4(&kr)[CH], const u32x4(&vr)[CH]) {
@@ -641,10 +643,19 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.scale_log2 = scale * 1.4426950408889634f;
   const int total_items = max_parts * Hkv * batch;
   dim3 grid(total_items < 2048 ? total_items : 2048);
+  // K/V are read exactly once per step: non-temporal loads (aux = 2).  In the Llama-3-8B decode step
+  // at batch 128 this took the attention from 127 to 111 us per layer (5.1 -> 5.8 TB/s;
+  // profiles/decode_round2.md).  DAB_KV_NT=0 restores the default policy for A/B runs.
+  static const bool kv_nt = [] {
+    const char* v = getenv("DAB_KV_NT");
+    return v == nullptr || v[0] != '0';
+  }();
   if (D == 128) {
-    hipLaunchKernelGGL(paged_decode_kernel<128>, grid, dim3(256), 0, s, prm, total_items);
+    if (kv_nt) hipLaunchKernelGGL((paged_decode_kernel<128, true>), grid, dim3(256), 0, s, prm, total_items);
+    else hipLaunchKernelGGL((paged_decode_kernel<128, false>), grid, dim3(256), 0, s, prm, total_items);
   } else if (D == 64) {
-    hipLaunchKernelGGL(paged_decode_kernel<64>, grid, dim3(256), 0, s, prm, total_items);
+    if (kv_nt) hipLaunchKernelGGL((paged_decode_kernel<64, true>), grid, dim3(256), 0, s, prm, total_items);
+    else hipLaunchKernelGGL((paged_decode_kernel<64, false>), grid, dim3(256), 0, s, prm, total_items);
   } else {
     return hipErrorInvalidValue;
   }

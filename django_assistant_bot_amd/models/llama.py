@@ -110,6 +110,7 @@ class LlamaModel:
         if (os.environ.get("DAB_DECODE_GEMM", "stream") == "stream" and self.device.type == "cuda"
                 and self.use_skinny):
             self.stream = self._make_stream_copies()
+
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
