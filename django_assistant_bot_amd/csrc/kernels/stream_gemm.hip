@@ -41,11 +41,11 @@ struct StreamParams {
   const bf16* residual;
   long ldr;
   int M, N, K, S, kc;
-  int epi;       // 0 none, 2 swiglu
+  int epi;       // 0 none, 2 swiglu (16-row gate | up groups), 4 swiglu (8-row groups)
   int slab_wt;   // split-K slabs stored write-through (sc1)
 };
 
-constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2;
+constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2, ST_EPI_SWIGLU8 = 4;
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
@@ -70,11 +70,15 @@ __device__ __forceinline__ bool static_for(F&& f) {
 
 // ABL (benchmark ablations only): 1 no X staging, 2 no MFMA, 3 weight stream only (no X, no LDS
 // reads, no MFMA); results are garbage, timings bound the parts.
-template <int MT, int RT, int KG, int KS, int NB, int NWIN, int NL, bool SHUF, bool NT_W, int ABL = 0>
-__global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamParams p) {
-  constexpr int NWC = 4;              // compute waves (waves 4.. are the NL X loaders)
+//
+// NWC compute waves (waves NWC.. are the NL X loaders).  BN = 16 RT NWC / KG need not be a power of
+// two: 112 rows (7 waves) tile Llama-3-8B's 28672 gate_up rows onto exactly 256 workgroups, 96 rows
+// (6 waves, 4 K-slices) its 6144 qkv rows; the epilogue tile keeps a power-of-two row stride BNP.
+template <int MT, int RT, int KG, int KS, int NB, int NWIN, int NL, bool SHUF, bool NT_W, int ABL = 0, int NWC = 4>
+__global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamParams p) {
   constexpr int RG = NWC / KG;        // row groups
   constexpr int BN = 16 * RT * RG;    // weight rows per workgroup
+  constexpr int BNP = BN <= 64 ? 64 : BN <= 128 ? 128 : 256;  // epilogue tile row stride (XOR swizzle range)
   constexpr int MP = 16 * MT;         // padded M
   constexpr int ROWB = KS * 2;        // bytes per staged X row
   constexpr int CPR = KS / 8;         // 16-B chunks per staged row
@@ -83,7 +87,8 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
   constexpr int GPL = GPS / NL;       // ... per loader wave
   constexpr int KW = KS / KG;         // k per compute wave per stage
   constexpr int CPW = KW / 32;        // 32-deep MFMA chunks per wave per stage
-  constexpr int RED = KG * MP * BN * 4;
+  constexpr int RED = KG * MP * BNP * 4;
+  static_assert(BN <= 256 && BN % 16 == 0, "tile rows");
   constexpr int SMEM = NB * XBUF > RED ? NB * XBUF : RED;
   static_assert(CPR >= 16 && CPW >= 1 && KW % 32 == 0, "stage shape");
   static_assert(NB >= 2 && (NB - 2) * GPL <= 63 && GPS % NL == 0, "loader vmcnt range");
@@ -228,7 +233,7 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
       for (int t = 0; t < MT; ++t) {
         const int m = 16 * t + li;
         const int col = (16 * (RT * rg + a) + 4 * g) ^ (4 * (m & 15));
-        *reinterpret_cast<f32x4*>(red + (kg * MP + m) * BN + col) = acc[a][t];
+        *reinterpret_cast<f32x4*>(red + (kg * MP + m) * BNP + col) = acc[a][t];
       }
   }
 
@@ -237,9 +242,9 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
   __builtin_amdgcn_s_barrier();
   auto tile4 = [&](int m, int c4) DAB_INLINE {
     const int col = c4 ^ (4 * (m & 15));
-    f32x4 v = *reinterpret_cast<const f32x4*>(red + m * BN + col);
+    f32x4 v = *reinterpret_cast<const f32x4*>(red + m * BNP + col);
 #pragma unroll
-    for (int q = 1; q < KG; ++q) v += *reinterpret_cast<const f32x4*>(red + (q * MP + m) * BN + col);
+    for (int q = 1; q < KG; ++q) v += *reinterpret_cast<const f32x4*>(red + (q * MP + m) * BNP + col);
     return v;
   };
   constexpr int NT = 64 * (NWC + NL);
@@ -266,20 +271,22 @@ __global__ __launch_bounds__(64 * (4 + NL), 1) void stream_gemm_kernel(StreamPar
     return;
   }
   bf16* out = (bf16*)p.out;
-  if (p.epi == ST_EPI_SWIGLU) {
-    // rows [32i, 32i+16) gate, [32i+16, 32i+32) up -> output columns n0/2 + 16i + j
+  if (p.epi == ST_EPI_SWIGLU || p.epi == ST_EPI_SWIGLU8) {
+    // hg-row groups: rows [2 hg i, 2 hg i + hg) gate, [2 hg i + hg, 2 hg (i + 1)) up -> output
+    // columns n0/2 + hg i + j; each thread makes 4 outputs
+    const int hg = p.epi == ST_EPI_SWIGLU ? 16 : 8, pp = hg / 4;
     for (int e = tid; e < MP * (BN / 8); e += NT) {
       const int m = e / (BN / 8), part = e % (BN / 8);
       if (m >= p.M) continue;
-      const int i = part >> 2, j0 = (part & 3) * 4;
-      const f32x4 gt = tile4(m, 32 * i + j0), up = tile4(m, 32 * i + 16 + j0);
+      const int i = part / pp, j0 = (part % pp) * 4;
+      const f32x4 gt = tile4(m, 2 * hg * i + j0), up = tile4(m, 2 * hg * i + hg + j0);
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = gt[j] / (1.f + __expf(-gt[j])) * up[j];
       u32x2 v;
       v[0] = pack2bf(o[0], o[1]);
       v[1] = pack2bf(o[2], o[3]);
-      *reinterpret_cast<u32x2*>(out + (size_t)m * p.ldo + n0 / 2 + 16 * i + j0) = v;
+      *reinterpret_cast<u32x2*>(out + (size_t)m * p.ldo + n0 / 2 + hg * i + j0) = v;
     }
     return;
   }
@@ -306,6 +313,7 @@ struct StreamCfg {
   int mt, rt, kg, nb, nwin, nl;
   bool shuf;    // weights in the shuffle_weights layout
   int abl = 0;  // benchmark ablation (see the kernel)
+  int nwc = 4;  // compute waves
 };
 static constexpr StreamCfg kStreamCfgs[] = {
     {8, 2, 2, 3, 3, 1, false},  // 0: M<=128 BN 64
@@ -328,24 +336,29 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {8, 2, 1, 4, 3, 4, true, 1},  // 17: = 10 without X staging        (ablation, wrong results)
     {8, 2, 1, 4, 3, 4, true, 2},  // 18: = 10 without MFMA             (ablation, wrong results)
     {8, 2, 1, 4, 3, 4, true, 3},  // 19: = 10 weight stream only       (ablation, wrong results)
+    // whole-chip tilings at M <= 128: BN = 16 x compute waves (one 16-row tile per wave)
+    {8, 1, 1, 4, 4, 2, true, 0, 7},  // 20: BN 112, 7 compute + 2 loader waves (gate_up 28672 -> 256 WGs)
+    {8, 1, 1, 4, 4, 2, true, 0, 6},  // 21: BN 96, 6 + 2 waves (qkv 6144 x S4 -> 256 WGs)
+    {8, 1, 1, 3, 6, 1, true, 0, 7},  // 22: = 20, 1 loader wave, 6-stage weight ring
+    {8, 1, 1, 3, 6, 2, true, 0, 6},  // 23: = 21, 6-stage weight ring
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
 template <int C>
 static void launch_cfg(const StreamParams& p, hipStream_t s, bool nt) {
   constexpr StreamCfg c = kStreamCfgs[C];
-  const dim3 grid((p.N / (16 * c.rt * (4 / c.kg))) * p.S), block(64 * (4 + c.nl));
+  const dim3 grid((p.N / (16 * c.rt * (c.nwc / c.kg))) * p.S), block(64 * (c.nwc + c.nl));
   if (nt)
-    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true, c.abl>), grid, block, 0,
-                       s, p);
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true, c.abl, c.nwc>), grid,
+                       block, 0, s, p);
   else
-    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, false, c.abl>), grid, block, 0,
-                       s, p);
+    hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, false, c.abl, c.nwc>), grid,
+                       block, 0, s, p);
 }
 
 int stream_gemm_bn(int cfg) {
   if (cfg < 0 || cfg >= kNumStreamCfgs) return 0;
-  return 16 * kStreamCfgs[cfg].rt * (4 / kStreamCfgs[cfg].kg);
+  return 16 * kStreamCfgs[cfg].rt * (kStreamCfgs[cfg].nwc / kStreamCfgs[cfg].kg);
 }
 
 int stream_gemm_max_m(int cfg) { return (cfg < 0 || cfg >= kNumStreamCfgs) ? 0 : 16 * kStreamCfgs[cfg].mt; }
@@ -367,7 +380,8 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   const int bn = stream_gemm_bn(cfg);
   if (!bn || M > stream_gemm_max_m(cfg)) return hipErrorInvalidValue;
   if (N % bn || S < 1 || K % (S * KS) || ldx % 8 || ldw % 8 || ldo % 8) return hipErrorInvalidValue;
-  if (epilogue != ST_EPI_NONE && epilogue != ST_EPI_SWIGLU) return hipErrorInvalidValue;
+  if (epilogue != ST_EPI_NONE && epilogue != ST_EPI_SWIGLU && epilogue != ST_EPI_SWIGLU8) return hipErrorInvalidValue;
+  if (epilogue == ST_EPI_SWIGLU && bn % 32) return hipErrorInvalidValue;  // whole 16 + 16 row pairs per tile
   if (S > 1 && (epilogue != ST_EPI_NONE || residual)) return hipErrorInvalidValue;
   if (residual && ldr % 8) return hipErrorInvalidValue;
   if ((long)bn * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;  // buffer descriptor range

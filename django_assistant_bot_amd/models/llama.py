@@ -132,15 +132,30 @@ class LlamaModel:
         return x
 
     STREAM_CFG_M64, STREAM_CFG_M128 = 13, 10  # stream_gemm.hip configurations (BN 128, shuffled)
+    # whole-chip tiling at M 65..128 (one 16-row tile per compute wave): gate_up's 28672 rows / 112
+    # make exactly 256 workgroups where BN 128 left 32 of the 256 CUs idle: 54.9 -> 51.5 us cold
+    # (kernel_bench stream).  qkv at 96 rows x 4 K-slices (cfg 21, also 256 workgroups) measured
+    # slower than BN 128 x 4 (17.1 vs 15.8 us) and stays on cfg 10.  DAB_STREAM_WIDE=0: BN 128 (A/B).
+    STREAM_WIDE = {"gate_up": 20}
+    _wide = os.environ.get("DAB_STREAM_WIDE", "1") != "0"
 
     @staticmethod
     def _stream_ok(w: torch.Tensor) -> bool:
         return w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
 
+    def _stream_cfg(self, name: str, M: int, N: int) -> int:
+        if M <= 64:
+            return self.STREAM_CFG_M64
+        cfg = self.STREAM_WIDE.get(name) if self._wide else None
+        if cfg is not None and N % ops.native().stream_gemm_bn(cfg) == 0:
+            return cfg
+        return self.STREAM_CFG_M128
+
     def _make_stream_copies(self) -> bool:
         """Shuffled decode copies of the projection weights (and of the LM head, which decode and
         the prefill last-token logits stream at M <= 128) when they fit comfortably (each copy is
-        the size of the weights; the KV pool is sized from what is left)."""
+        the size of the weights; the KV pool is sized from what is left).  The gate_up copy is
+        regrouped to 8-row [gate | up] pairs (EPI_SWIGLU8) so any 16-row multiple tiles it."""
         names = ("qkv", "o", "gate_up", "down") if self.interleaved_mlp else ("qkv", "o", "down")
         mats = [(L, n) for L in self.layers for n in names if self._stream_ok(getattr(L, f"{n}_w"))]
         extra = sum(getattr(L, f"{n}_w").numel() * 2 for L, n in mats)
@@ -150,15 +165,18 @@ class LlamaModel:
         if not mats or extra > 0.4 * free:
             return False
         for L, n in mats:
-            setattr(L, f"{n}_ws", ops.shuffle_weights(getattr(L, f"{n}_w")))
+            w = getattr(L, f"{n}_w")
+            if n == "gate_up":
+                w = ops.regroup_gate_up(w, 16, 8)
+            setattr(L, f"{n}_ws", ops.shuffle_weights(w))
         if head:
             self.lm_head_ws = ops.shuffle_weights(self.lm_head)
         return True
 
     @staticmethod
-    def _stream_splits(N: int, K: int) -> int:
-        """K-slices for stream_gemm: the fewest that give >= 192 workgroups of 128 weight rows."""
-        tiles, best = N // 128, 1
+    def _stream_splits(N: int, K: int, bn: int = 128) -> int:
+        """K-slices for stream_gemm: the fewest that give >= 192 workgroups of ``bn`` weight rows."""
+        tiles, best = N // bn, 1
         for s in (1, 2, 4, 8, 16):
             if K % (128 * s):
                 break
@@ -179,8 +197,8 @@ class LlamaModel:
         consumer can sum them) or prefill path (native MFMA GEMM: the 256x256 8-phase kernel for
         large token counts, ``gemm256.hip``)."""
         if sk and ws is not None:
-            cfg = self.STREAM_CFG_M64 if x.shape[0] <= 64 else self.STREAM_CFG_M128
-            s = self._stream_splits(w.shape[0], w.shape[1])
+            cfg = self._stream_cfg(name, x.shape[0], w.shape[0])
+            s = self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
             out = ops.stream_gemm(x, ws, splits=s, cfg=cfg, nt=True)
             return ops.skinny_reduce(out) if (s > 1 and not allow_slabs) else out
         if not sk or name not in self.skinny_for:
@@ -227,8 +245,8 @@ class LlamaModel:
         o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
         h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
         if sk and self.interleaved_mlp and L.gate_up_ws is not None:
-            act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU, nt=True,
-                                  cfg=self.STREAM_CFG_M64 if T <= 64 else self.STREAM_CFG_M128)
+            act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU8, nt=True,
+                                  cfg=self._stream_cfg("gate_up", T, L.gate_up_ws.shape[0]))
         elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
             act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
         elif self.interleaved_mlp and h.is_cuda:

@@ -17,6 +17,7 @@ from . import reference as ref
 from ._lib import expect, expect_bf16_contig, native, ptr, same_device, stream
 
 EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SCORES = ref.EPI_NONE, ref.EPI_GELU, ref.EPI_SWIGLU, ref.EPI_SCORES
+EPI_SWIGLU8 = ref.EPI_SWIGLU8
 
 
 def _i32(t: torch.Tensor) -> None:
@@ -480,10 +481,12 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=N
         expect(out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
         ldo = N
     else:
-        n_out = N // 2 if epilogue == EPI_SWIGLU else N
+        n_out = N // 2 if epilogue in (EPI_SWIGLU, EPI_SWIGLU8) else N
         if residual is not None:
             expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
                    and tuple(residual.shape) == (M, N), "residual must be bf16 [M, N]")
+        if epilogue == EPI_SWIGLU:
+            expect(bn % 32 == 0, f"stream_gemm cfg {cfg}: EPI_SWIGLU needs 32-row tiles (use EPI_SWIGLU8)")
         if out is None:
             out = torch.empty((M, n_out), dtype=torch.bfloat16, device=x.device)
         expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
@@ -511,14 +514,22 @@ def skinny_reduce(slabs, residual=None, out=None):
     return out
 
 
-def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor) -> torch.Tensor:
-    """[F, H] gate and up weights -> [2F, H] interleaved in 16-row groups [g16 | u16 | g16 | u16 ...]
-    (the layout the SWIGLU epilogue of gemm_bt consumes)."""
+def interleave_gate_up(w_gate: torch.Tensor, w_up: torch.Tensor, group: int = 16) -> torch.Tensor:
+    """[F, H] gate and up weights -> [2F, H] interleaved in ``group``-row groups [g | u | g | u ...]
+    (16: the layout the SWIGLU epilogue of gemm_bt / gemm256 consumes; 8: EPI_SWIGLU8)."""
     Fd, H = w_gate.shape
-    assert Fd % 16 == 0
-    g = w_gate.view(Fd // 16, 16, H)
-    u = w_up.view(Fd // 16, 16, H)
+    assert Fd % group == 0
+    g = w_gate.reshape(Fd // group, group, H)
+    u = w_up.reshape(Fd // group, group, H)
     return torch.stack([g, u], dim=1).reshape(2 * Fd, H).contiguous()
+
+
+def regroup_gate_up(w: torch.Tensor, src: int = 16, dst: int = 8) -> torch.Tensor:
+    """Re-interleave [2F, H] gate|up weights from ``src``-row to ``dst``-row groups."""
+    n2, H = w.shape
+    v = w.reshape(n2 // (2 * src), 2, src, H)
+    gate, up = v[:, 0].reshape(n2 // 2, H), v[:, 1].reshape(n2 // 2, H)
+    return interleave_gate_up(gate, up, dst)
 
 
 # ----------------------------------------------------------------------------------------------

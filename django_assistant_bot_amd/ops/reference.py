@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 
 EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SCORES = 0, 1, 2, 3
+EPI_SWIGLU8 = 4  # SwiGLU over 8-row [gate | up] groups (decode copies of whole-chip stream_gemm tilings)
 
 
 def rmsnorm(x, w, eps, residual=None):
@@ -171,9 +172,9 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
         c = c + bias.float()
     if epilogue == EPI_GELU:
         c = F.gelu(c)
-    elif epilogue == EPI_SWIGLU:
-        N = c.shape[1]
-        c = c.view(c.shape[0], N // 32, 2, 16)
+    elif epilogue in (EPI_SWIGLU, EPI_SWIGLU8):
+        N, hg = c.shape[1], 16 if epilogue == EPI_SWIGLU else 8
+        c = c.view(c.shape[0], N // (2 * hg), 2, hg)
         c = (F.silu(c[:, :, 0]) * c[:, :, 1]).reshape(c.shape[0], N // 2)
     if residual is not None:
         c = c + residual.float()

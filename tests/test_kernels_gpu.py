@@ -266,9 +266,10 @@ def test_skinny_gemm(M, N, K, S):
         close(ops.skinny_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(17)))
+@pytest.mark.parametrize("cfg", list(range(17)) + [20, 21, 22, 23])
 @pytest.mark.parametrize("M", [1, 37, 64, 100, 128])
-@pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1)])
+@pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1),
+                                   (672, 512, 1), (1344, 1024, 4), (2688, 1792, 7)])
 def test_stream_gemm(cfg, M, N, K, S):
     """Warp-specialised streaming GEMM vs the fp32 reference: bf16 out (+ residual) and fp32 slabs,
     stage counts that do and do not fill the register ring (nst = 1..10)."""
@@ -301,6 +302,22 @@ def test_stream_swiglu_and_strided_x(cfg, M):
         w = ops.shuffle_weights(w)
     got = ops.stream_gemm(x, w, epilogue=ops.EPI_SWIGLU, cfg=cfg)
     exp = ref.silu_mul(ref.gemm_bt(x.contiguous(), torch.cat([wg, wu], 0)))
+    close(got, exp, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("cfg", [10, 13, 20, 21, 22, 23])
+@pytest.mark.parametrize("M", [5, 64, 128])
+def test_stream_swiglu8(cfg, M):
+    """8-row [gate | up] groups (EPI_SWIGLU8, the decode copy of gate_up): BN 96 / 112 / 128 tiles."""
+    if M > ops.native().stream_gemm_max_m(cfg):
+        pytest.skip("M outside this configuration")
+    F, K = 1344, 1024
+    x, wg, wu = bf(M, K), bf(F, K, scale=0.05), bf(F, K, scale=0.05)
+    w16 = ops.interleave_gate_up(wg, wu)
+    w8 = ops.regroup_gate_up(w16, 16, 8)
+    assert torch.equal(w8, ops.interleave_gate_up(wg, wu, 8))
+    got = ops.stream_gemm(x, ops.shuffle_weights(w8), epilogue=ops.EPI_SWIGLU8, cfg=cfg)
+    exp = ref.silu_mul(ref.gemm_bt(x, torch.cat([wg, wu], 0)))
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 
