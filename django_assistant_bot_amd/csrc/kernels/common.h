@@ -52,6 +52,22 @@ __device__ __forceinline__ u32x4 pack8(const float* f) {
   return v;
 }
 
+// Exact-erf GELU, 0.5 x (1 + erf(x / sqrt 2)), without the library erff (a long piecewise routine
+// that, in a GEMM epilogue, costs more VALU time than the tile's bf16 stores): erfc by Abramowitz &
+// Stegun 7.1.26 (|error| <= 1.5e-7 in erf), one v_rcp + one v_exp + 7 FMAs.  For x < 0 the result is
+// 0.5 x erfc(|x| / sqrt 2) directly (no cancellation), for x >= 0 it is x - 0.5 x erfc(x / sqrt 2).
+__device__ __forceinline__ float gelu_erf(float x) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.f));
+  float q = fmaf(1.061405429f, t, -1.453152027f);
+  q = fmaf(q, t, 1.421413741f);
+  q = fmaf(q, t, -0.284496736f);
+  q = fmaf(q, t, 0.254829592f);
+  q *= t;
+  const float c = 0.5f * x * q * __builtin_amdgcn_exp2f(z * z * -1.4426950408889634f);  // 0.5 x erfc(z)
+  return x >= 0.f ? x - c : c;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void gelu_kernel(bf16* __restrict__ out, const
       for (int j = 0; j < 8; ++j) v[j] += b[j];
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+    for (int j = 0; j < 8; ++j) v[j] = gelu_erf(v[j]);
     reinterpret_cast<u32x4*>(out)[i] = pack8(v);
   }
 }

@@ -197,7 +197,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
         }
         if (EPI == EPI_GELU) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = 0.5f * o[r] * (1.f + erff(o[r] * 0.70710678118654752f));
+          for (int r = 0; r < 4; ++r) o[r] = gelu_erf(o[r]);
         }
         if (p.residual) {
           const bf16* rr = p.residual + (size_t)m * p.ldr + n;

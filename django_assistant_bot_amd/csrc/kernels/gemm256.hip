@@ -386,7 +386,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             }
             if constexpr (EPI == G_GELU) {
 #pragma unroll
-              for (int r = 0; r < 8; ++r) o[r] = 0.5f * o[r] * (1.f + erff(o[r] * 0.70710678118654752f));
+              for (int r = 0; r < 8; ++r) o[r] = gelu_erf(o[r]);
             }
             if constexpr (RES) {
               const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(rR, (unsigned)((mr * p.ldr + nc) * 2), 0, 0);

@@ -68,6 +68,18 @@ def test_bert_embed_and_pool():
     close(ops.embed_gather(ids, word), word[ids.long()], atol=0, rtol=0)
 
 
+def test_gelu_erf_sweep():
+    """The epilogue GELU (A&S 7.1.26 erfc, common.h gelu_erf) against torch's exact-erf GELU on every
+    bf16 value in [-12, 12]: within one bf16 rounding of the exact result (absolute 2e-7 near 0)."""
+    x = torch.arange(-12 * 4096, 12 * 4096, device=DEV, dtype=torch.float32).div(4096).to(torch.bfloat16)
+    x = torch.unique(x).reshape(1, -1)
+    x = x[:, : x.shape[1] // 8 * 8].contiguous()
+    exact = torch.nn.functional.gelu(x.float())
+    got = ops.gelu(x).float()
+    ulp = exact.abs().clamp_min(1e-30) * 2.0 ** -8
+    assert bool(((got - exact).abs() <= ulp + 2e-7).all())
+
+
 def test_gelu_silu():
     x, b = bf(33, 3072), bf(3072)
     close(ops.gelu(x, b), ref.gelu(x, b))
