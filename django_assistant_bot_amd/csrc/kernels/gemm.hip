@@ -15,6 +15,8 @@
 //   * operands swapped in the MFMA (B rows feed the A slot) so each lane ends with 4 consecutive
 //     output columns of one row -> 8-B / 16-B epilogue stores;
 //   * bijective XCD-aware block remap (T1) so neighbouring tiles share an XCD's L2.
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -271,6 +273,15 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   if (M <= 0 || N <= 0) return 0;
   if (K % 64 || N % 4 || lda % 8 || ldb % 8 || cap <= 0 || !thr || !cnt || !cand_val || !cand_idx)
     return hipErrorInvalidValue;
+  // query batches that fill 256-row tiles: the persistent 8-phase kernel (a 10M-row scan at K 768 is
+  // 39k short-K tiles per 256 queries; the one-tile-per-workgroup kernel below pays its prologue and
+  // epilogue on every one of them).  DAB_CAND256=0 keeps the 128x128 kernel (A/B runs).
+  static const bool use256 = [] {
+    const char* v = getenv("DAB_CAND256");
+    return v == nullptr || v[0] != '0';
+  }();
+  if (use256 && M >= 128 && K % 128 == 0)
+    return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   GemmParams p{};
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;

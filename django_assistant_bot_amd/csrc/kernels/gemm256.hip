@@ -36,7 +36,7 @@ namespace dab {
 
 namespace {
 
-enum { G_NONE = 0, G_GELU = 1, G_SWIGLU = 2 };
+enum { G_NONE = 0, G_GELU = 1, G_SWIGLU = 2, G_CAND = 3 };
 
 struct G256 {
   const bf16* A;
@@ -47,6 +47,15 @@ struct G256 {
   int M, N, K;
   long lda, ldb, ldc, ldr;
   int gm;  // tile rows per group of the grouped tile order
+  // G_CAND (index threshold search, see gemm.hip EPI_CANDIDATES): filtered scores >= thr[m] are
+  // appended to row m's candidate list; no C is written and N need not be a multiple of 256
+  const int* row_group;  // [N] (<0 = deleted) or null
+  const int* q_group;    // [M] (<0 = any) or null
+  const float* thr;      // [M]
+  int* cnt;              // [M]
+  float* cand_val;       // [M, cap]
+  int* cand_idx;         // [M, cap]
+  int cap;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -92,7 +101,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // so the tile ids are split into 8 contiguous chunks (bijective for any count) and the nper
   // workgroups of chunk x take ids cstart + l, cstart + l + nper, ... -> at any time the ~32
   // workgroups of one XCD run consecutive (grouped) tiles that share A / B panels in its L2.
-  const int tiles_m = (p.M + 255) >> 8, tiles_n = p.N >> 8;
+  const int tiles_m = (p.M + 255) >> 8, tiles_n = EPI == G_CAND ? (p.N + 255) >> 8 : p.N >> 8;
   const int nwg = tiles_m * tiles_n;
   const int G = gridDim.x, bid = blockIdx.x;
   const int x = bid & 7, l = bid >> 3;
@@ -304,7 +313,64 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
     const long c_rows = min(256, p.M - m0);
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
-    if constexpr (EPI == G_SWIGLU) {
+    if constexpr (EPI == G_CAND) {
+      // Same lane map as the plain epilogue below (permlane16 pairs: 8 contiguous columns per lane).
+      // The per-row threshold / group and per-column row-group loads are waited for here, which
+      // also retires the next tile's prefetched pieces (as the bias epilogue does); the appends that
+      // follow are younger than every piece a later counted wait looks for, so they only make those
+      // waits stricter.
+      const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
+      float thr_r[2][4];
+      int qg_r[2][4];
+      int rg[2][8];
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = min(m0 + 128 * ih + 64 * wr + 16 * i + e_li, p.M - 1);
+          thr_r[ih][i] = p.thr[m];
+          qg_r[ih][i] = p.q_group ? p.q_group[m] : -1;
+        }
+#pragma unroll
+      for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const int n = n0 + 128 * jh + 32 * e_wc + cq + r;
+          rg[jh][r] = n >= p.N ? -1 : p.row_group ? p.row_group[n] : 0;
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int m = m0 + 128 * ih + 64 * wr + 16 * i + e_li;
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh) {
+            float o[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[ih][jh][i][0][r]),
+                                                         __float_as_uint(acc[ih][jh][i][1][r]), false, false);
+              o[r] = __uint_as_float(sw[0]);
+              o[4 + r] = __uint_as_float(sw[1]);
+            }
+            if (m >= p.M) continue;
+            const int nb = n0 + 128 * jh + 32 * e_wc + cq;
+            const int qg = qg_r[ih][i];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const bool ok = rg[jh][r] >= 0 && (qg < 0 || rg[jh][r] == qg);
+              if (ok && o[r] >= thr_r[ih][i]) {
+                const int slot = atomicAdd(p.cnt + m, 1);
+                if (slot < p.cap) {
+                  p.cand_val[(size_t)m * p.cap + slot] = o[r];
+                  p.cand_idx[(size_t)m * p.cap + slot] = nb + r;
+                }
+              }
+            }
+          }
+        }
+    } else if constexpr (EPI == G_SWIGLU) {
       // weight rows interleaved in 16-row groups [gate 16 | up 16]: jn = 0 gate, jn = 1 up
       float bg[2][4], bu[2][4];
       if constexpr (BIAS) {
@@ -419,6 +485,38 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 #undef G256_READ_A
 #undef G256_READ_B
 #undef G256_MFMA
+}
+
+// Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
+// index rows B [N, K], any N; K % 128 == 0.
+int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
+                       const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                       hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 128 || K <= 0 || lda % 8 || ldb % 8 || cap <= 0) return hipErrorInvalidValue;
+  if ((255L * lda + K) * 2 >= (1L << 31) || (255L * ldb + K) * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  G256 p{};
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = ldb;
+  p.gm = 4;
+  p.row_group = row_group;
+  p.q_group = q_group;
+  p.thr = thr;
+  p.cnt = cnt;
+  p.cand_val = cand_val;
+  p.cand_idx = cand_idx;
+  p.cap = cap;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const int nwg = tiles > cus ? cus : (int)tiles;
+  hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false>), dim3(nwg), dim3(512), 0, s, p);
+  return hipGetLastError();
 }
 
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.

@@ -53,6 +53,9 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
 // gemm256.hip (large-M prefill / encoder GEMM, 256x256 8-phase schedule; epilogue 0 none, 1 GELU,
 // 2 SwiGLU on [gate 16 | up 16]-interleaved weight rows; bias / residual optional)
 int gemm256_ok(int M, int N, int K, long lda, long ldb);
+int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
+                       const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                       hipStream_t s);
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
             const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s);
 

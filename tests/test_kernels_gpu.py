@@ -428,8 +428,11 @@ def test_sampling_distribution(fast):
     assert int(tok.max()) <= 1
 
 
+@pytest.mark.parametrize("nq", [37, 300])
 @pytest.mark.parametrize("groups", [False, True])
-def test_index_threshold_search_matches_full_scan(groups):
+def test_index_threshold_search_matches_full_scan(groups, nq):
+    """37 queries: the 128x128 candidate kernel; 300: the persistent gemm256 G_CAND epilogue
+    (600k rows: the last 256-row tile is partial)."""
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
     n, dim = 600_000, 128
@@ -438,8 +441,8 @@ def test_index_threshold_search_matches_full_scan(groups):
     grp = (torch.arange(n) % 3).numpy().astype("int32") if groups else None
     idx.add(torch.arange(n).numpy(), torch.randn(n, dim, device=DEV, generator=g), groups=grp)
     idx.remove(list(range(0, 5000, 7)))
-    q = torch.randn(37, dim, device=DEV, generator=g)
-    qg = [i % 3 if i % 4 else -1 for i in range(37)] if groups else None
+    q = torch.randn(nq, dim, device=DEV, generator=g)
+    qg = [i % 3 if i % 4 else -1 for i in range(nq)] if groups else None
     idx.threshold_search = True
     v1, i1, d1 = idx.search(q, 250, q_groups=qg)
     assert idx.stats["threshold_searches"] == 1 and idx.stats["threshold_overflows"] == 0
@@ -448,6 +451,29 @@ def test_index_threshold_search_matches_full_scan(groups):
     torch.testing.assert_close(v1, v2)
     # same scores; ids may differ only among exactly tied scores
     assert (i1 == i2).float().mean() > 0.999
+
+
+@pytest.mark.parametrize("M", [5, 300])
+def test_score_candidates_exact_set(M):
+    """Every filtered score >= thr[m] is appended exactly once (both kernels; N not a multiple of 256)."""
+    N, K = 100_004, 256
+    A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
+    qg = torch.tensor([(-1 if i % 3 == 0 else i % 3) for i in range(M)], device=DEV, dtype=torch.int32)
+    full = ops.gemm_bt(A, B, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg)
+    thr = torch.quantile(full.clamp_min(-1.0), 0.995, dim=1).contiguous()
+    cap = 4096
+    cv, ci, cnt = ops.score_candidates(A, B, thr, cap, rg, qg)
+    assert int(cnt.max()) <= cap
+    for m in range(0, M, max(1, M // 23)):
+        k = int(cnt[m])
+        got = set(ci[m, :k].tolist())
+        exp = set((full[m] >= thr[m]).nonzero().flatten().tolist())
+        # scores within an fp32 rounding of the threshold may land on either side
+        near = set(((full[m] - thr[m]).abs() < 1e-5).nonzero().flatten().tolist())
+        assert (got ^ exp) <= near and len(got) == k
+        torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
 def test_index_threshold_search_overflow_falls_back():
