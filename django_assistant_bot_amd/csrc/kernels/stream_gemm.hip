@@ -341,6 +341,11 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {8, 1, 1, 4, 4, 2, true, 0, 6},  // 21: BN 96, 6 + 2 waves (qkv 6144 x S4 -> 256 WGs)
     {8, 1, 1, 3, 6, 1, true, 0, 7},  // 22: = 20, 1 loader wave, 6-stage weight ring
     {8, 1, 1, 3, 6, 2, true, 0, 6},  // 23: = 21, 6-stage weight ring
+    // M <= 256 (decode batches of 129..256): X stage 64 KB, two-stage X ring
+    {16, 1, 1, 2, 3, 1, true, 0, 8},  // 24: BN 128, 8 compute + 1 loader wave
+    {16, 1, 1, 2, 3, 2, true, 0, 4},  // 25: BN 64, 4 + 2 waves
+    {16, 2, 1, 2, 2, 2, true, 0, 4},  // 26: BN 128, RT 2, 2-stage weight ring
+    {16, 1, 2, 2, 4, 2, true, 0, 8},  // 27: BN 64, 2 k-groups x 4 row groups, 8 + 2 waves
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 

@@ -143,7 +143,15 @@ class LlamaModel:
     def _stream_ok(w: torch.Tensor) -> bool:
         return w.shape[0] % 128 == 0 and w.shape[1] % 128 == 0
 
+    # decode batches of 129..256 rows: 64-row tiles, 2 k-groups x 4 row groups (cfg 27; M = 256, cold
+    # weights: qkv 27.4 / o 18.6 / gate_up 98.7 / down 49.2 us against 32.4 / 25.8 / 104 / 55 for two
+    # M = 128 passes, profiles/decode_round2.md), so the step no longer falls back to the large-M GEMM
+    STREAM_CFG_M256 = 27
+    STREAM_MAX_M = 256
+
     def _stream_cfg(self, name: str, M: int, N: int) -> int:
+        if M > 128:
+            return self.STREAM_CFG_M256
         if M <= 64:
             return self.STREAM_CFG_M64
         cfg = self.STREAM_WIDE.get(name) if self._wide else None
@@ -201,7 +209,7 @@ class LlamaModel:
             s = self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
             out = ops.stream_gemm(x, ws, splits=s, cfg=cfg, nt=True)
             return ops.skinny_reduce(out) if (s > 1 and not allow_slabs) else out
-        if not sk or name not in self.skinny_for:
+        if not sk or name not in self.skinny_for or x.shape[0] > ops.SKINNY_MAX_M:
             return ops.gemm_bt(x, w) if x.is_cuda else ops.linear(x, w)
         s = self._splits(w)
         if s > 1 and not allow_slabs:
@@ -216,7 +224,8 @@ class LlamaModel:
         x = ops.embed_gather(ids, self.embed)
         # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
         # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
-        sk = self.use_skinny and meta.decode and T <= ops.SKINNY_MAX_M and x.is_cuda
+        max_m = self.STREAM_MAX_M if self.stream else ops.SKINNY_MAX_M
+        sk = self.use_skinny and meta.decode and T <= max_m and x.is_cuda
         residual = None
         for li, L in enumerate(self.layers):
             x, residual = self._layer(li, L, x, residual, meta, kv, sk)
@@ -247,7 +256,7 @@ class LlamaModel:
         if sk and self.interleaved_mlp and L.gate_up_ws is not None:
             act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU8, nt=True,
                                   cfg=self._stream_cfg("gate_up", T, L.gate_up_ws.shape[0]))
-        elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for:
+        elif sk and self.interleaved_mlp and "gate_up" in self.skinny_for and T <= ops.SKINNY_MAX_M:
             act = ops.skinny_gemm(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)
         elif self.interleaved_mlp and h.is_cuda:
             act = ops.gemm_bt(h, L.gate_up_w, epilogue=ops.EPI_SWIGLU)  # SwiGLU in the GEMM epilogue
@@ -320,14 +329,14 @@ class LlamaModel:
         return a
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
-        """[n, H] -> [n, V] logits (bf16; the sampler reads bf16 or fp32).  Up to 128 rows (decode
+        """[n, H] -> [n, V] logits (bf16; the sampler reads bf16 or fp32).  Up to 256 rows (decode
         steps, prefill last tokens) stream the shuffled LM-head copy through ``stream_gemm``;
         larger batches run the native MFMA GEMM."""
         if not h.is_cuda:
             return ops.linear(h, self.lm_head)
         n = h.shape[0]
-        if self.lm_head_ws is not None and n <= 128:
-            cfg = self.STREAM_CFG_M64 if n <= 64 else self.STREAM_CFG_M128
+        if self.lm_head_ws is not None and n <= self.STREAM_MAX_M:
+            cfg = self._stream_cfg("lm_head", n, self.lm_head.shape[0])
             return ops.stream_gemm(h, self.lm_head_ws, cfg=cfg, nt=True)
         if "lm_head" in self.skinny_for and n <= ops.SKINNY_MAX_M and self.lm_head.shape[0] % 64 == 0:
             return ops.skinny_gemm(h, self.lm_head)

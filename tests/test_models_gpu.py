@@ -34,7 +34,7 @@ def _run(model, cfg, prompts, device, dtype):
 
 
 @pytest.mark.parametrize("mode", ["stream", "skinny"])
-@pytest.mark.parametrize("B", [3, 20, 64, 128])
+@pytest.mark.parametrize("B", [3, 20, 64, 128, 200, 256])
 def test_decode_skinny_matches_library_path_and_reference(B, mode, monkeypatch):
     """Decode projections on the warp-specialised stream kernel (shuffled weights) or the split-K
     skinny kernel vs hipBLASLt vs the fp32 reference."""
