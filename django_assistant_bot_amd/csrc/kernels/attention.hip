@@ -21,6 +21,10 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <type_traits>
+
+#define DAB_ALWAYS_INLINE __attribute__((always_inline))
+
 namespace dab {
 
 constexpr float kNegInf = -__builtin_huge_valf();
@@ -272,6 +276,308 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_f
       *reinterpret_cast<u32x2*>(orow + 16 * t + 4 * g) = v;
     }
   }
+}
+
+// -----------------------------------------------------------------------------------------------
+// Llama prefill attention (D = 128, paged KV cache, GQA): 32x32x16 MFMA tiles.
+//
+// The 16x16 kernel above feeds every K / V fragment it reads from LDS to ONE MFMA for 16 queries;
+// at D = 128 that made its LDS traffic (reads + register-staged tile writes) larger than its MFMA
+// time.  Here a wave owns 32 queries and every fragment feeds a 32x32x16 MFMA (half the LDS bytes
+// per FLOP, cdna_hip_programming.md Appendix B "Fused attention prefill"):
+//   * workgroup = 4 waves x 32 queries of one (sequence, head); 64-key K / V tiles arrive by LDS-DMA
+//     (buffer_load ... lds, no VGPR round trip) into a 2-deep ring (64 KB: 2 workgroups per CU); the
+//     descriptor range stops at the last valid key, so rows past it are zeros (finite under the mask);
+//   * S^T = K Q^T (K rows as the A operand, Q^T fragments held in registers): lane (q, hi) ends with
+//     32 of the 64 scores of query q; row max / sum combine with the partner lane q ^ 32;
+//   * P^T is the B operand of O^T += V^T P^T straight from the S accumulators (cvt_pk only, the k
+//     order permuted to match), V^T fragments by ds_read_b64_tr_b16 (hardware transpose);
+//   * LDS rows are 256 B; the 16-B chunk c of row r lives at c ^ f(r), f(r) = (r & 3) << 2 | (r >> 2) & 3:
+//     conflict-free for the 16-row ds_read_b128 lane groups of the K reads AND for the 4-row x 64-B
+//     pieces of the transposed V reads (each row of a 4-row group lands in its own 64-B bank range).
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// f(integral_constant<I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ int f128(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// The 8 transposed V reads of one k-step (ds_read_b64_tr_b16) as ONE asm statement that also waits
+// for them: the intrinsic form makes hipcc drain every LDS-DMA still in flight (vmcnt(0)) before the
+// first transposed read, i.e. the next tile's copy that should stream in under this tile's P.V, and
+// separate asm reads would let hipcc copy an output register before the data has landed.  The
+// per-lane addresses are loop invariants; OFF (tile buffer, key block) is the instruction offset.
+template <int OFF>
+__device__ __forceinline__ void ds_tr16_x8(const unsigned (&a)[8], u32x2 (&r)[8]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %7, %15 offset:%16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "i"(OFF)
+      : "memory");
+}
+
+__device__ __forceinline__ unsigned lds_addr(const char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
+  constexpr int D = 128, KT = 64, QB = 128;
+  constexpr int TILE = KT * D * 2;  // 16 KB
+  constexpr int BUF = 2 * TILE;     // K | V
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  // same XCD-major (query block, head, sequence) walk as flash_fwd_kernel
+  const int nqb = gridDim.x;
+  const int nwg = nqb * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+  const int qb = sid % nqb;
+  const int h = (sid / nqb) % gridDim.y;
+  const int b = sid / (nqb * gridDim.y);
+  const int q_start = p.cu_q[b];
+  const int seqlen_q = p.cu_q[b + 1] - q_start;
+  const int q0 = qb * QB;
+  if (q0 >= seqlen_q) return;  // whole workgroup
+  const int kv_len = p.ctx_k[b];
+  const int hk = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, lq = lane & 31, hi = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int my_q = q0 + 32 * w + lq;
+  const bool q_valid = my_q < seqlen_q;
+  const int q_pos = kv_len - seqlen_q + my_q;
+  // highest key position any valid query of this wave attends to (wave-uniform)
+  const int w_last_q = min(q0 + 32 * w + 31, seqlen_q - 1);
+  const int w_kmax = CAUSAL ? kv_len - seqlen_q + w_last_q : kv_len - 1;
+  const bool w_any = q0 + 32 * w < seqlen_q;
+
+  // Q^T fragments (B operand): lane (q, hi) holds Q[q][16 s + 8 hi .. + 8], s = 0..7
+  bf16x8 qf[8];
+  {
+    const bf16* qrow = p.q + (size_t)(q_start + (q_valid ? my_q : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[st] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
+    }
+  }
+
+  int n_keys = kv_len;
+  if (CAUSAL) {
+    const int last_q = min(q0 + QB - 1, seqlen_q - 1);
+    n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
+  }
+  const int n_tiles = div_up(n_keys, KT);
+
+  // LDS-DMA staging (buffer_load ... lds): wave w issues K / V pieces i = 4 w .. 4 w + 3 (1 KB =
+  // 4 rows each); LDS slot (row 4 i + lane / 16, physical chunk lane % 16) receives logical chunk
+  // (lane % 16) ^ f(row).  The descriptor range ends at the last valid key: rows past it read zeros.
+  const int st_row = lane >> 4, st_pc = lane & 15;
+  // block ids of the first 128 tiles (8192 keys) in two registers per lane, read once; per tile a
+  // readlane (no memory round trip in the loop: a block-id load there exposed a full global-memory
+  // latency per tile, because the DMA request that needs it waits for it)
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  const int tpb = p.block_size / KT;  // tiles per cache block
+  const int bt_a = lane < n_tiles ? bt[lane / tpb] : 0;
+  const int bt_b = 64 + lane < n_tiles ? bt[(64 + lane) / tpb] : 0;
+  auto blk_of = [&](int t) {
+    if (t < 64) return __builtin_amdgcn_readlane(bt_a, t);
+    if (t < 128) return __builtin_amdgcn_readlane(bt_b, t - 64);
+    // past 8192 keys (volatile: never speculated; readfirstlane: the block id, and with it the
+    // DMA descriptor, stays wave-uniform, so hipcc builds no waterfall loop around the DMA)
+    return __builtin_amdgcn_readfirstlane(((volatile const int*)bt)[t / tpb]);
+  };
+  auto issue = [&](int t, int buf, int blk) {
+    const int k0 = t * KT;
+    const int nvalid = min(KT, kv_len - k0);
+    const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (k0 % p.block_size)) * D;
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)(p.k_cache + base), (short)0, nvalid * D * 2, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), (short)0, nvalid * D * 2, 0x00020000);
+    char* kdst = smem + buf * BUF;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * w + j;
+      const int row = 4 * i + st_row;
+      const unsigned off = (unsigned)(row * D + 8 * (st_pc ^ f128(row))) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(kdst + i * 1024), 16, off,
+                                               0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(kdst + TILE + i * 1024),
+                                               16, off, 0, 0, 0);
+    }
+  };
+
+  f32x16 o[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m_run = -1e30f, l_run = 0.f;  // running max in log2 units (scores x scale_log2)
+  const float sc = p.scale_log2;
+
+  // Loop-invariant LDS addresses (the tile buffer and the key block go in the instruction offset).
+  // K reads of k-step st: row lq (and 32 + lq: +8 KB), logical chunk 2 st + hi at (2 st + hi) ^ f(lq).
+  const unsigned smem0 = lds_addr(smem);
+  unsigned kadr[8];
+  {
+    const int fr = f128(lq);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) kadr[st] = smem0 + lq * 256 + 16 * ((2 * st + hi) ^ fr);
+  }
+  // Transposed V reads: 16-lane group G = lane / 16 covers d 32 db + 16 (G & 1) + (0..15); lane
+  // 4 qq + pp supplies row k + qq, d 4 pp .. 4 pp + 3.  For k-step (kb, ss) the first read's rows are
+  // 32 kb + 16 ss + 4 (G >> 1) + qq, whose f is (qq << 2) | (G >> 1) for every kb, ss (and
+  // | ((G >> 1) + 2) for the second read, 8 rows on), so only the offset changes with (kb, ss).
+  unsigned vadr[8];
+  {
+    const int G = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    const int r0 = 4 * (G >> 1) + qq;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int c = 4 * db + 2 * (G & 1) + (pp >> 1);
+      const int boff = 8 * (pp & 1);
+      vadr[2 * db] = smem0 + TILE + r0 * 256 + 16 * (c ^ f128(r0)) + boff;
+      vadr[2 * db + 1] = smem0 + TILE + (r0 + 8) * 256 + 16 * (c ^ f128(r0 + 8)) + boff;
+    }
+  }
+
+  // kadr / vadr point into the buffer of the tile being computed: toggled (xor BUF) after every tile
+  // (one body for both buffers: a body per buffer made hipcc move the 64 O registers at the join)
+  auto compute = [&](const int k0) DAB_ALWAYS_INLINE {
+    constexpr int B0 = 0;
+    // ---- S^T = K Q^T: K fragments in two batches of 8 reads
+    f32x16 s0, s1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s0[r] = s1[r] = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 ka[4], kb2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto* kp = (const __attribute__((address_space(3))) bf16x8*)(uintptr_t)(kadr[4 * half + i] + B0);
+        ka[i] = kp[0];
+        kb2[i] = kp[8192 / 16];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s0 = mfma32(ka[i], qf[4 * half + i], s0);
+        s1 = mfma32(kb2[i], qf[4 * half + i], s1);
+      }
+    }
+    // ---- online softmax on the raw scores (scale folded into the exponent's FMA): lane (q, hi)
+    // holds keys k0 + crow(r, hi) (s0) and + 32 (s1)
+    const bool need_mask = k0 + KT > kv_len || (CAUSAL && k0 + KT - 1 > kv_len - seqlen_q + q0);
+    if (need_mask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= kv_len || (CAUSAL && key > q_pos)) s0[r] = kNegInf;
+        if (key + 32 >= kv_len || (CAUSAL && key + 32 > q_pos)) s1[r] = kNegInf;
+      }
+    }
+    float mx = kNegInf;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx * sc);
+    // raw v_exp_f32 (exp2f adds a denormal-range fix-up around each one; results below 2^-126 are
+    // irrelevant next to the row maximum's 1)
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], sc, -m_new));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], sc, -m_new));
+      ls += s0[r] + s1[r];
+    }
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+    if (__any(alpha < 1.f)) {  // the running max moved for some query of the wave
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+    // ---- O^T += V^T P^T.  P^T needs no lane movement (cdna_hip_programming.md section 3, "an
+    // accumulator tile as the next MFMA's operand"): registers 8 ss .. 8 ss + 7 of S block kb,
+    // packed to bf16, are the B fragment of k-step (kb, ss), element j of lane half hi holding key
+    // 32 kb + 16 ss + 8 (j >> 2) + 4 hi + (j & 3); the V^T A fragment takes its elements from the
+    // same keys: two transposed reads of 4 keys at 32 kb + 16 ss + 4 hi (+ 8).
+    static_for<0, 4>([&](auto KS_) DAB_ALWAYS_INLINE {
+      constexpr int kb = decltype(KS_)::value >> 1, ss = decltype(KS_)::value & 1;
+      const f32x16& sv = kb ? s1 : s0;
+      u32x4 pu;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pu[e] = pack2bf(sv[8 * ss + 2 * e], sv[8 * ss + 2 * e + 1]);
+      const bf16x8 pf = __builtin_bit_cast(bf16x8, pu);
+      u32x2 tr[8];
+      ds_tr16_x8<B0 + kb * 8192 + ss * 4096>(vadr, tr);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        u32x4 u;
+        u[0] = tr[2 * db][0];
+        u[1] = tr[2 * db][1];
+        u[2] = tr[2 * db + 1][0];
+        u[3] = tr[2 * db + 1][1];
+        o[db] = mfma32(__builtin_bit_cast(bf16x8, u), pf, o[db]);
+      }
+      return true;
+    });
+  };
+
+  // One tile in flight: tile t + 1 is requested once tile t has landed and streams in under tile
+  // t's math.
+  if (n_tiles > 0) issue(0, 0, blk_of(0));
+  for (int t = 0; t < n_tiles; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < n_tiles) {
+      __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (t + 1) & 1 (tile t - 1)
+      const int blk = blk_of(t + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
+      issue(t + 1, buf ^ 1, blk);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile t
+    const int k0 = t * KT;
+    if (w_any && k0 <= w_kmax) compute(k0);  // else this wave's queries see no key of the tile
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      kadr[i] ^= BUF;
+      vadr[i] ^= BUF;
+    }
+  }
+
+  // ---- epilogue: O[q][d], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hi
+  float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+  if (!q_valid) return;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16* orow = p.out + (size_t)(q_start + my_q) * p.o_stride_tok + (size_t)h * p.o_stride_head;
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      u32x2 v;
+      v[0] = pack2bf(o[db][4 * rg] * inv, o[db][4 * rg + 1] * inv);
+      v[1] = pack2bf(o[db][4 * rg + 2] * inv, o[db][4 * rg + 3] * inv);
+      *reinterpret_cast<u32x2*>(orow + 32 * db + 8 * rg + 4 * hi) = v;
+    }
 }
 
 // -----------------------------------------------------------------------------------------------
@@ -573,6 +879,14 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     if (v == nullptr) return -1;
     return (v[0] == 'w' && v[1] == '8') ? 1 : (v[0] == 'w' && v[1] == '4') ? 2 : (v[0] == 'q') ? 0 : -1;
   }();
+  // Llama prefill (D = 128 over the paged cache): the 32x32 kernel; DAB_FLASH_VARIANT=w8 (or any
+  // explicit variant) keeps the 16x16 kernels for A/B runs
+  if (D == 128 && paged && variant < 0 && block_size % 64 == 0) {
+    dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
+    if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
+    else hipLaunchKernelGGL((flash_d128_kernel<false>), g32, dim3(256), 0, s, prm);
+    return hipGetLastError();
+  }
   const int var = variant >= 0 ? variant : (D == 128 ? 1 : 2);
   const bool wide = max_seqlen_q > 64 && var != 2;
   const int qb = wide ? 128 : 64;

@@ -160,15 +160,26 @@ def _paged_setup(ctx, Hkv, D, bs, nb):
     return kc, vc, bt.to(DEV)
 
 
-def test_flash_paged_prefill():
-    ctx, qlen = [100, 200, 64, 1000], [30, 64, 64, 257]
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_paged_prefill(causal):
+    """D = 128 paged prefill (the 32x32-MFMA kernel): ragged query / context lengths, both masks;
+    cache slots past each context hold NaN (they must not reach the output)."""
+    ctx, qlen = [100, 200, 64, 1000, 33], [30, 64, 64, 257, 33]
     Hq, Hkv, D, bs = 8, 2, 128, 64
     kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 64)
+    btc = bt.cpu()
+    for i, c in enumerate(ctx):  # poison the unused tail of each sequence's last block
+        if c % bs:
+            blk = int(btc[i, c // bs])
+            kc[blk, :, c % bs:] = float("nan")
+            vc[blk, :, c % bs:] = float("nan")
     q = bf(sum(qlen), Hq, D)
     cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device=DEV)
     ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
-    out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(qlen), causal=True)
-    exp = ref.flash_attention_paged(q, kc, vc, bt, cu, ctxt, True, 1 / math.sqrt(D))
+    out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(qlen), causal=causal)
+    kc0, vc0 = kc.nan_to_num(0.0), vc.nan_to_num(0.0)
+    exp = ref.flash_attention_paged(q, kc0, vc0, bt, cu, ctxt, causal, 1 / math.sqrt(D))
+    assert torch.isfinite(out.float()).all()
     close(out, exp)
 
 
@@ -515,7 +526,8 @@ def test_cu_masked_stream_runs_kernels():
         nat.destroy_stream(h)
 
 
-@pytest.mark.parametrize("ctx,qlen", [([4096, 6000], [512, 1024]), ([8192], [8192]), ([8192, 5000], [1, 700])])
+@pytest.mark.parametrize("ctx,qlen", [([4096, 6000], [512, 1024]), ([8192], [8192]), ([8192, 5000], [1, 700]),
+                                      ([9000], [300])])
 def test_flash_paged_prefill_long_context_llama_heads(ctx, qlen):
     """Llama-3-8B head layout (Hq 32, Hkv 8, D 128) at 4K-8K context: chunked prefill (q = the last
     qlen positions of ctx) and a full 8K prompt, against the fp32 reference."""

@@ -169,3 +169,21 @@ def test_random_tp_shards_replicate_embedding_and_lm_head():
     assert not torch.equal(a["l0.qkv_w"], b["l0.qkv_w"])
     full = random_decoder_weights(cfg, dtype=torch.float32, seed=4)
     assert torch.equal(shard_decoder_weights(full, cfg, 1, 2)["lm_head"], full["lm_head"])
+
+
+def test_gate_up_regroup_and_swiglu8_reference():
+    """The decode copy of gate_up is regrouped from 16-row to 8-row [gate | up] pairs (any 16-row
+    multiple then tiles it); the EPI_SWIGLU8 reference equals SiLU(gate) * up of the plain layout."""
+    from django_assistant_bot_amd import ops
+    from django_assistant_bot_amd.ops import reference as ref
+
+    F, H = 112, 64
+    g, u, x = torch.randn(F, H), torch.randn(F, H), torch.randn(5, H)
+    w16 = ops.interleave_gate_up(g, u)
+    w8 = ops.regroup_gate_up(w16, 16, 8)
+    assert torch.equal(w8, ops.interleave_gate_up(g, u, 8))
+    exp = torch.nn.functional.silu(x @ g.t()) * (x @ u.t())
+    got8 = ref.gemm_bt(x, w8, epilogue=ops.EPI_SWIGLU8, out_f32=True)
+    got16 = ref.gemm_bt(x, w16, epilogue=ops.EPI_SWIGLU, out_f32=True)
+    torch.testing.assert_close(got8, exp, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(got16, exp, atol=1e-4, rtol=1e-4)
