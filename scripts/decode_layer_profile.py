@@ -16,6 +16,12 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from step_breakdown import short  # noqa: E402
 
 
+# Llama prefill attention launches (the 32x32 D=128 kernel, or the 16x16 one it replaced); the
+# encoder's D=64 flash launches belong to the query-embedding step, not to a prefill
+def _is_prefill_attn(name: str) -> bool:
+    return "flash_d128" in name or "flash_fwd_kernel<128" in name
+
+
 def main():
     d, prefix = sys.argv[1], sys.argv[2]
     nsteps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 20
@@ -27,7 +33,7 @@ def main():
     rows.sort()
     starts = [i for i, r in enumerate(rows) if "embed_gather_kernel" in r[2]] + [len(rows)]
     steps = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
-    dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any("flash_fwd" in n for _, _, n in s)]
+    dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any(_is_prefill_attn(n) for _, _, n in s)]
     dec = dec[-nsteps:]
     slots = defaultdict(lambda: {"dur": [], "gap": [], "name": ""})
     spans = []

@@ -8,6 +8,12 @@ import os
 import sys
 
 
+# Llama prefill attention launches (the 32x32 D=128 kernel, or the 16x16 one it replaced); the
+# encoder's D=64 flash launches belong to the query-embedding step, not to a prefill
+def _is_prefill_attn(name: str) -> bool:
+    return "flash_d128" in name or "flash_fwd_kernel<128" in name
+
+
 def main():
     d, prefix, out = sys.argv[1], sys.argv[2], sys.argv[3]
     stats = list(csv.DictReader(open(os.path.join(d, f"{prefix}_kernel_stats.csv"))))
@@ -24,7 +30,7 @@ def main():
         named.sort()
         # decode window: after the last prefill attention kernel, from the first to the last paged
         # decode kernel -> GPU busy share and inter-kernel gaps inside the graph replays
-        last_pf = max((i for i, k in enumerate(named) if "flash_fwd" in k[2]), default=-1)
+        last_pf = max((i for i, k in enumerate(named) if _is_prefill_attn(k[2])), default=-1)
         dec = [k for k in named[last_pf + 1:]]
         di = [i for i, k in enumerate(dec) if "paged_decode" in k[2]]
         if di:

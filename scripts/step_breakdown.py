@@ -13,6 +13,12 @@ import sys
 from collections import defaultdict
 
 
+# Llama prefill attention launches (the 32x32 D=128 kernel, or the 16x16 one it replaced); the
+# encoder's D=64 flash launches belong to the query-embedding step, not to a prefill
+def _is_prefill_attn(name: str) -> bool:
+    return "flash_d128" in name or "flash_fwd_kernel<128" in name
+
+
 def short(name: str) -> str:
     name = name.replace("void ", "")
     if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
@@ -50,8 +56,8 @@ def main():
     starts = [i for i, r in enumerate(rows) if "embed_gather_kernel" in r[2]] + [len(rows)]
     steps = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
     lines = [f"# per-step kernel breakdown: {prefix}", ""]
-    dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any("flash_fwd" in n for _, _, n in s)]
-    pre = [s for s in steps if any("flash_fwd" in n for _, _, n in s)]
+    dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any(_is_prefill_attn(n) for _, _, n in s)]
+    pre = [s for s in steps if any(_is_prefill_attn(n) for _, _, n in s)]
     if pre:
         big = max(pre, key=lambda s: s[-1][1] - s[0][0])
         lines += window_table(big, "largest prefill step")
