@@ -41,12 +41,15 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
     if device_type == "cuda":
+        # more ranks than GPUs (a multi-rank rehearsal on a 1-GPU box, with DAB_DIST_BACKEND=gloo:
+        # RCCL refuses two ranks on one device) wrap around; one rank per GPU otherwise
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
     if backend is None:
-        backend = "nccl" if device_type == "cuda" else "gloo"
+        backend = os.environ.get("DAB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {}
