@@ -603,7 +603,12 @@ struct DecodeParams {
   float scale_log2;
 };
 
-template <int D, bool KV_NT>
+// DMA (D = 128): each wave streams its 32-key K / V sub-tiles straight into its LDS slot by LDS-DMA
+// (buffer_load ... lds, non-temporal: MI355X_MICROARCH.md rows ldsdma-fill / nt-weights put the
+// LDS-DMA stream at 6.5-6.8 TB/s chip-wide against 5.7-5.8 for register gathers) instead of through
+// a register double buffer + ds_write; one slot per wave, the 8 waves of a CU's two workgroups keep
+// ~128 KB in flight.  The next sub-tile's block id is fetched under the current sub-tile's DMA.
+template <int D, bool KV_NT, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, int total_items) {
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
@@ -746,16 +751,51 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
       __builtin_amdgcn_wave_barrier();
     };
     const int kw = k_begin + w * KT;
-    load_sub(kA, vA, kw);
-    load_sub(kB, vB, kw + 4 * KT);
-    for (int k0 = kw; k0 < k_end; k0 += 8 * KT) {
-      stage(kA, vA);
-      load_sub(kA, vA, k0 + 8 * KT);
-      compute(k0);
-      if (k0 + 4 * KT >= k_end) break;
-      stage(kB, vB);
-      load_sub(kB, vB, k0 + 12 * KT);
-      compute(k0 + 4 * KT);
+    if constexpr (DMA) {
+      static_assert(D == 128, "DMA staging assumes 256-B rows (4 rows per 1 KB piece)");
+      // LDS slot (row 4 i + lane / 16, physical chunk lane % 16) of piece i holds logical chunk
+      // (lane % 16) ^ (2 row & 15): the swz<128> image compute() reads
+      const int drow = lane >> 4;
+      auto blk_at = [&](int k0) {
+        return p.block_tables[(size_t)b * p.max_blocks + min(k0, k_last) / p.block_size];
+      };
+      auto dma = [&](int k0, int blk) {
+        const int kc = min(k0, k_last);
+        const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (kc % p.block_size)) * D;
+        const int bytes = k0 > k_last ? 0 : min(KT, k_end - k0) * D * 2;
+        const auto kd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.k_cache + base), 0, bytes, 0x00020000);
+        const auto vd = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), 0, bytes, 0x00020000);
+#pragma unroll
+        for (int i = 0; i < KT / 4; ++i) {
+          const int row = 4 * i + drow;
+          const unsigned off = (unsigned)(row * 256 + 16 * ((lane & 15) ^ ((2 * row) & 15)));
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(kd, (__attribute__((address_space(3))) void*)(ks + i * 1024), 16, off,
+                                                   0, 0, KV_NT ? 2 : 0);
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(vd, (__attribute__((address_space(3))) void*)(vs + i * 1024), 16, off,
+                                                   0, 0, KV_NT ? 2 : 0);
+        }
+      };
+      int blk = __builtin_amdgcn_readfirstlane(blk_at(kw));
+      for (int k0 = kw; k0 < k_end; k0 += 4 * KT) {
+        dma(k0, blk);
+        blk = blk_at(k0 + 4 * KT);  // in flight under this sub-tile's copy and math
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // this sub-tile's 16 pieces landed
+        compute(k0);
+        blk = __builtin_amdgcn_readfirstlane(blk);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      load_sub(kA, vA, kw);
+      load_sub(kB, vB, kw + 4 * KT);
+      for (int k0 = kw; k0 < k_end; k0 += 8 * KT) {
+        stage(kA, vA);
+        load_sub(kA, vA, k0 + 8 * KT);
+        compute(k0);
+        if (k0 + 4 * KT >= k_end) break;
+        stage(kB, vB);
+        load_sub(kB, vB, k0 + 12 * KT);
+        compute(k0 + 4 * KT);
+      }
     }
 
     // combine the 4 waves of the workgroup through LDS
@@ -965,8 +1005,18 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
     return v == nullptr || v[0] != '0';
   }();
   if (D == 128) {
-    if (kv_nt) hipLaunchKernelGGL((paged_decode_kernel<128, true>), grid, dim3(256), 0, s, prm, total_items);
-    else hipLaunchKernelGGL((paged_decode_kernel<128, false>), grid, dim3(256), 0, s, prm, total_items);
+    static const bool dma = [] {
+      const char* v = getenv("DAB_DECODE_DMA");
+      return v == nullptr || v[0] != '0';
+    }();
+    if (dma && block_size % 32 == 0) {
+      if (kv_nt) hipLaunchKernelGGL((paged_decode_kernel<128, true, true>), grid, dim3(256), 0, s, prm, total_items);
+      else hipLaunchKernelGGL((paged_decode_kernel<128, false, true>), grid, dim3(256), 0, s, prm, total_items);
+    } else if (kv_nt) {
+      hipLaunchKernelGGL((paged_decode_kernel<128, true>), grid, dim3(256), 0, s, prm, total_items);
+    } else {
+      hipLaunchKernelGGL((paged_decode_kernel<128, false>), grid, dim3(256), 0, s, prm, total_items);
+    }
   } else if (D == 64) {
     if (kv_nt) hipLaunchKernelGGL((paged_decode_kernel<64, true>), grid, dim3(256), 0, s, prm, total_items);
     else hipLaunchKernelGGL((paged_decode_kernel<64, false>), grid, dim3(256), 0, s, prm, total_items);
