@@ -24,6 +24,11 @@ def main():
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--copies", type=int, default=3)
     ap.add_argument("--iters", type=int, default=12)
+    ap.add_argument("--pool-blocks", type=int, default=0,
+                    help="cache blocks per copy (0: exactly the live ones); a pool the size of the "
+                         "engine's (~24k blocks = 3 GB per layer's K) spreads the live blocks over it")
+    ap.add_argument("--spread", choices=("random", "compact"), default="random",
+                    help="live blocks drawn at random from the pool, or the lowest ids in order")
     a = ap.parse_args()
     Hq, Hkv, D, bs, B = 32, 8, 128, 64, a.batch
     g = torch.Generator().manual_seed(0)
@@ -34,11 +39,12 @@ def main():
             ctx_h = torch.full((B,), 1200)
         nbs = [math.ceil(int(c) / bs) for c in ctx_h]
         nb = sum(nbs)
+        pool = max(nb, a.pool_blocks)
         caches = []
         for _ in range(a.copies):
-            kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
-            caches.append((kc, torch.randn_like(kc)))
-        perm = torch.randperm(nb, generator=g)
+            kc = torch.empty(pool, Hkv, bs, D, device="cuda", dtype=torch.bfloat16).normal_()
+            caches.append((kc, torch.empty_like(kc).normal_()))
+        perm = torch.randperm(pool, generator=g)[:nb] if a.spread == "random" else torch.arange(nb)
         bt = torch.zeros((B, max(nbs)), dtype=torch.int32)
         o = 0
         for i, n in enumerate(nbs):
@@ -50,7 +56,7 @@ def main():
         longest = torch.argsort(ctx_h, descending=True).to(torch.int32).cuda()
         byts = 2.0 * float(ctx_h.sum()) * Hkv * D * 2
         res = {"op": "paged-decode", "ctx": dist_name, "B": B, "mean_ctx": int(ctx_h.float().mean()),
-               "GB": round(byts / 1e9, 3)}
+               "GB": round(byts / 1e9, 3), "pool_blocks": pool, "spread": a.spread}
         ref = None
         for part in (2048, 1024, 512):
             ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / part), "cuda")

@@ -1,6 +1,7 @@
 #include "kv_manager.h"
 
 #include <algorithm>
+#include <functional>
 #include <iterator>
 #include <stdexcept>
 
@@ -10,7 +11,8 @@ KVBlockManager::KVBlockManager(int num_blocks, int block_size, bool prefix_cache
     : num_blocks_(num_blocks), block_size_(block_size), prefix_cache_(prefix_cache) {
   if (num_blocks <= 0 || block_size <= 0) throw std::invalid_argument("num_blocks and block_size must be > 0");
   free_.reserve(num_blocks);
-  for (int b = num_blocks - 1; b >= 0; --b) free_.push_back(b);
+  for (int b = 0; b < num_blocks; ++b) free_.push_back(b);  // ascending = a valid min-heap
+  lru_cap_ = std::max(64, num_blocks / 4);
   ref_.assign(num_blocks, 0);
   block_hash_.assign(num_blocks, 0);
   lru_pos_.resize(num_blocks);
@@ -29,6 +31,7 @@ uint64_t KVBlockManager::chain_hash(uint64_t parent, const int32_t* toks, int n)
 int32_t KVBlockManager::alloc_block() {
   int32_t b;
   if (!free_.empty()) {
+    std::pop_heap(free_.begin(), free_.end(), std::greater<int32_t>());
     b = free_.back();
     free_.pop_back();
   } else if (!lru_.empty()) {
@@ -50,10 +53,23 @@ void KVBlockManager::release_block(int32_t b) {
     lru_.push_back(b);
     lru_pos_[b] = std::prev(lru_.end());
     in_lru_[b] = 1;
+    if ((int)lru_.size() > lru_cap_) {  // the oldest cached prefix block goes back to the free heap
+      const int32_t e = lru_.front();
+      lru_.pop_front();
+      in_lru_[e] = 0;
+      cached_.erase(block_hash_[e]);
+      block_hash_[e] = 0;
+      push_free(e);
+    }
   } else {
     block_hash_[b] = 0;
-    free_.push_back(b);
+    push_free(b);
   }
+}
+
+void KVBlockManager::push_free(int32_t b) {
+  free_.push_back(b);
+  std::push_heap(free_.begin(), free_.end(), std::greater<int32_t>());
 }
 
 int KVBlockManager::add_sequence(int64_t seq_id, const std::vector<int32_t>& tokens, int reserve) {

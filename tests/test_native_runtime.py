@@ -102,3 +102,22 @@ def test_merge_topk(n):
     ids = np.array([[1, 2, 3], [4, 5, -1]], dtype=np.int64)
     v, i = n.merge_topk(vals, ids, 4)
     assert list(i) == [1, 4, 5, 2] and np.allclose(v, [0.9, 0.8, 0.7, 0.5])
+
+
+def test_kv_manager_packs_blocks_low_and_caps_cached_prefixes(n):
+    """Fresh blocks come lowest id first (a batch's live blocks stay packed at the low end of the
+    pool) and at most max(64, pool / 4) unreferenced prefix blocks are kept cached."""
+    m = n.KVBlockManager(1024, 4, True)
+    for s in range(100):  # 100 sequences x 3 registrable blocks, all freed -> 300 cached > cap 256
+        m.add_sequence(s, [s * 1000 + i for i in range(13)], 0)
+        m.commit_prefix(s, 13)
+    for s in range(100):
+        m.free_sequence(s)
+    assert m.num_free_blocks() == 1024
+    # the 44 oldest cached blocks went back to the free heap; a new sequence packs into the lowest
+    # free ids (not the LRU tail of the pool)
+    m.add_sequence(500, list(range(7000, 7040)), 0)
+    got = list(m.blocks(500))
+    assert got == sorted(got) and got[0] < 400 and len(got) == 10
+    # the most recently cached prefixes still hit
+    assert m.add_sequence(501, [99 * 1000 + i for i in range(13)], 0) == 12
