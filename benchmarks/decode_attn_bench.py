@@ -27,6 +27,10 @@ def main():
     ap.add_argument("--pool-blocks", type=int, default=0,
                     help="cache blocks per copy (0: exactly the live ones); a pool the size of the "
                          "engine's (~24k blocks = 3 GB per layer's K) spreads the live blocks over it")
+    ap.add_argument("--between", type=int, default=0,
+                    help="stream a gate_up-sized decode GEMM (235 MB of weights, cold copies) between "
+                         "attention launches, as the layer does (0: attention back to back)")
+    ap.add_argument("--between-rows", type=int, default=28672, help="weight rows of that GEMM (K 4096)")
     ap.add_argument("--spread", choices=("random", "compact"), default="random",
                     help="live blocks drawn at random from the pool, or the lowest ids in order")
     a = ap.parse_args()
@@ -58,13 +62,18 @@ def main():
         res = {"op": "paged-decode", "ctx": dist_name, "B": B, "mean_ctx": int(ctx_h.float().mean()),
                "GB": round(byts / 1e9, 3), "pool_blocks": pool, "spread": a.spread}
         ref = None
+        gemm_w = [ops.shuffle_weights(torch.randn(a.between_rows, 4096, device="cuda").to(torch.bfloat16))
+                  for _ in range(2)] if a.between else []
+        gemm_x = torch.randn(B, 4096, device="cuda").to(torch.bfloat16)
         for part in (2048, 1024, 512):
             ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / part), "cuda")
             for oname, order in (("batch", None), ("longest", longest)):
                 outs = []
 
                 def run():
-                    for kc, vc in caches:
+                    for i, (kc, vc) in enumerate(caches):
+                        if gemm_w:
+                            ops.stream_gemm(gemm_x, gemm_w[i % 2], cfg=10, nt=True)
                         outs.append(ops.paged_decode(q, kc, vc, bt, ctx, part, ws, order=order))
                 run()
                 torch.cuda.synchronize()
