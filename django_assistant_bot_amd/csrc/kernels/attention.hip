@@ -963,24 +963,6 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   return hipGetLastError();
 }
 
-// Experimental (DAB_KV_TOUCH=1): one dword of every head slice of every live cache block is read
-// before the decode attention launch, so the attention does not meet the block's address
-// translation cold (probe for the ~10 % the attention loses right after a large weight stream).
-__global__ __launch_bounds__(256) void kv_touch_kernel(const bf16* __restrict__ k_cache, const bf16* __restrict__ v_cache,
-                                                       const int* __restrict__ block_tables, int max_blocks,
-                                                       const int* __restrict__ ctx_lens, int Hkv, int block_size, int D,
-                                                       int* sink) {
-  const int b = blockIdx.x;
-  const int nblk = (ctx_lens[b] + block_size - 1) / block_size;
-  unsigned acc = 0;
-  for (int e = threadIdx.x; e < nblk * Hkv; e += blockDim.x) {
-    const int j = e / Hkv, h = e % Hkv;
-    const size_t off = (((size_t)block_tables[(size_t)b * max_blocks + j] * Hkv + h) * block_size) * D;
-    acc += k_cache[off] + v_cache[off];
-  }
-  if (acc == 0x7fffffffu) sink[0] = (int)acc;  // never true in practice; keeps the loads
-}
-
 // The workgroups of a launch are dispatched in blockIdx order as CU slots free up; at RAG batch sizes
 // every CU runs about two (sequence, kv head) items one after the other, so with sequences of mixed
 // length the launch ends when the unluckiest slot has run two long ones.  ``order`` (optional, a
@@ -1013,13 +995,6 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_size = part_size;
   prm.max_parts = max_parts;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  static const bool touch = [] {
-    const char* v = getenv("DAB_KV_TOUCH");
-    return v != nullptr && v[0] == '1';
-  }();
-  if (touch && counters)
-    hipLaunchKernelGGL(kv_touch_kernel, dim3(batch), dim3(256), 0, s, (const bf16*)k_cache, (const bf16*)v_cache,
-                       block_tables, max_blocks, ctx_lens, Hkv, block_size, D, counters + batch * Hkv);
   const int total_items = max_parts * Hkv * batch;
   dim3 grid(total_items < 2048 ? total_items : 2048);
   // K/V are read exactly once per step: non-temporal loads (aux = 2).  In the Llama-3-8B decode step
