@@ -73,7 +73,7 @@ def main():
                 def run():
                     for i, (kc, vc) in enumerate(caches):
                         if gemm_w:
-                            ops.stream_gemm(gemm_x, gemm_w[i % 2], cfg=10, nt=True)
+                            ops.stream_gemm(gemm_x, gemm_w[i % 2], cfg=10, nt=os.environ.get("BETWEEN_NT", "1") == "1")
                         outs.append(ops.paged_decode(q, kc, vc, bt, ctx, part, ws, order=order))
                 run()
                 torch.cuda.synchronize()
