@@ -282,6 +282,16 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   }();
   if (use256 && M >= 128 && K % 128 == 0)
     return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
+  // 32..64 queries: the index streams through the decode GEMM's weight ring (64 queries x 10M rows:
+  // 5.88 -> 5.05 ms).  Below 32 it loses (1 query: 4.22 vs 3.70 ms): every 64-row workgroup re-stages
+  // the padded 64-row query block, as many L2 bytes as the index rows it scans.
+  // DAB_CAND_STREAM=0 keeps the 128x128 kernel.
+  static const bool use_stream = [] {
+    const char* v = getenv("DAB_CAND_STREAM");
+    return v == nullptr || v[0] != '0';
+  }();
+  if (use_stream && M >= 32 && M <= 64 && K % 128 == 0)
+    return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   GemmParams p{};
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;

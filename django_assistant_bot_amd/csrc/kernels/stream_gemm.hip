@@ -41,11 +41,20 @@ struct StreamParams {
   const bf16* residual;
   long ldr;
   int M, N, K, S, kc;
-  int epi;       // 0 none, 2 swiglu (16-row gate | up groups), 4 swiglu (8-row groups)
+  int epi;       // 0 none, 2 swiglu (16-row gate | up groups), 4 swiglu (8-row groups), 8 candidates
   int slab_wt;   // split-K slabs stored write-through (sc1)
+  // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
+  // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
+  const int* row_group;  // [N] (<0 = deleted) or null
+  const int* q_group;    // [M] (<0 = any) or null
+  const float* thr;      // [M]
+  int* cnt;              // [M]
+  float* cand_val;       // [M, cap]
+  int* cand_idx;         // [M, cap]
+  int cap;
 };
 
-constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2, ST_EPI_SWIGLU8 = 4;
+constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2, ST_EPI_SWIGLU8 = 4, ST_EPI_CAND = 8;
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 constexpr int clcm(int a, int b) { return a / cgcd(a, b) * b; }
@@ -95,7 +104,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   static_assert(NWC % KG == 0, "k groups");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
-  const int tiles = p.N / BN;
+  const int tiles = (p.N + BN - 1) / BN;  // partial last tile: candidates only (rows >= N read zeros)
   const int nwg = tiles * p.S;
   const int bid = blockIdx.x;
   const int xcd = bid % 8, q8 = nwg / 8, r8 = nwg % 8;
@@ -150,8 +159,8 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   } else {
     // ------------------------------------------------------------------ compute waves
     const int rg = w / KG, kg = w % KG;
-    const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)n0 * p.ldw), 0, (int)(BN * p.ldw * 2),
-                                                        0x00020000);
+    const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)n0 * p.ldw), 0,
+                                                        (int)(min(BN, p.N - n0) * p.ldw * 2), 0x00020000);
     // row-major W: lane (li, g) reads row li, k 8g..8g+7 of a 16 x 32 chunk (16 rows x 64 B per load);
     // SHUF (shuffle_weights layout [N/16][K/32][64 lanes][8]): every load is 1 KB contiguous
     const int w_voff = SHUF ? lane * 16 + ((k_begin + kg * KW) / 32) * 1024
@@ -270,6 +279,28 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     }
     return;
   }
+  if (p.epi == ST_EPI_CAND) {
+    for (int e = tid; e < MP * (BN / 4); e += NT) {
+      const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
+      if (m >= p.M) continue;
+      const f32x4 v = tile4(m, c4);
+      const float t = p.thr[m];
+      const int qg = p.q_group ? p.q_group[m] : -1;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n0 + c4 + j;
+        if (n >= p.N || v[j] < t) continue;
+        const int rg = p.row_group ? p.row_group[n] : 0;
+        if (rg < 0 || (qg >= 0 && rg != qg)) continue;
+        const int slot = atomicAdd(p.cnt + m, 1);
+        if (slot < p.cap) {
+          p.cand_val[(size_t)m * p.cap + slot] = v[j];
+          p.cand_idx[(size_t)m * p.cap + slot] = n;
+        }
+      }
+    }
+    return;
+  }
   bf16* out = (bf16*)p.out;
   if (p.epi == ST_EPI_SWIGLU || p.epi == ST_EPI_SWIGLU8) {
     // hg-row groups: rows [2 hg i, 2 hg i + hg) gate, [2 hg i + hg, 2 hg (i + 1)) up -> output
@@ -352,7 +383,8 @@ constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 template <int C>
 static void launch_cfg(const StreamParams& p, hipStream_t s, bool nt) {
   constexpr StreamCfg c = kStreamCfgs[C];
-  const dim3 grid((p.N / (16 * c.rt * (c.nwc / c.kg))) * p.S), block(64 * (c.nwc + c.nl));
+  const int bn = 16 * c.rt * (c.nwc / c.kg);
+  const dim3 grid(((p.N + bn - 1) / bn) * p.S), block(64 * (c.nwc + c.nl));
   if (nt)
     hipLaunchKernelGGL((stream_gemm_kernel<c.mt, c.rt, c.kg, 128, c.nb, c.nwin, c.nl, c.shuf, true, c.abl, c.nwc>), grid,
                        block, 0, s, p);
@@ -412,6 +444,38 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   }();
   p.slab_wt = slab_wt;
   launch_any(cfg, p, s, nt_weights != 0);
+  return hipGetLastError();
+}
+
+// Index threshold candidates for small query batches (M <= 64): the index rows stream through the
+// weight ring like decode weights (row-major, 16 rows x 64 B per load), the queries sit in LDS.
+// At M = 1..64 the MFMA tiles of the GEMM kernels are mostly padding and the scan is HBM-bound.
+int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
+                            const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                            hipStream_t s) {
+  constexpr int KS = 128, CFG = 7;  // M <= 64, BN 64, 4 loader waves, row-major weights
+  if (M <= 0 || N <= 0) return 0;
+  if (M > stream_gemm_max_m(CFG) || K % KS || ldx % 8 || ldw % 8 || cap <= 0) return hipErrorInvalidValue;
+  if ((long)stream_gemm_bn(CFG) * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  StreamParams p{};
+  p.X = (const bf16*)X;
+  p.ldx = ldx;
+  p.W = (const bf16*)W;
+  p.ldw = ldw;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.S = 1;
+  p.kc = K;
+  p.epi = ST_EPI_CAND;
+  p.row_group = row_group;
+  p.q_group = q_group;
+  p.thr = thr;
+  p.cnt = cnt;
+  p.cand_val = cand_val;
+  p.cand_idx = cand_idx;
+  p.cap = cap;
+  launch_cfg<CFG>(p, s, true);
   return hipGetLastError();
 }
 

@@ -439,11 +439,11 @@ def test_sampling_distribution(fast):
     assert int(tok.max()) <= 1
 
 
-@pytest.mark.parametrize("nq", [37, 300])
+@pytest.mark.parametrize("nq", [7, 37, 300])
 @pytest.mark.parametrize("groups", [False, True])
 def test_index_threshold_search_matches_full_scan(groups, nq):
-    """37 queries: the 128x128 candidate kernel; 300: the persistent gemm256 G_CAND epilogue
-    (600k rows: the last 256-row tile is partial)."""
+    """7 queries: the 128x128 candidate kernel; 37: the streaming one; 300: the persistent gemm256
+    G_CAND epilogue (600k rows: the last 256-row tile is partial)."""
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
     n, dim = 600_000, 128
@@ -464,9 +464,10 @@ def test_index_threshold_search_matches_full_scan(groups, nq):
     assert (i1 == i2).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("M", [5, 300])
+@pytest.mark.parametrize("M", [5, 40, 300])
 def test_score_candidates_exact_set(M):
-    """Every filtered score >= thr[m] is appended exactly once (both kernels; N not a multiple of 256)."""
+    """Every filtered score >= thr[m] is appended exactly once (the 128x128, streaming and gemm256
+    candidate kernels; N not a multiple of 64 / 256)."""
     N, K = 100_004, 256
     A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
     B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
