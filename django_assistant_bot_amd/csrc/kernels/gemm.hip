@@ -290,6 +290,8 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
     const char* v = getenv("DAB_CAND_STREAM");
     return v == nullptr || v[0] != '0';
   }();
+  if (use_stream && M <= 16 && K % 256 == 0 && K <= 1024)
+    return index_scan_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   if (use_stream && M >= 32 && M <= 64 && K % 128 == 0)
     return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   GemmParams p{};

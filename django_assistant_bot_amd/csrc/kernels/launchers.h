@@ -71,6 +71,10 @@ int skinny_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, 
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
 int stream_gemm_bn(int cfg);
+// index_scan.hip: persistent scan for 1..16 queries (queries staged in LDS once), K % 256 == 0, K <= 1024
+int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
+                          const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                          hipStream_t s);
 int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                             const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                             hipStream_t s);

@@ -439,14 +439,14 @@ def test_sampling_distribution(fast):
     assert int(tok.max()) <= 1
 
 
-@pytest.mark.parametrize("nq", [7, 37, 300])
+@pytest.mark.parametrize("nq", [1, 7, 20, 37, 300])
 @pytest.mark.parametrize("groups", [False, True])
 def test_index_threshold_search_matches_full_scan(groups, nq):
-    """7 queries: the 128x128 candidate kernel; 37: the streaming one; 300: the persistent gemm256
-    G_CAND epilogue (600k rows: the last 256-row tile is partial)."""
+    """1 / 7 queries: the persistent LDS-query scan (index_scan.hip); 20: the 128x128 candidate
+    kernel; 37: the weight-ring one; 300: the gemm256 G_CAND epilogue (600k rows: partial last tiles)."""
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
-    n, dim = 600_000, 128
+    n, dim = 600_000, 256
     g = torch.Generator(device=DEV).manual_seed(5)
     idx = VectorIndex(dim, DEV, capacity=n)
     grp = (torch.arange(n) % 3).numpy().astype("int32") if groups else None
@@ -464,7 +464,7 @@ def test_index_threshold_search_matches_full_scan(groups, nq):
     assert (i1 == i2).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("M", [5, 40, 300])
+@pytest.mark.parametrize("M", [1, 5, 24, 40, 300])
 def test_score_candidates_exact_set(M):
     """Every filtered score >= thr[m] is appended exactly once (the 128x128, streaming and gemm256
     candidate kernels; N not a multiple of 64 / 256)."""
