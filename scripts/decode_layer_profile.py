@@ -38,7 +38,7 @@ def main():
     slots = defaultdict(lambda: {"dur": [], "gap": [], "name": ""})
     spans = []
     for s in dec:
-        spans.append((s[-1][1] - s[0][0]) / 1e3)
+        spans.append((s[-1][1] - s[0][0]) / 1e6)
         att = [i for i, (_, _, n) in enumerate(s) if "paged_decode" in n]
         for li in range(1, len(att) - 1):
             a, b = att[li], att[li + 1]
