@@ -1,6 +1,8 @@
-"""Multi-process (gloo, world_size 2, CPU) checks of the distributed paths: tensor-parallel Llama
-forward == the unsharded model, ShardedIndex search == a single index, DP corpus embedding == a
-single-rank embedding.  The same code runs over RCCL on GPUs (backend chosen by parallel.dist.init)."""
+"""Multi-process (gloo, CPU) checks of the distributed paths: tensor-parallel Llama forward and
+leader/follower serving == the unsharded model (world 2, and world 4 / 8 on the Llama-3-70B head
+layout, where TP 8 leaves one KV head per rank), ShardedIndex search == a single index, DP corpus
+embedding == a single-rank embedding.  The same code runs over RCCL on GPUs (backend chosen by
+parallel.dist.init)."""
 import os
 import socket
 
@@ -38,20 +40,25 @@ def _entry(rank, fn, port, world, *args):
         pdist.shutdown()
 
 
-def _tp_body(info, out_path):
+# (world, model): the 70B head layout (64 query / 8 KV heads) at TP 4 and TP 8 (one KV head per rank)
+TP_CASES = [(2, "tiny-llama"), (4, "tiny-llama-70b-layout"), (8, "tiny-llama-70b-layout")]
+
+
+def _tp_body(info, out_path, model_name):
     from django_assistant_bot_amd.models.configs import decoder_config
     from django_assistant_bot_amd.models.llama import AttnMeta, KVCache, LlamaModel
     from django_assistant_bot_amd.models.weights import random_decoder_weights, shard_decoder_weights
     from django_assistant_bot_amd.parallel import dist as pdist
 
-    cfg = decoder_config("tiny-llama")
+    W = info.world_size
+    cfg = decoder_config(model_name)
     full = random_decoder_weights(cfg, dtype=torch.float32, seed=11)
-    group, tp_rank, _ = pdist.tp_groups(WORLD)
-    shard = shard_decoder_weights(full, cfg, tp_rank, WORLD)
-    model = LlamaModel(cfg, shard, "cpu", tp_group=group, tp_size=WORLD)
+    group, tp_rank, _ = pdist.tp_groups(W)
+    shard = shard_decoder_weights(full, cfg, tp_rank, W)
+    model = LlamaModel(cfg, shard, "cpu", tp_group=group, tp_size=W)
     ids = torch.arange(5, 45, dtype=torch.int32)
     T = ids.numel()
-    kv = KVCache(cfg.layers, 4, cfg.kv_heads // WORLD, 64, cfg.head_dim, "cpu", dtype=torch.float32)
+    kv = KVCache(cfg.layers, 4, cfg.kv_heads // W, 64, cfg.head_dim, "cpu", dtype=torch.float32)
     meta = AttnMeta(decode=False, positions=torch.arange(T, dtype=torch.int32), slots=torch.arange(T),
                     block_tables=torch.arange(4, dtype=torch.int32)[None], ctx_lens=torch.tensor([T], dtype=torch.int32),
                     cu_q=torch.tensor([0, T], dtype=torch.int32), max_q=T)
@@ -64,9 +71,10 @@ def _tp_body(info, out_path):
         torch.save({"err": (h - ref).abs().max().item(), "logits_err": lg_err}, out_path)
 
 
-def test_tensor_parallel_forward_matches_full_model(tmp_path):
+@pytest.mark.parametrize("world,model_name", TP_CASES)
+def test_tensor_parallel_forward_matches_full_model(tmp_path, world, model_name):
     out = str(tmp_path / "tp.pt")
-    _run(_tp_body, out)
+    _run(_tp_body, out, model_name, world=world)
     res = torch.load(out, weights_only=True)
     assert res["err"] < 1e-4 and res["logits_err"] < 1e-4
 
@@ -247,17 +255,18 @@ def _drive(engine):
     return [engine.pop_output(r).token_ids for r in rids]
 
 
-def _tp_serving_body(info, out_path):
+def _tp_serving_body(info, out_path, model_name):
     from django_assistant_bot_amd.models.configs import decoder_config
     from django_assistant_bot_amd.models.weights import random_decoder_weights, shard_decoder_weights
     from django_assistant_bot_amd.parallel import dist as pdist
     from django_assistant_bot_amd.parallel import tp_serving
 
-    cfg = decoder_config("tiny-llama")
+    W = info.world_size
+    cfg = decoder_config(model_name)
     full = random_decoder_weights(cfg, dtype=torch.float32, seed=21)
-    group, tp_rank, _ = pdist.tp_groups(WORLD)
-    ctrl = tp_serving.control_group(list(range(WORLD)))
-    eng = _tp_engine(cfg, shard_decoder_weights(full, cfg, tp_rank, WORLD), tp_group=group, tp_size=WORLD,
+    group, tp_rank, _ = pdist.tp_groups(W)
+    ctrl = tp_serving.control_group(list(range(W)))
+    eng = _tp_engine(cfg, shard_decoder_weights(full, cfg, tp_rank, W), tp_group=group, tp_size=W,
                      tp_rank=tp_rank)
     if info.rank == 0:
         leader = tp_serving.TPLeader(eng, ctrl)
@@ -270,13 +279,14 @@ def _tp_serving_body(info, out_path):
         assert not eng.has_unfinished()
 
 
-def test_tp_leader_follower_serving_matches_single_process(tmp_path):
+@pytest.mark.parametrize("world,model_name", TP_CASES)
+def test_tp_leader_follower_serving_matches_single_process(tmp_path, world, model_name):
     out = str(tmp_path / "tp_tokens.pt")
-    _run(_tp_serving_body, out)
+    _run(_tp_serving_body, out, model_name, world=world)
     from django_assistant_bot_amd.models.configs import decoder_config
     from django_assistant_bot_amd.models.weights import random_decoder_weights
 
-    cfg = decoder_config("tiny-llama")
+    cfg = decoder_config(model_name)
     ref = _drive(_tp_engine(cfg, random_decoder_weights(cfg, dtype=torch.float32, seed=21)))
     got = torch.load(out, weights_only=True)
     assert got == ref
