@@ -6,4 +6,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   -- python bench.py --steps 1 --warmup 1 "$@" > gpurun_out/prof_bench.log 2>&1 || exit $?
 d=$(dirname "$(find gpurun_out/prof_bench -name 'run_kernel_stats.csv' | head -1)")
 python scripts/step_breakdown.py "$d" run --out gpurun_out/prof_bench_steps.md && \
+python scripts/gap_report.py "$d" run --min-us 50 --top 40 ${GAP_LAST_MS:+--last-ms $GAP_LAST_MS} --out gpurun_out/prof_bench_gaps.md > /dev/null && \
 python scripts/prof_summary.py "$d" run gpurun_out/prof_bench_stats.md --drop-trace
