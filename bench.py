@@ -74,11 +74,30 @@ def synth_text(rng: np.random.Generator, n_words: int) -> str:
 
 
 class SyntheticDocuments(dict):
-    """Lazily materialised document store: doc id -> StoredDocument with ~200-300 words."""
+    """Document store: doc id -> StoredDocument with ~200-300 words.  ``materialize`` builds every
+    document up front (an in-memory store, like the rows a deployment would fetch from its database);
+    otherwise documents are generated on first access."""
 
     def __init__(self, n_docs: int, seed: int):
         super().__init__()
         self.n_docs, self.seed = n_docs, seed
+
+    def materialize(self):
+        """All documents at once: word ids for the whole corpus in one draw, then one join per
+        document (every 13th word ends a sentence)."""
+        from django_assistant_bot_amd.engine.rag import StoredDocument
+
+        rng = np.random.default_rng(self.seed * 7919 + 17)
+        lens = rng.integers(200, 300, self.n_docs)
+        offs = np.concatenate([[0], np.cumsum(lens)])
+        words = rng.integers(0, len(_WORDS), int(offs[-1]))
+        pos = np.arange(int(offs[-1])) - np.repeat(offs[:-1], lens)
+        vocab = np.array(list(_WORDS) + [w + "." for w in _WORDS], dtype=object)
+        toks = vocab[words + len(_WORDS) * (pos % 13 == 12)].tolist()
+        for k in range(self.n_docs):
+            dict.__setitem__(self, k, StoredDocument(k, f"Document {k}", f"Wiki / Section {k // 100} / Document {k}",
+                                                     " ".join(toks[offs[k]:offs[k + 1]])))
+        return self
 
     def __contains__(self, k):
         return 0 <= int(k) < self.n_docs
@@ -157,6 +176,31 @@ def measure_fast_steps(rag, llm, questions, info, dev, classify_tokens: int = 16
             "answer_tokens": [classify_tokens, known_tokens], "batch": len(questions)}
 
 
+def _host_profiler():
+    """cProfile of the first timed batch's host side when DAB_HOST_PROFILE names an output file
+    (finds the host work that leaves the GPU idle between the query embedding and the prefill)."""
+    if not os.environ.get("DAB_HOST_PROFILE"):
+        return None
+    import cProfile
+
+    prof = cProfile.Profile()
+    prof.enable()
+    return prof
+
+
+def _dump_host_profile(prof):
+    import io
+    import pstats
+
+    prof.disable()
+    buf = io.StringIO()
+    st = pstats.Stats(prof, stream=buf).sort_stats("cumulative")
+    st.print_stats(60)
+    st.sort_stats("tottime").print_stats(40)
+    with open(os.environ["DAB_HOST_PROFILE"], "w") as f:
+        f.write(buf.getvalue())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -223,7 +267,7 @@ def main():
     # ---- synthetic corpus: index rows (questions) grouped into documents
     n_rows = args.index_rows
     n_docs = max(1, n_rows // args.rows_per_doc)
-    docs = SyntheticDocuments(n_docs, args.seed)
+    docs = SyntheticDocuments(n_docs, args.seed).materialize()
     if serve:  # replicated: every rank holds all rows (identical generator), no collective per search
         index = VectorIndex(embedder.dim, dev)
         gen = torch.Generator(device=dev).manual_seed(args.seed * 31)
@@ -327,7 +371,10 @@ def main():
         for step in range(n_steps):
             if step == args.warmup:
                 stats0, t0 = sync_start()
+            prof = _host_profiler() if step == args.warmup else None
             res = rag.answer(my_q[step * B:(step + 1) * B], params, bot_group=0)
+            if prof is not None:
+                _dump_host_profile(prof)
             if step >= args.warmup:
                 latencies += [r.latency_s for r in res]
                 prompt_lens += [r.usage["prompt_tokens"] for r in res]
