@@ -90,11 +90,14 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_f
   const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
   const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
-  const int qb = sid % nqb;
   const int h = (sid / nqb) % gridDim.y;
   const int b = sid / (nqb * gridDim.y);
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
+  // causal: a sequence's last query block (the most key tiles) starts first, so the short blocks
+  // fill the end of each XCD's walk instead of a long one trailing alone
+  const int nqb_b = div_up(seqlen_q, QB);
+  const int qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
   const int q0 = qb * QB;
   if (q0 >= seqlen_q) return;
   int kv_len, k_start = 0;
@@ -351,11 +354,14 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
   const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
   const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
-  const int qb = sid % nqb;
   const int h = (sid / nqb) % gridDim.y;
   const int b = sid / (nqb * gridDim.y);
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
+  // causal: a sequence's last query block (the most key tiles) starts first, so the short blocks
+  // fill the end of each XCD's walk instead of a long one trailing alone
+  const int nqb_b = div_up(seqlen_q, QB);
+  const int qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
   const int q0 = qb * QB;
   if (q0 >= seqlen_q) return;  // whole workgroup
   const int kv_len = p.ctx_k[b];
