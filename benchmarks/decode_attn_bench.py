@@ -31,12 +31,18 @@ def main():
                     help="stream a gate_up-sized decode GEMM (235 MB of weights, cold copies) between "
                          "attention launches, as the layer does (0: attention back to back)")
     ap.add_argument("--between-rows", type=int, default=28672, help="weight rows of that GEMM (K 4096)")
+    ap.add_argument("--between-kind", choices=("gemm", "copy", "spin"), default="gemm",
+                    help="what runs between attention launches: the streaming GEMM, a device copy of "
+                         "the same bytes (HBM traffic without MFMA), or a spin kernel of about the "
+                         "same duration (no memory traffic)")
+    ap.add_argument("--parts", default="2048,1024,512", help="partition sizes to time")
+    ap.add_argument("--dists", default="mixed,uniform", help="context distributions to time")
     ap.add_argument("--spread", choices=("random", "compact"), default="random",
                     help="live blocks drawn at random from the pool, or the lowest ids in order")
     a = ap.parse_args()
     Hq, Hkv, D, bs, B = 32, 8, 128, 64, a.batch
     g = torch.Generator().manual_seed(0)
-    for dist_name in ("mixed", "uniform"):
+    for dist_name in a.dists.split(","):
         if dist_name == "mixed":
             ctx_h = torch.randint(950, 1450, (B,), generator=g)
         else:
@@ -65,7 +71,17 @@ def main():
         gemm_w = [ops.shuffle_weights(torch.randn(a.between_rows, 4096, device="cuda").to(torch.bfloat16))
                   for _ in range(2)] if a.between else []
         gemm_x = torch.randn(B, 4096, device="cuda").to(torch.bfloat16)
-        for part in (2048, 1024, 512):
+        copy_dst = torch.empty_like(gemm_w[0]) if a.between and a.between_kind == "copy" else None
+
+        def between(i):
+            if a.between_kind == "gemm":
+                ops.stream_gemm(gemm_x, gemm_w[i % 2], cfg=10, nt=os.environ.get("BETWEEN_NT", "1") == "1")
+            elif a.between_kind == "copy":
+                copy_dst.copy_(gemm_w[i % 2])
+            else:
+                torch.cuda._sleep(100_000)  # ~50 us of spinning at ~2 GHz, no memory traffic
+
+        for part in (int(x) for x in a.parts.split(",")):
             ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / part), "cuda")
             for oname, order in (("batch", None), ("longest", longest)):
                 outs = []
@@ -73,7 +89,7 @@ def main():
                 def run():
                     for i, (kc, vc) in enumerate(caches):
                         if gemm_w:
-                            ops.stream_gemm(gemm_x, gemm_w[i % 2], cfg=10, nt=os.environ.get("BETWEEN_NT", "1") == "1")
+                            between(i)
                         outs.append(ops.paged_decode(q, kc, vc, bt, ctx, part, ws, order=order))
                 run()
                 torch.cuda.synchronize()
