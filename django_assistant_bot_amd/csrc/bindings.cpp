@@ -148,6 +148,14 @@ PYBIND11_MODULE(_native, m) {
                                      reinterpret_cast<int*>(cand_idx), cap, ST(s)),
           "gemm_score_candidates");
   });
+  m.def("index_scan_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
+                                         u cnt, u cand_val, u cand_idx, int cap, u s) {
+    check(dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, reinterpret_cast<const int*>(row_group),
+                                          reinterpret_cast<const int*>(q_group), reinterpret_cast<const float*>(thr),
+                                          reinterpret_cast<int*>(cnt), reinterpret_cast<float*>(cand_val),
+                                          reinterpret_cast<int*>(cand_idx), cap, ST(s)),
+          "index_scan_candidates_shuf");
+  });
   m.def("skinny_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
                           int S, int epilogue, u s, int nt) {
     check(dab::skinny_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt),

@@ -14,7 +14,10 @@
 //   * queries [16, K] in LDS with chunk c of row r at c ^ (r & 15): conflict-free ds_read_b128
 //     B fragments (one fragment feeds both A tiles' MFMAs);
 //   * epilogue straight from the accumulators: a score >= thr[query] (rare) loads its row's group
-//     and appends (score, row) to the query's list with one atomic (gemm.hip EPI_CANDIDATES).
+//     and appends (score, row) to the query's list with one atomic (gemm.hip EPI_CANDIDATES);
+//   * SHUF: the rows come from a copy in the decode-stream layout [rows/16][K/32][64 lanes][8]
+//     (ops.shuffle_weights), where each 16-row x 32-k A fragment is 1 KB contiguous in lane order:
+//     every load is one fully coalesced 1 KB read instead of 16 rows x 64 B.
 #include "common.h"
 #include "launchers.h"
 
@@ -43,6 +46,7 @@ constexpr int kScanNWIN = 8;   // chunks (of 32 k) in flight per wave
 
 }  // namespace
 
+template <bool SHUF>
 __global__ __launch_bounds__(256, 2) void index_scan_kernel(ScanParams p) {
   constexpr int RT = kScanRT, NWIN = kScanNWIN;
   __shared__ __attribute__((aligned(16))) char xs[16 * kScanKMax * 2];
@@ -71,14 +75,23 @@ __global__ __launch_bounds__(256, 2) void index_scan_kernel(ScanParams p) {
   auto tile_row0 = [&](int i) { return (blockIdx.x + i * gridDim.x) * 128 + 32 * w; };
   // descriptor of tile i (rows past N read zeros); past the wave's last tile: empty range (the ring's
   // run-out loads return zeros without memory traffic)
+  // SHUF: the tile's two 16-row blocks are whole in the copy (its row count is a multiple of 32);
+  // rows >= N there score like any row and are dropped by the epilogue's n < N test
   auto rsrc_of = [&](int i) {
     const int r0 = tile_row0(i);
-    const int rows = i < my_tiles ? max(0, min(32, p.N - r0)) : 0;
-    return __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)min(r0, p.N - 1) * p.ldw), (short)0,
-                                             (int)(rows * p.ldw * 2), 0x00020000);
+    if constexpr (SHUF) {
+      const int bytes = i < my_tiles ? 2 * nck * 1024 : 0;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)(min(r0, p.N - 1) / 16) * nck * 512), (short)0,
+                                               bytes, 0x00020000);
+    } else {
+      const int rows = i < my_tiles ? max(0, min(32, p.N - r0)) : 0;
+      return __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)min(r0, p.N - 1) * p.ldw), (short)0,
+                                               (int)(rows * p.ldw * 2), 0x00020000);
+    }
   };
-  const int voff = (int)((li * p.ldw + 8 * g) * 2);
-  const int astr = (int)(16 * p.ldw * 2);
+  const int voff = SHUF ? lane * 16 : (int)((li * p.ldw + 8 * g) * 2);
+  const int astr = SHUF ? nck * 1024 : (int)(16 * p.ldw * 2);  // next 16-row block
+  constexpr int CSTR = SHUF ? 1024 : 64;                         // next 32-k chunk
 
   bf16x8 wr[NWIN][RT];
   int ld_tile = 0, ld_c = 0;  // next chunk to load (wave-uniform)
@@ -87,7 +100,7 @@ __global__ __launch_bounds__(256, 2) void index_scan_kernel(ScanParams p) {
 #pragma unroll
     for (int a = 0; a < RT; ++a)
       wr[slot][a] = __builtin_bit_cast(
-          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ld_rs, voff + a * astr, ld_c * 64, 2));  // nt: read once
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ld_rs, voff + a * astr, ld_c * CSTR, 2));  // nt: read once
     if (++ld_c == nck) {
       ld_c = 0;
       ld_rs = rsrc_of(++ld_tile);
@@ -133,12 +146,9 @@ __global__ __launch_bounds__(256, 2) void index_scan_kernel(ScanParams p) {
   }
 }
 
-int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
-                          const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                          hipStream_t s) {
-  if (M <= 0 || N <= 0) return 0;
-  if (M > 16 || K > kScanKMax || K % (32 * kScanNWIN) || ldx % 8 || ldw % 8 || cap <= 0) return hipErrorInvalidValue;
-  if (32L * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+static int index_scan_launch(bool shuf, const void* X, long ldx, const void* W, long ldw, int M, int N, int K,
+                             const int* row_group, const int* q_group, const float* thr, int* cnt, float* cand_val,
+                             int* cand_idx, int cap, hipStream_t s) {
   ScanParams p;
   p.X = (const bf16*)X;
   p.ldx = ldx;
@@ -158,8 +168,29 @@ int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int 
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = (N + 127) / 128;
   const int grid = tiles < 2 * cus ? tiles : 2 * cus;
-  hipLaunchKernelGGL(index_scan_kernel, dim3(grid), dim3(256), 0, s, p);
+  if (shuf)
+    hipLaunchKernelGGL(index_scan_kernel<true>, dim3(grid), dim3(256), 0, s, p);
+  else
+    hipLaunchKernelGGL(index_scan_kernel<false>, dim3(grid), dim3(256), 0, s, p);
   return hipGetLastError();
+}
+
+int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
+                          const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                          hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 16 || K > kScanKMax || K % (32 * kScanNWIN) || ldx % 8 || ldw % 8 || cap <= 0) return hipErrorInvalidValue;
+  if (32L * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  return index_scan_launch(false, X, ldx, W, ldw, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
+}
+
+// W: the rows in the shuffle_weights layout, with at least round_up(N, 32) rows
+int index_scan_candidates_shuf(const void* X, long ldx, const void* W, int M, int N, int K, const int* row_group,
+                               const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
+                               int cap, hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (M > 16 || K > kScanKMax || K % (32 * kScanNWIN) || ldx % 8 || cap <= 0) return hipErrorInvalidValue;
+  return index_scan_launch(true, X, ldx, W, K, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
 }
 
 }  // namespace dab

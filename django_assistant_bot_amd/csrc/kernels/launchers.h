@@ -75,6 +75,10 @@ int stream_gemm_bn(int cfg);
 int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                           hipStream_t s);
+// ... the same scan over a copy of the rows in the shuffle_weights layout (>= round_up(N, 32) rows)
+int index_scan_candidates_shuf(const void* X, long ldx, const void* W, int M, int N, int K, const int* row_group,
+                               const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
+                               int cap, hipStream_t s);
 int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                             const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                             hipStream_t s);

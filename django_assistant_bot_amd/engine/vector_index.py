@@ -14,6 +14,8 @@ compaction), growth, and safetensors snapshots for warm starts.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -32,11 +34,13 @@ class VectorIndex:
         self.vecs = self.row_ids = self.row_docs = self.row_group = None
         self._row_of: dict[int, int] = {}
         self._sorted = None  # lazily built (sorted ids, rows) for vectorised id -> row lookups
+        self._shuf = None  # the rows in the shuffle_weights layout (see shuffled_scan), or None
         self._dead = 0
         self._grow(max(64, capacity))
 
     # ------------------------------------------------------------------ storage
     def _grow(self, cap: int):
+        self._shuf = None
         cap = (cap + 63) // 64 * 64
         dev = self.device
         vecs = torch.zeros((cap, self.dim), dtype=self.dtype, device=dev)
@@ -55,6 +59,10 @@ class VectorIndex:
     threshold_search = True
     threshold_min_rows = 1 << 19
     sample_stride = 16
+    # 1..16-query searches scan a second copy of the rows in the decode-stream layout (every
+    # 16-row x 32-k fragment one coalesced 1 KB load: index_scan.hip SHUF).  It is built at the
+    # first such search, kept current by add(), and costs one more copy of the vectors in HBM.
+    shuffled_scan = os.environ.get("DAB_INDEX_SHUF", "1") != "0"
 
     def __len__(self) -> int:
         return len(self._row_of)
@@ -108,6 +116,8 @@ class VectorIndex:
             return (x.pin_memory() if pin else x).to(self.device, non_blocking=True)
         r = dev(rows)
         self.vecs[r] = v
+        if self._shuf is not None:
+            ops.shuffle_rows_into(self._shuf, r, v)
         self.row_ids[r] = dev(ids)
         self.row_docs[r] = dev(docs)
         self.row_group[r] = dev(grp)
@@ -128,6 +138,7 @@ class VectorIndex:
         live = (self.row_group[: self.n] >= 0).nonzero().flatten()
         m = live.numel()
         self.vecs[:m] = self.vecs[live]
+        self._shuf = None
         self.row_ids[:m] = self.row_ids[live]
         self.row_docs[:m] = self.row_docs[live]
         self.row_group[:m] = self.row_group[live]
@@ -250,7 +261,13 @@ class VectorIndex:
         del s_scores
         thr = tv[:, kk - 1].contiguous()
         cap = max(4096, 64 * k * self.sample_stride // 16)
-        cand_val, cand_idx, cnt = ops.score_candidates(q, self.vecs[:n4], thr, cap, self.row_group[:n4], qg)
+        if self._use_shuffled(q.shape[0]):
+            if self._shuf is None:
+                with torch.inference_mode(False):  # a normal tensor: add() updates it in place later
+                    self._shuf = ops.shuffle_weights(self.vecs)
+            cand_val, cand_idx, cnt = ops.score_candidates_shuffled(q, self._shuf, n4, thr, cap, self.row_group[:n4], qg)
+        else:
+            cand_val, cand_idx, cnt = ops.score_candidates(q, self.vecs[:n4], thr, cap, self.row_group[:n4], qg)
         if int(cnt.max()) > cap:
             self.stats["threshold_overflows"] += 1
             return None
@@ -258,6 +275,10 @@ class VectorIndex:
         vals, pos = ops.topk_rows(cand_val, min(k, cap))
         rows = torch.gather(cand_idx, 1, pos.long())
         return vals, rows.masked_fill(torch.isinf(vals), 0)
+
+    def _use_shuffled(self, m: int) -> bool:
+        return (self.shuffled_scan and self.device.type == "cuda" and m <= 16 and self.dtype == torch.bfloat16
+                and self.dim % 256 == 0 and self.dim <= 1024)
 
     # ------------------------------------------------------------------ persistence
     def save(self, path: str) -> None:
@@ -276,6 +297,7 @@ class VectorIndex:
         idx = cls(st["vecs"].shape[1], device, capacity=max(64, st["vecs"].shape[0]), dtype=st["vecs"].dtype)
         n = st["vecs"].shape[0]
         idx.vecs[:n] = st["vecs"].to(idx.device)
+        idx._shuf = None
         idx.row_ids[:n] = st["ids"].to(idx.device)
         idx.row_docs[:n] = st["docs"].to(idx.device)
         idx.row_group[:n] = st["group"].to(idx.device)

@@ -383,6 +383,39 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
     return cand_val, cand_idx, cnt
 
 
+def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=None):
+    """``score_candidates`` for 1..16 queries over a copy of the rows in the ``shuffle_weights``
+    layout (``B_shuf`` [R, K], R >= round_up(N, 32), R % 16 == 0): the persistent scan of
+    index_scan.hip reads every 16-row x 32-k fragment as one coalesced 1 KB load."""
+    expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
+    M, K = A.shape
+    expect(1 <= M <= 16 and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..16 K-contiguous queries")
+    expect(B_shuf.is_contiguous() and B_shuf.shape[1] == K and K % 256 == 0 and K <= 1024, "K % 256 == 0, K <= 1024")
+    expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 32) * 32, "shuffled copy needs round_up(N, 32) rows")
+    expect(thr.dtype == torch.float32 and thr.is_contiguous() and thr.numel() >= M, "thr must be fp32 [M]")
+    if row_group is not None:
+        _i32(row_group)
+        expect(row_group.numel() >= N, "row_group shorter than N")
+    if q_group is not None:
+        _i32(q_group)
+        expect(q_group.numel() >= M, "q_group shorter than M")
+    cand_val = torch.full((M, cap), float("-inf"), dtype=torch.float32, device=A.device)
+    cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
+    cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
+    native().index_scan_candidates_shuf(ptr(A), A.stride(0), ptr(B_shuf), M, int(N), K, ptr(row_group), ptr(q_group),
+                                        ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
+    return cand_val, cand_idx, cnt
+
+
+def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor) -> None:
+    """Writes ``vals`` [n, K] as rows ``rows`` of ``dst``, a [R, K] tensor in the ``shuffle_weights``
+    layout (the incremental form of shuffle_weights, for copies that are updated in place)."""
+    R, K = dst.shape
+    v5 = dst.view(R // 16, K // 32, 4, 16, 8)
+    rows = rows.to(dst.device, torch.long)
+    v5[rows // 16, :, :, rows % 16, :] = vals.to(dst.dtype).reshape(-1, K // 32, 4, 8)
+
+
 SKINNY_MAX_M = 128
 _SK_KSTAGE = 256
 

@@ -488,6 +488,66 @@ def test_score_candidates_exact_set(M):
         torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+def test_score_candidates_shuffled_exact_set(M):
+    """The persistent scan over a shuffle_weights copy of the rows (index_scan.hip SHUF) appends
+    exactly the filtered scores >= thr[m] (N not a multiple of 32: the copy is zero-padded)."""
+    N, K = 100_004, 768
+    A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
+    qg = torch.tensor([(-1 if i % 3 == 0 else i % 3) for i in range(M)], device=DEV, dtype=torch.int32)
+    full = ops.gemm_bt(A, B, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg)
+    thr = torch.quantile(full.clamp_min(-1.0), 0.995, dim=1).contiguous()
+    Bp = torch.zeros((-(-N // 32) * 32, K), dtype=torch.bfloat16, device=DEV)
+    Bp[:N] = B
+    cap = 4096
+    cv, ci, cnt = ops.score_candidates_shuffled(A, ops.shuffle_weights(Bp), N, thr, cap, rg, qg)
+    assert int(cnt.max()) <= cap
+    for m in range(M):
+        k = int(cnt[m])
+        got = set(ci[m, :k].tolist())
+        exp = set((full[m] >= thr[m]).nonzero().flatten().tolist())
+        near = set(((full[m] - thr[m]).abs() < 1e-5).nonzero().flatten().tolist())
+        assert (got ^ exp) <= near and len(got) == k
+        torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
+
+
+def test_index_shuffled_copy_tracks_updates():
+    """The shuffled copy behind 1..16-query searches follows upserts, fresh rows, removals and a
+    capacity growth: results equal the row-major scan after each."""
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+    n, dim = 560_000, 256
+    g = torch.Generator(device=DEV).manual_seed(9)
+    idx = VectorIndex(dim, DEV, capacity=n + 1000)
+    idx.add(torch.arange(n).numpy(), torch.randn(n, dim, device=DEV, generator=g))
+    q = torch.randn(3, dim, device=DEV, generator=g)
+
+    def check():
+        idx.shuffled_scan = True
+        v1, i1, _ = idx.search(q, 100)
+        assert idx._shuf is not None
+        idx.shuffled_scan = False
+        v2, i2, _ = idx.search(q, 100)
+        torch.testing.assert_close(v1, v2)
+        assert (i1 == i2).float().mean() > 0.999
+
+    check()
+    # upsert existing ids towards the queries (they must now rank first) + fresh rows, no growth
+    hot = torch.arange(10, 20).numpy()
+    idx.add(hot, q[0].repeat(10, 1) + 0.01 * torch.randn(10, dim, device=DEV, generator=g))
+    idx.add(torch.arange(n, n + 500).numpy(), torch.randn(500, dim, device=DEV, generator=g))
+    assert idx._shuf is not None  # updated in place
+    check()
+    v, i, _ = idx.search(q[:1], 10)
+    assert set(i[0].tolist()) == set(hot.tolist())
+    idx.remove(hot[:5].tolist())
+    check()
+    idx.add(torch.arange(n + 500, n + 3000).numpy(), torch.randn(2500, dim, device=DEV, generator=g))  # grows
+    check()
+
+
 def test_index_threshold_search_overflow_falls_back():
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
