@@ -148,13 +148,22 @@ PYBIND11_MODULE(_native, m) {
                                      reinterpret_cast<int*>(cand_idx), cap, ST(s)),
           "gemm_score_candidates");
   });
-  m.def("index_scan_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
-                                         u cnt, u cand_val, u cand_idx, int cap, u s) {
-    check(dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, reinterpret_cast<const int*>(row_group),
-                                          reinterpret_cast<const int*>(q_group), reinterpret_cast<const float*>(thr),
-                                          reinterpret_cast<int*>(cnt), reinterpret_cast<float*>(cand_val),
-                                          reinterpret_cast<int*>(cand_idx), cap, ST(s)),
-          "index_scan_candidates_shuf");
+  // candidates over a shuffle_weights copy of the rows: 1..16 queries on the persistent scan,
+  // 32..64 on the weight-streaming kernel
+  m.def("score_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
+                                    u cnt, u cand_val, u cand_idx, int cap, u s) {
+    auto* rg = reinterpret_cast<const int*>(row_group);
+    auto* qg = reinterpret_cast<const int*>(q_group);
+    auto* th = reinterpret_cast<const float*>(thr);
+    auto* ct = reinterpret_cast<int*>(cnt);
+    auto* cv = reinterpret_cast<float*>(cand_val);
+    auto* ci = reinterpret_cast<int*>(cand_idx);
+    int rc = hipErrorInvalidValue;
+    if (M <= 16)
+      rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
+    else if (M >= 32 && M <= 64)
+      rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
+    check(rc, "score_candidates_shuf");
   });
   m.def("skinny_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
                           int S, int epilogue, u s, int nt) {

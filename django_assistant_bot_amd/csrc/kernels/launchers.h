@@ -82,6 +82,9 @@ int index_scan_candidates_shuf(const void* X, long ldx, const void* W, int M, in
 int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                             const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                             hipStream_t s);
+int stream_score_candidates_shuf(const void* X, long ldx, const void* W, int M, int N, int K, const int* row_group,
+                                 const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
+                                 int cap, hipStream_t s);
 int stream_gemm_max_m(int cfg);
 int stream_gemm_shuffled(int cfg);  // 1: cfg reads weights in the ops.shuffle_weights layout
 

@@ -159,8 +159,11 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   } else {
     // ------------------------------------------------------------------ compute waves
     const int rg = w / KG, kg = w % KG;
+    // SHUF: whole 16-row blocks (a block's rows are interleaved in every 1 KB fragment; the rows
+    // past N of a partial block exist in the copy and are dropped by the epilogues)
+    const int w_rows = SHUF ? min(BN, (p.N - n0 + 15) / 16 * 16) : min(BN, p.N - n0);
     const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)n0 * p.ldw), 0,
-                                                        (int)(min(BN, p.N - n0) * p.ldw * 2), 0x00020000);
+                                                        (int)(w_rows * p.ldw * 2), 0x00020000);
     // row-major W: lane (li, g) reads row li, k 8g..8g+7 of a 16 x 32 chunk (16 rows x 64 B per load);
     // SHUF (shuffle_weights layout [N/16][K/32][64 lanes][8]): every load is 1 KB contiguous
     const int w_voff = SHUF ? lane * 16 + ((k_begin + kg * KW) / 32) * 1024
@@ -450,13 +453,16 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
 // Index threshold candidates for small query batches (M <= 64): the index rows stream through the
 // weight ring like decode weights (row-major, 16 rows x 64 B per load), the queries sit in LDS.
 // At M = 1..64 the MFMA tiles of the GEMM kernels are mostly padding and the scan is HBM-bound.
-int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
-                            const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                            hipStream_t s) {
-  constexpr int KS = 128, CFG = 7;  // M <= 64, BN 64, 4 loader waves, row-major weights
+static int stream_candidates_launch(bool shuf, const void* X, long ldx, const void* W, long ldw, int M, int N, int K,
+                                    const int* row_group, const int* q_group, const float* thr, int* cnt,
+                                    float* cand_val, int* cand_idx, int cap, hipStream_t s) {
+  constexpr int KS = 128;
+  // M <= 64, BN 64, 4 loader waves: row-major rows (cfg 7) or a shuffle_weights copy (cfg 12)
+  const int CFG = shuf ? 12 : 7;
   if (M <= 0 || N <= 0) return 0;
   if (M > stream_gemm_max_m(CFG) || K % KS || ldx % 8 || ldw % 8 || cap <= 0) return hipErrorInvalidValue;
   if ((long)stream_gemm_bn(CFG) * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  if (shuf && (ldw != K || K % 32)) return hipErrorInvalidValue;
   StreamParams p{};
   p.X = (const bf16*)X;
   p.ldx = ldx;
@@ -475,8 +481,25 @@ int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, in
   p.cand_val = cand_val;
   p.cand_idx = cand_idx;
   p.cap = cap;
-  launch_cfg<CFG>(p, s, true);
+  if (shuf)
+    launch_cfg<12>(p, s, true);
+  else
+    launch_cfg<7>(p, s, true);
   return hipGetLastError();
+}
+
+int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
+                            const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
+                            hipStream_t s) {
+  return stream_candidates_launch(false, X, ldx, W, ldw, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap,
+                                  s);
+}
+
+// W: the rows in the shuffle_weights layout, at least round_up(N, 64) of them
+int stream_score_candidates_shuf(const void* X, long ldx, const void* W, int M, int N, int K, const int* row_group,
+                                 const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
+                                 int cap, hipStream_t s) {
+  return stream_candidates_launch(true, X, ldx, W, K, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
 }
 
 }  // namespace dab

@@ -59,7 +59,7 @@ class VectorIndex:
     threshold_search = True
     threshold_min_rows = 1 << 19
     sample_stride = 16
-    # 1..16-query searches scan a second copy of the rows in the decode-stream layout (every
+    # 1..16 / 32..64-query searches scan a second copy of the rows in the decode-stream layout (every
     # 16-row x 32-k fragment one coalesced 1 KB load: index_scan.hip SHUF).  It is built at the
     # first such search, kept current by add(), and costs one more copy of the vectors in HBM.
     shuffled_scan = os.environ.get("DAB_INDEX_SHUF", "1") != "0"
@@ -277,8 +277,8 @@ class VectorIndex:
         return vals, rows.masked_fill(torch.isinf(vals), 0)
 
     def _use_shuffled(self, m: int) -> bool:
-        return (self.shuffled_scan and self.device.type == "cuda" and m <= 16 and self.dtype == torch.bfloat16
-                and self.dim % 256 == 0 and self.dim <= 1024)
+        return (self.shuffled_scan and self.device.type == "cuda" and self.dtype == torch.bfloat16
+                and ops.kernels.shuffled_scan_ok(m, self.dim))
 
     # ------------------------------------------------------------------ persistence
     def save(self, path: str) -> None:

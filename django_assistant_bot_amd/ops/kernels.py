@@ -384,14 +384,15 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
 
 
 def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=None):
-    """``score_candidates`` for 1..16 queries over a copy of the rows in the ``shuffle_weights``
-    layout (``B_shuf`` [R, K], R >= round_up(N, 32), R % 16 == 0): the persistent scan of
-    index_scan.hip reads every 16-row x 32-k fragment as one coalesced 1 KB load."""
+    """``score_candidates`` for 1..16 or 32..64 queries over a copy of the rows in the
+    ``shuffle_weights`` layout (``B_shuf`` [R, K], R >= round_up(N, 64), R % 16 == 0): every
+    16-row x 32-k fragment is one coalesced 1 KB load (1..16 queries: the persistent scan of
+    index_scan.hip; 32..64: the weight-streaming kernel's candidate epilogue)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
     M, K = A.shape
-    expect(1 <= M <= 16 and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..16 K-contiguous queries")
-    expect(B_shuf.is_contiguous() and B_shuf.shape[1] == K and K % 256 == 0 and K <= 1024, "K % 256 == 0, K <= 1024")
-    expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 32) * 32, "shuffled copy needs round_up(N, 32) rows")
+    expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..16 or 32..64 queries, K ok")
+    expect(B_shuf.is_contiguous() and B_shuf.shape[1] == K, "shuffled copy [R, K]")
+    expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 64) * 64, "shuffled copy needs round_up(N, 64) rows")
     expect(thr.dtype == torch.float32 and thr.is_contiguous() and thr.numel() >= M, "thr must be fp32 [M]")
     if row_group is not None:
         _i32(row_group)
@@ -402,9 +403,14 @@ def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=No
     cand_val = torch.full((M, cap), float("-inf"), dtype=torch.float32, device=A.device)
     cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
     cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
-    native().index_scan_candidates_shuf(ptr(A), A.stride(0), ptr(B_shuf), M, int(N), K, ptr(row_group), ptr(q_group),
-                                        ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
+    native().score_candidates_shuf(ptr(A), A.stride(0), ptr(B_shuf), M, int(N), K, ptr(row_group), ptr(q_group),
+                                   ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
     return cand_val, cand_idx, cnt
+
+
+def shuffled_scan_ok(M: int, K: int) -> bool:
+    """Query counts / widths ``score_candidates_shuffled`` serves."""
+    return (1 <= M <= 16 and K % 256 == 0 and K <= 1024) or (32 <= M <= 64 and K % 128 == 0)
 
 
 def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor) -> None:

@@ -488,10 +488,11 @@ def test_score_candidates_exact_set(M):
         torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("M", [1, 5, 16, 37, 64])
 def test_score_candidates_shuffled_exact_set(M):
-    """The persistent scan over a shuffle_weights copy of the rows (index_scan.hip SHUF) appends
-    exactly the filtered scores >= thr[m] (N not a multiple of 32: the copy is zero-padded)."""
+    """The scans over a shuffle_weights copy of the rows (1..16 queries: index_scan.hip SHUF;
+    32..64: the streaming kernel's cfg 12) append exactly the filtered scores >= thr[m] (N not a
+    multiple of 64: the copy is zero-padded)."""
     N, K = 100_004, 768
     A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
     B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
@@ -499,7 +500,7 @@ def test_score_candidates_shuffled_exact_set(M):
     qg = torch.tensor([(-1 if i % 3 == 0 else i % 3) for i in range(M)], device=DEV, dtype=torch.int32)
     full = ops.gemm_bt(A, B, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg)
     thr = torch.quantile(full.clamp_min(-1.0), 0.995, dim=1).contiguous()
-    Bp = torch.zeros((-(-N // 32) * 32, K), dtype=torch.bfloat16, device=DEV)
+    Bp = torch.zeros((-(-N // 64) * 64, K), dtype=torch.bfloat16, device=DEV)
     Bp[:N] = B
     cap = 4096
     cv, ci, cnt = ops.score_candidates_shuffled(A, ops.shuffle_weights(Bp), N, thr, cap, rg, qg)
@@ -522,9 +523,13 @@ def test_index_shuffled_copy_tracks_updates():
     g = torch.Generator(device=DEV).manual_seed(9)
     idx = VectorIndex(dim, DEV, capacity=n + 1000)
     idx.add(torch.arange(n).numpy(), torch.randn(n, dim, device=DEV, generator=g))
-    q = torch.randn(3, dim, device=DEV, generator=g)
+    q = torch.randn(40, dim, device=DEV, generator=g)  # searches of 3 (index_scan) and 40 (stream) queries
 
     def check():
+        check_m(q[:3])
+        check_m(q)
+
+    def check_m(q):
         idx.shuffled_scan = True
         v1, i1, _ = idx.search(q, 100)
         assert idx._shuf is not None
