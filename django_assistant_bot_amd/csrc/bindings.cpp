@@ -149,7 +149,7 @@ PYBIND11_MODULE(_native, m) {
           "gemm_score_candidates");
   });
   // candidates over a shuffle_weights copy of the rows: 1..16 queries on the persistent scan,
-  // 32..64 on the weight-streaming kernel
+  // 17..128 on the weight-streaming kernel
   m.def("score_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
                                     u cnt, u cand_val, u cand_idx, int cap, u s) {
     auto* rg = reinterpret_cast<const int*>(row_group);
@@ -161,7 +161,7 @@ PYBIND11_MODULE(_native, m) {
     int rc = hipErrorInvalidValue;
     if (M <= 16)
       rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
-    else if (M >= 32 && M <= 64)
+    else if (M <= 128)
       rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
     check(rc, "score_candidates_shuf");
   });

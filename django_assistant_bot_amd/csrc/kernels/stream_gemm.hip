@@ -457,8 +457,9 @@ static int stream_candidates_launch(bool shuf, const void* X, long ldx, const vo
                                     const int* row_group, const int* q_group, const float* thr, int* cnt,
                                     float* cand_val, int* cand_idx, int cap, hipStream_t s) {
   constexpr int KS = 128;
-  // M <= 64, BN 64, 4 loader waves: row-major rows (cfg 7) or a shuffle_weights copy (cfg 12)
-  const int CFG = shuf ? 12 : 7;
+  // M <= 64, BN 64, 4 loader waves: row-major rows (cfg 7) or a shuffle_weights copy (cfg 12);
+  // M <= 128 (shuffled copy only): BN 128 (cfg 10, the decode GEMM's)
+  const int CFG = shuf ? (M > 64 ? 10 : 12) : 7;
   if (M <= 0 || N <= 0) return 0;
   if (M > stream_gemm_max_m(CFG) || K % KS || ldx % 8 || ldw % 8 || cap <= 0) return hipErrorInvalidValue;
   if ((long)stream_gemm_bn(CFG) * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;
@@ -481,7 +482,9 @@ static int stream_candidates_launch(bool shuf, const void* X, long ldx, const vo
   p.cand_val = cand_val;
   p.cand_idx = cand_idx;
   p.cap = cap;
-  if (shuf)
+  if (CFG == 10)
+    launch_cfg<10>(p, s, true);
+  else if (CFG == 12)
     launch_cfg<12>(p, s, true);
   else
     launch_cfg<7>(p, s, true);
@@ -495,7 +498,7 @@ int stream_score_candidates(const void* X, long ldx, const void* W, long ldw, in
                                   s);
 }
 
-// W: the rows in the shuffle_weights layout, at least round_up(N, 64) of them
+// W: the rows in the shuffle_weights layout, at least round_up(N, 128) of them (M <= 128)
 int stream_score_candidates_shuf(const void* X, long ldx, const void* W, int M, int N, int K, const int* row_group,
                                  const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
                                  int cap, hipStream_t s) {

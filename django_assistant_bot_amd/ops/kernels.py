@@ -384,15 +384,15 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
 
 
 def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=None):
-    """``score_candidates`` for 1..16 or 32..64 queries over a copy of the rows in the
-    ``shuffle_weights`` layout (``B_shuf`` [R, K], R >= round_up(N, 64), R % 16 == 0): every
-    16-row x 32-k fragment is one coalesced 1 KB load (1..16 queries: the persistent scan of
-    index_scan.hip; 32..64: the weight-streaming kernel's candidate epilogue)."""
+    """``score_candidates`` for 1..128 queries over a copy of the rows in the ``shuffle_weights``
+    layout (``B_shuf`` [R, K], R >= round_up(N, 128), R % 16 == 0): every 16-row x 32-k fragment
+    is one coalesced 1 KB load (1..16 queries: the persistent scan of index_scan.hip; 17..128: the
+    weight-streaming kernel's candidate epilogue)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
     M, K = A.shape
-    expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..16 or 32..64 queries, K ok")
+    expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..128 queries, K % 128 (K % 256, K <= 1024 for <= 16)")
     expect(B_shuf.is_contiguous() and B_shuf.shape[1] == K, "shuffled copy [R, K]")
-    expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 64) * 64, "shuffled copy needs round_up(N, 64) rows")
+    expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 128) * 128, "shuffled copy needs round_up(N, 128) rows")
     expect(thr.dtype == torch.float32 and thr.is_contiguous() and thr.numel() >= M, "thr must be fp32 [M]")
     if row_group is not None:
         _i32(row_group)
@@ -410,7 +410,7 @@ def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=No
 
 def shuffled_scan_ok(M: int, K: int) -> bool:
     """Query counts / widths ``score_candidates_shuffled`` serves."""
-    return (1 <= M <= 16 and K % 256 == 0 and K <= 1024) or (32 <= M <= 64 and K % 128 == 0)
+    return (1 <= M <= 16 and K % 256 == 0 and K <= 1024) or (16 < M <= 128 and K % 128 == 0)
 
 
 def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor) -> None:
