@@ -380,6 +380,10 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {16, 1, 1, 2, 3, 2, true, 0, 4},  // 25: BN 64, 4 + 2 waves
     {16, 2, 1, 2, 2, 2, true, 0, 4},  // 26: BN 128, RT 2, 2-stage weight ring
     {16, 1, 2, 2, 4, 2, true, 0, 8},  // 27: BN 64, 2 k-groups x 4 row groups, 8 + 2 waves
+    // M <= 128, BN 192 (6 compute waves x RT 2, 2 waves per SIMD): 2/3 of cfg 10's X staging per
+    // weight byte (LM head: 128256 = 668 x 192)
+    {8, 2, 1, 4, 3, 2, true, 0, 6},  // 28: 6 + 2 waves
+    {8, 2, 1, 4, 2, 2, true, 0, 6},  // 29: = 28 with a 2-stage weight ring
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 

@@ -136,7 +136,9 @@ class LlamaModel:
     # make exactly 256 workgroups where BN 128 left 32 of the 256 CUs idle: 54.9 -> 51.5 us cold
     # (kernel_bench stream).  qkv at 96 rows x 4 K-slices (cfg 21, also 256 workgroups) measured
     # slower than BN 128 x 4 (17.1 vs 15.8 us) and stays on cfg 10.  DAB_STREAM_WIDE=0: BN 128 (A/B).
-    STREAM_WIDE = {"gate_up": 20}
+    # The LM head at M 65..128 uses 192-row tiles (6 compute waves): 2/3 of the X staging per
+    # weight byte, 228.7 -> 221.3 us (kernel_bench stream lm_head, cold weights).
+    STREAM_WIDE = {"gate_up": 20, "lm_head": 28}
     _wide = os.environ.get("DAB_STREAM_WIDE", "1") != "0"
 
     @staticmethod

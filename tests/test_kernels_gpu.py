@@ -289,7 +289,7 @@ def test_skinny_gemm(M, N, K, S):
         close(ops.skinny_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", list(range(17)) + [20, 21, 22, 23, 25, 27])
+@pytest.mark.parametrize("cfg", list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29])
 @pytest.mark.parametrize("M", [1, 37, 64, 100, 128, 200, 256])
 @pytest.mark.parametrize("N,K,S", [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1),
                                    (672, 512, 1), (1344, 1024, 4), (2688, 1792, 7)])
