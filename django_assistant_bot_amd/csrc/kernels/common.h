@@ -72,6 +72,11 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return x >= 0.f ? x - c : c;
 }
 
+// SiLU x / (1 + e^-x) with one v_rcp_f32 instead of the IEEE division (a ~10-instruction
+// div_scale / div_fmas / div_fixup sequence per element in the SwiGLU epilogues); the reciprocal's
+// 1-ulp error is far below the bf16 rounding of the result.  x -> -inf: rcp(inf) = 0 -> -0.
+__device__ __forceinline__ float silu_f(float x) { return x * __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, c
       unpack8(xr[c + fvec], u);
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+    for (int j = 0; j < 8; ++j) o[j] = silu_f(g[j]) * u[j];
     reinterpret_cast<u32x4*>(out + r * F)[c] = pack8(o);
   }
 }

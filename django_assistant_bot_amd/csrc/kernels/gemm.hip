@@ -150,7 +150,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
             gt += bf2f(p.bias[ng + r]);
             up += bf2f(p.bias[ng + 16 + r]);
           }
-          o[r] = gt / (1.f + __expf(-gt)) * up;
+          o[r] = silu_f(gt) * up;
         }
         u32x2 v;
         v[0] = pack2bf(o[0], o[1]);

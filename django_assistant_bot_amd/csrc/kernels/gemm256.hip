@@ -400,7 +400,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
                 gt += bg[jh][r];
                 up += bu[jh][r];
               }
-              o[r] = gt / (1.f + __expf(-gt)) * up;
+              o[r] = silu_f(gt) * up;
             }
             u32x2 v;
             v[0] = pack2bf(o[0], o[1]);

@@ -316,7 +316,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
       const f32x4 gt = tile4(m, 2 * hg * i + j0), up = tile4(m, 2 * hg * i + hg + j0);
       float o[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) o[j] = gt[j] / (1.f + __expf(-gt[j])) * up[j];
+      for (int j = 0; j < 4; ++j) o[j] = silu_f(gt[j]) * up[j];
       u32x2 v;
       v[0] = pack2bf(o[0], o[1]);
       v[1] = pack2bf(o[2], o[3]);
