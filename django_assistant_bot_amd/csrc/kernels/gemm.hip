@@ -204,7 +204,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
         if (p.residual) {
           const bf16* rr = p.residual + (size_t)m * p.ldr + n;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] += bf2f(rr[r]);
+          for (int r = 0; r < 4; ++r) o[r] = (p.out_f32 ? o[r] : bf2f(f2bf(o[r]))) + bf2f(rr[r]);  // bf16 GEMM + add
         }
       }
       if (p.out_f32) {

@@ -457,9 +457,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             if constexpr (RES) {
               const u32x4 rv = __builtin_amdgcn_raw_buffer_load_b128(rR, (unsigned)((mr * p.ldr + nc) * 2), 0, 0);
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                o[2 * q] += __uint_as_float(rv[q] << 16);
-                o[2 * q + 1] += __uint_as_float(rv[q] & 0xffff0000u);
+              for (int q = 0; q < 4; ++q) {  // round like a bf16 GEMM output, then the bf16 add (HF)
+                o[2 * q] = bf2f(f2bf(o[2 * q])) + __uint_as_float(rv[q] << 16);
+                o[2 * q + 1] = bf2f(f2bf(o[2 * q + 1])) + __uint_as_float(rv[q] & 0xffff0000u);
               }
             }
             u32x4 v;

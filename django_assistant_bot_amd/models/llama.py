@@ -231,14 +231,24 @@ class LlamaModel:
         residual = None
         for li, L in enumerate(self.layers):
             x, residual = self._layer(li, L, x, residual, meta, kv, sk)
-        out, _ = ops.rmsnorm(x, self.final_norm, cfg.eps, residual=residual)
-        return out
+        return self._final_norm(x, residual)
+
+    def _final_norm(self, x, residual):
+        if x is None:  # the residual stream already holds the last projection (fused prefill add)
+            return ops.rmsnorm(residual, self.final_norm, self.cfg.eps)[0]
+        return ops.rmsnorm(x, self.final_norm, self.cfg.eps, residual=residual)[0]
 
     def _layer(self, li: int, L: DecoderLayer, x, residual, meta: AttnMeta, kv: KVCache, sk: bool):
         """One decoder layer: (layer input, residual stream) -> (next layer input, residual stream)."""
         cfg, D, T = self.cfg, self.cfg.head_dim, meta.positions.numel()  # x may be [S, T, H] split-K slabs
         slabs_ok = self.tp_size == 1  # under TP the partial sums go through the all-reduce as bf16
-        if residual is None:
+        # prefill (TP 1): the o / down GEMMs add the residual in their epilogue (gemm256 RES, rounded
+        # like the separate bf16 add), so the RMSNorms read and write one tensor instead of two each;
+        # x is None then: the residual stream already holds the layer input
+        fuse = not sk and self.tp_size == 1 and (x if x is not None else residual).is_cuda
+        if x is None:
+            h, _ = ops.rmsnorm(residual, L.attn_norm, cfg.eps)
+        elif residual is None:
             h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
             residual = x
         else:
@@ -253,8 +263,12 @@ class LlamaModel:
         else:
             a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                           meta.max_q, causal=True)
-        o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
-        h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
+        if fuse:
+            residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual)
+            h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)
+        else:
+            o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o", ws=L.o_ws))
+            h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
         if sk and self.interleaved_mlp and L.gate_up_ws is not None:
             act = ops.stream_gemm(h, L.gate_up_ws, epilogue=ops.EPI_SWIGLU8, nt=True,
                                   cfg=self._stream_cfg("gate_up", T, L.gate_up_ws.shape[0]))
@@ -265,6 +279,8 @@ class LlamaModel:
         else:
             gu = ops.gemm_bt(h, L.gate_up_w) if h.is_cuda else ops.linear(h, L.gate_up_w)
             act = ops.silu_mul(gu, interleaved=self.interleaved_mlp)
+        if fuse:
+            return None, ops.gemm_bt(act, L.down_w, residual=residual)
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down", ws=L.down_ws))
         return x, residual
 
@@ -301,7 +317,7 @@ class LlamaModel:
         outs = []
         for s, (x, residual) in zip(streams, state):
             with torch.cuda.stream(s):
-                outs.append(ops.rmsnorm(x, self.final_norm, self.cfg.eps, residual=residual)[0])
+                outs.append(self._final_norm(x, residual))
         for s, out in zip(streams, outs):
             if s is not main:
                 main.wait_stream(s)

@@ -177,7 +177,9 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
         c = c.view(c.shape[0], N // (2 * hg), 2, hg)
         c = (F.silu(c[:, :, 0]) * c[:, :, 1]).reshape(c.shape[0], N // 2)
     if residual is not None:
-        c = c + residual.float()
+        # a bf16 output is the rounded projection plus the residual, rounded again (HF's
+        # `hidden + dense(x)` in bf16)
+        c = (c if out_f32 else c.to(A.dtype).float()) + residual.float()
     return c if out_f32 else c.to(A.dtype)
 
 
