@@ -63,17 +63,19 @@ class BertEncoder:
         x = ops.bert_embed(ids, pos_ids, None, self.word, self.pos, self.typ, self.eln_g, self.eln_b, cfg.eps)
         for L in self.layers:
             # every projection on the native MFMA GEMM (gemm256 at >= 1024 tokens) with the bias (and
-            # the up projection's GELU) in its epilogue; residual adds fused into the LayerNorm
+            # the up projection's GELU) in its epilogue; the residual adds too (the bf16 projection
+            # plus the residual, rounded: HF's `LayerNorm(dense(x) + input)`), so each LayerNorm reads
+            # one tensor
             qkv = ops.linear(x, L.qkv_w, L.qkv_b)
             q = qkv[:, :H].view(T, nh, D)
             k = qkv[:, H:2 * H].view(T, nh, D)
             v = qkv[:, 2 * H:].view(T, nh, D)
             a = ops.flash_attention_packed(q, k, v, cu_seqlens, cu_seqlens, max_seqlen, causal=False)
-            h = ops.linear(a.view(T, H), L.o_w, L.o_b)
-            x = ops.layernorm(h, L.ln1_g, L.ln1_b, cfg.eps, residual=x)
+            h = ops.linear(a.view(T, H), L.o_w, L.o_b, residual=x)
+            x = ops.layernorm(h, L.ln1_g, L.ln1_b, cfg.eps)
             f = ops.linear(x, L.i_w, L.i_b, act="gelu")  # bias + GELU(erf) epilogue
-            h = ops.linear(f, L.d_w, L.d_b)
-            x = ops.layernorm(h, L.ln2_g, L.ln2_b, cfg.eps, residual=x)
+            h = ops.linear(f, L.d_w, L.d_b, residual=x)
+            x = ops.layernorm(h, L.ln2_g, L.ln2_b, cfg.eps)
         return x
 
     def encode(self, ids, pos_ids, cu_seqlens, max_seqlen, normalize=None, want_bf16=False):
