@@ -86,6 +86,10 @@ class _Req:
         return self.prompt + self.out if self.preempted else self.prompt
 
 
+# DAB_PREFILL_DEFER=0: read every prefill chunk's tokens back before the next launch (A/B runs)
+_DEFER_PREFILL = os.environ.get("DAB_PREFILL_DEFER", "1") != "0"
+
+
 def _bucket_sizes(max_batch):
     b = [1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384, 448, 512]
     return [x for x in b if x < max_batch] + [max_batch]
@@ -204,6 +208,9 @@ class LLMEngine:
                        for k in ("_h_ids", "_h_pos", "_h_slots", "_h_ctx", "_h_bt", "_h_temp", "_h_topk", "_h_topp",
                                  "_h_cnt", "_h_tokens", "_h_order")}
         self._inflight = None  # launched decode step whose tokens are not consumed yet
+        # launched prefill chunk whose sampled first tokens are not read back yet (GPU): the next
+        # chunk is launched before they are, so consecutive chunks run back to back
+        self._pending_prefill = None
         max_parts = math.ceil(self.max_model_len / part_size)
         self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
             else None
@@ -275,6 +282,16 @@ class LLMEngine:
             self.fault_hook(self)
         if self.auto_expire:
             self.expire_deadlines()
+        if self._pending_prefill is not None:
+            # another plain prefill chunk goes onto the GPU before the previous one's tokens are read
+            chunks = self._schedule_prefill() if not self.running or self.mixed_prefill_tokens <= 0 else []
+            if chunks:
+                prev, self._pending_prefill = self._pending_prefill, None
+                self._run_prefill(chunks)
+                self._finish_prefill(prev)
+                return [k for k in self.finished if k not in done_before]
+            self._finish_prefill(self._pending_prefill)
+            self._pending_prefill = None
         if self._inflight is not None and not self._can_pipeline():
             self._finish_inflight()
         if self._can_pipeline():
@@ -303,6 +320,9 @@ class LLMEngine:
         its output (tokens so far) is kept under ``finish_reason=reason``."""
         if self._inflight is not None:
             self._finish_inflight()
+        if self._pending_prefill is not None:
+            pend, self._pending_prefill = self._pending_prefill, None
+            self._finish_prefill(pend)
         for q in (self.waiting, self.prefilling, self.running):
             for r in q:
                 if r.rid == rid:
@@ -321,6 +341,7 @@ class LLMEngine:
         pool is rebuilt so nothing leaks if the fault left the bookkeeping half-updated."""
         ids = [r.rid for q in (self.waiting, self.prefilling, self.running) for r in q]
         self._inflight = None
+        self._pending_prefill = None
         self.waiting.clear()
         self.prefilling.clear()
         self.running.clear()
@@ -426,18 +447,31 @@ class LLMEngine:
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
         self.stats["prefill_tokens"] += T
         self.stats["prefill_steps"] += 1
+        reqs, toks = [], []
         if last_rows:
             sel = torch.as_tensor([int(cu[i + 1]) - 1 for i in last_rows], dtype=torch.long).to(dev)
             logits = self.model.logits(hidden.index_select(0, sel))
             reqs = [chunks[i][0] for i in last_rows]
-            toks = self._sample(logits, reqs)
-        self._collect_gpu_times(block=bool(last_rows))
+            toks = self._sample(logits, reqs, to_host=not self.is_gpu)
         for r, s, n in chunks:
             r.computed = s + n
+        pend = (chunks, reqs, toks, t0)
+        if self.is_gpu and _DEFER_PREFILL:
+            self._pending_prefill = pend  # read back after the next launch (step)
+        else:
+            self._finish_prefill(pend)
+
+    def _finish_prefill(self, pend):
+        """Reads a launched prefill chunk's sampled first tokens (device -> host) and moves the
+        sequences whose prompt it completed to the running set."""
+        chunks, reqs, toks, t0 = pend
+        if torch.is_tensor(toks):
+            toks = toks.cpu().tolist()
+        self._collect_gpu_times(block=bool(reqs))
         now = time.perf_counter()
         for r, s, n in chunks:
             r.prefill_s += now - t0
-        if last_rows:
+        if reqs:
             for r, t in zip(reqs, toks):
                 self.blocks.commit_prefix(r.seq, len(r.full_prompt()))
                 self.prefilling.remove(r)
@@ -523,7 +557,7 @@ class LLMEngine:
             key = f"gpu_{name}_ms"
             self.stats[key] = self.stats.get(key, 0.0) + ms
 
-    def _sample(self, logits, reqs):
+    def _sample(self, logits, reqs, to_host: bool = True):
         n = len(reqs)
         temps = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in reqs], dtype=torch.float32)
         topk = torch.tensor([r.params.top_k for r in reqs], dtype=torch.int32)
@@ -535,7 +569,7 @@ class LLMEngine:
                        or r.params.temperature <= 0 for r in reqs)
             toks = ops.sample_tokens(logits, temps.to(d), topk.to(d), topp.to(d), self.seed, cnt.to(d), fast=fast)
             toks = self._tp_sync_tokens(toks)
-            return toks.cpu().tolist()
+            return toks.cpu().tolist() if to_host else toks
         g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
         return ops.sample_tokens(logits, temps, topk, topp, self.seed, cnt, generator=g).tolist()
 
