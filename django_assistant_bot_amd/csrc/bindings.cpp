@@ -108,6 +108,17 @@ PYBIND11_MODULE(_native, m) {
                                      (const int*)ctx_k, batch, max_sq, Hq, Hkv, D, causal, paged, scale, ST(s)),
                 "flash_attention");
         });
+  // Llama prefill attention with RoPE applied to Q on load (positions int32 [Tq], cos/sin table)
+  m.def("flash_attention_rope",
+        [](u q, long qst, long qsh, u kc, u vc, u bt, int max_blocks, int bs, u out, long ost, long osh, u cu_q,
+           u ctx_k, int batch, int max_sq, int Hq, int Hkv, int D, int causal, float scale, u rope_pos, u rope_cs,
+           u s) {
+          check(dab::flash_attention(CVP(q), qst, qsh, nullptr, nullptr, 0, 0, CVP(kc), CVP(vc), (const int*)bt,
+                                     max_blocks, bs, VP(out), ost, osh, (const int*)cu_q, nullptr, (const int*)ctx_k,
+                                     batch, max_sq, Hq, Hkv, D, causal, 1, scale, ST(s), (const int*)rope_pos,
+                                     CVP(rope_cs)),
+                "flash_attention_rope");
+        });
   // HIP stream restricted to a set of CUs (bit i of the mask words = CU i): lets a compute-bound
   // workload run beside a bandwidth-bound one on disjoint CUs (benchmarks/overlap_probe.py).  The
   // handle is wrapped by torch.cuda.ExternalStream; destroy it with destroy_stream.

@@ -56,6 +56,10 @@ struct FlashParams {
   const int* ctx_k;
   int Hq, Hkv;
   float scale_log2;
+  // flash_d128 only: rotate Q by RoPE on load (positions of the packed query tokens, [max_pos, 64]
+  // float2 cos/sin table), when the RoPE/KV-write kernel wrote only K / V
+  const int* rope_pos;
+  const float2* rope_cs;
 };
 
 // One workgroup = 16 QT NW queries (NW waves x QT 16-query sub-tiles) of one (sequence, head);
@@ -384,6 +388,25 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
     for (int st = 0; st < 8; ++st) {
       const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
       qf[st] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
+    }
+    if (p.rope_cs && q_valid) {
+      // dims 16 st + 8 hi + j (st < 4) pair with the same lane's dims + 64 (st + 4)
+      const float4* csp = reinterpret_cast<const float4*>(p.rope_cs + (size_t)p.rope_pos[q_start + my_q] * 64);
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        float4 c4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) c4[e] = csp[(16 * st + 8 * hi) / 2 + e];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 cc = c4[j >> 1];
+          const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
+          float x1 = bf2f((uint16_t)qf[st][j]), x2 = bf2f((uint16_t)qf[st + 4][j]);
+          rope_rot(x1, x2, cs);
+          qf[st][j] = (short)f2bf(x1);
+          qf[st + 4][j] = (short)f2bf(x2);
+        }
+      }
     }
   }
 
@@ -889,10 +912,13 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     long kv_stride_tok, long kv_stride_head, const void* k_cache, const void* v_cache,
                     const int* block_tables, int max_blocks, int block_size, void* out, long o_stride_tok,
                     long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
-                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s) {
+                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s,
+                    const int* rope_pos, const void* rope_cs) {
   if (batch <= 0 || max_seqlen_q <= 0) return 0;
   if (Hq % Hkv || (paged && block_size % 64)) return hipErrorInvalidValue;
   FlashParams prm;
+  prm.rope_pos = rope_pos;
+  prm.rope_cs = (const float2*)rope_cs;
   prm.q = (const bf16*)q;
   prm.q_stride_tok = q_stride_tok;
   prm.q_stride_head = q_stride_head;
@@ -933,6 +959,7 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     else hipLaunchKernelGGL((flash_d128_kernel<false>), g32, dim3(256), 0, s, prm);
     return hipGetLastError();
   }
+  if (rope_cs) return hipErrorInvalidValue;  // Q RoPE lives only in the D = 128 paged kernel above
   const int var = variant >= 0 ? variant : (D == 128 ? 1 : 2);
   const bool wide = max_seqlen_q > 64 && var != 2;
   const int qb = wide ? 128 : 64;

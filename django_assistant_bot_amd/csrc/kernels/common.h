@@ -127,6 +127,15 @@ __device__ __forceinline__ float key_float(uint32_t k) {
   return __uint_as_float(u);
 }
 
+// Rotate-half RoPE of the pair (x1 = dim i, x2 = dim i + D/2) by (cos, sin): explicit FMAs, so the
+// RoPE/KV-write kernel and the prefill attention's Q prologue round identically.
+__device__ __forceinline__ void rope_rot(float& x1, float& x2, const float2 cs) {
+  const float o1 = fmaf(x1, cs.x, -(x2 * cs.y));
+  const float o2 = fmaf(x2, cs.x, x1 * cs.y);
+  x1 = o1;
+  x2 = o2;
+}
+
 // One 8-dim chunk pair (dims i0..i0+7 and i0+D/2..) of head `h` of token `t` of a QKV projection,
 // with rotate-half RoPE applied when `rotate`: the shared body of rope_kv_kernel and of the fused
 // decode-attention prologue (bitwise the same result in both).  The projection is either bf16 rows
@@ -188,13 +197,7 @@ __device__ __forceinline__ void rope_chunk(const bf16* __restrict__ qkv, const f
   }
   if (rotate) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float2 v = cs[j];
-      const float o1 = x1[j] * v.x - x2[j] * v.y;
-      const float o2 = x2[j] * v.x + x1[j] * v.y;
-      x1[j] = o1;
-      x2[j] = o2;
-    }
+    for (int j = 0; j < 8; ++j) rope_rot(x1[j], x2[j], cs[j]);
   }
 }
 

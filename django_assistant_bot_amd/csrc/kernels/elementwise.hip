@@ -63,13 +63,15 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
                                                       long slab_stride) {
   const int per_head = D >> 4;  // threads per head
   const int heads = Hq + 2 * Hkv;
-  const size_t total = (size_t)T * heads * per_head;
+  const int h0 = q_out ? 0 : Hq;  // no q output: k / v heads only (the attention rotates q itself)
+  const int hrun = heads - h0;
+  const size_t total = (size_t)T * hrun * per_head;
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const int c = (int)(idx % per_head);
   const size_t th = idx / per_head;
-  const int h = (int)(th % heads);
-  const int t = (int)(th / heads);
+  const int h = h0 + (int)(th % hrun);
+  const int t = (int)(th / hrun);
   const int half = D >> 1;
   const int i0 = c * 8;
   // rotation and cache slot first (pos -> cos/sin is a dependent chain): their round trips overlap
@@ -123,7 +125,7 @@ int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos
                   const float* slabs, int S, long slab_stride) {
   if (T <= 0) return 0;
   if (D % 16 || ld % 8 || (slabs && (S < 1 || slab_stride % 4))) return hipErrorInvalidValue;
-  const size_t total = (size_t)T * (Hq + 2 * Hkv) * (D / 16);
+  const size_t total = (size_t)T * (q_out ? Hq + 2 * Hkv : 2 * Hkv) * (D / 16);
   hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const bf16*)qkv, ld,
                      positions, (const float2*)cos_sin, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, slots, T, Hq,
                      Hkv, D, block_size, slabs, S, slab_stride);

@@ -38,7 +38,8 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     long kv_stride_tok, long kv_stride_head, const void* k_cache, const void* v_cache,
                     const int* block_tables, int max_blocks, int block_size, void* out, long o_stride_tok,
                     long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
-                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s);
+                    int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s,
+                    const int* rope_pos = nullptr, const void* rope_cs = nullptr);
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,

@@ -254,6 +254,16 @@ class LlamaModel:
         else:
             h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
         qkv = self._proj(h, L.qkv_w, sk, name="qkv", ws=L.qkv_ws)
+        if (not meta.decode and not meta.n_decode and qkv.is_cuda and qkv.dtype == torch.bfloat16
+                and ops.kernels.flash_rope_ok(D, kv.block_size)):
+            # prefill: the RoPE/KV-write kernel writes only K / V; the attention rotates Q on load
+            # straight from the projection (a [T, Hq*D] write and read less per layer)
+            ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D,
+                              write_q=False)
+            q = qkv[:, :self.hq * D].view(T, self.hq, D)
+            a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
+                                          meta.max_q, causal=True, rope=(meta.positions, self.cos_sin))
+            return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D)
         q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
         if meta.decode:
             a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
@@ -263,6 +273,11 @@ class LlamaModel:
         else:
             a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                           meta.max_q, causal=True)
+        return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D)
+
+    def _layer_tail(self, li, L, a, residual, meta, sk, fuse, slabs_ok, T, D):
+        """o projection, MLP norm, gate_up (+SwiGLU), down: -> (next layer input, residual stream)."""
+        cfg = self.cfg
         if fuse:
             residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual)
             h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)

@@ -151,10 +151,12 @@ def silu_mul(x, interleaved=False):
     return out
 
 
-def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D):
+def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, write_q=True):
     """Applies RoPE to the q/k heads of ``qkv`` [T, (Hq+2Hkv)*D]; writes k, v into the paged caches
     [num_blocks, Hkv, block_size, D] at ``slots`` (int64, <0 skipped); returns q [T, Hq, D].
-    ``qkv`` may also be fp32 split-K slabs [S, T, (Hq+2Hkv)*D], summed inside the kernel."""
+    ``qkv`` may also be fp32 split-K slabs [S, T, (Hq+2Hkv)*D], summed inside the kernel.
+    ``write_q=False`` (bf16 ``qkv``): k / v only, returns None (the prefill attention rotates q on
+    load: ``flash_attention_paged(..., rope=...)``)."""
     block_size = k_cache.shape[2]
     slabs = qkv.dtype == torch.float32 and qkv.dim() == 3
     if not qkv.is_cuda:
@@ -170,6 +172,12 @@ def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D):
     expect(positions.numel() == T and slots.numel() == T, "positions / slots length mismatch")
     expect(tuple(k_cache.shape[1:]) == (Hkv, block_size, D) and k_cache.shape == v_cache.shape, "cache shape mismatch")
     expect(cos_sin.shape[1] == D // 2, "cos/sin table width mismatch")
+    if not write_q:
+        expect(not slabs, "write_q=False needs a bf16 qkv")
+        expect_bf16_contig(qkv)
+        native().rope_kv_write(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), 0, ptr(k_cache),
+                               ptr(v_cache), ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv))
+        return None
     q = torch.empty((T, Hq, D), dtype=torch.bfloat16, device=qkv.device)
     if slabs:
         expect(qkv.is_contiguous(), "slabs must be contiguous")
@@ -219,13 +227,24 @@ def flash_attention_packed(q, k, v, cu_q, cu_k, max_seqlen_q, causal=False, scal
     return out
 
 
+def flash_rope_ok(D: int, block_size: int) -> bool:
+    """Whether flash_attention_paged can rotate q itself (the 32x32 D = 128 kernel's Q prologue)."""
+    return D == 128 and block_size % 64 == 0 and not os.environ.get("DAB_FLASH_VARIANT")
+
+
 def flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_seqlen_q, causal=True, scale=None,
-                          out=None):
+                          out=None, rope=None):
     """Prefill attention: q [Tq, Hq, D] packed by cu_q, keys/values of each sequence are its first
-    ctx_lens[b] tokens in the paged caches (the query chunk is the tail of that context)."""
+    ctx_lens[b] tokens in the paged caches (the query chunk is the tail of that context).
+    ``rope=(positions int32 [Tq], cos_sin [max_pos, D/2, 2] fp32)``: q is the un-rotated projection
+    and RoPE is applied on load (``flash_rope_ok``)."""
     D = q.shape[-1]
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if not q.is_cuda:
+        if rope is not None:
+            pos, cs = rope
+            T, Hq = q.shape[0], q.shape[1]
+            q = ref.rope_q(q.reshape(T, Hq, D), pos, cs)
         return ref.flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, causal, scale)
     _i32(cu_q)
     _i32(ctx_lens)
@@ -237,6 +256,16 @@ def flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max
     out = torch.empty((q.shape[0], Hq, D), dtype=q.dtype, device=q.device) if out is None else out
     B = cu_q.numel() - 1
     expect(block_tables.shape[0] >= B and ctx_lens.numel() >= B, "block table / ctx_lens rows < batch")
+    if rope is not None:
+        pos, cs = rope
+        _i32(pos)
+        expect(flash_rope_ok(D, bs) and cs.dtype == torch.float32 and cs.is_contiguous() and pos.numel() == q.shape[0],
+               "q RoPE in the attention needs D 128, block size % 64, fp32 cos/sin and one position per query")
+        native().flash_attention_rope(ptr(q), qst, qsh, ptr(k_cache), ptr(v_cache), ptr(block_tables),
+                                      block_tables.shape[1], bs, ptr(out), out.stride(0), out.stride(1), ptr(cu_q),
+                                      ptr(ctx_lens), B, int(max_seqlen_q), Hq, Hkv, D, int(bool(causal)),
+                                      float(scale), ptr(pos), ptr(cs), stream(q))
+        return out
     native().flash_attention(ptr(q), qst, qsh, 0, 0, 0, 0, ptr(k_cache), ptr(v_cache), ptr(block_tables),
                              block_tables.shape[1], bs, ptr(out), out.stride(0), out.stride(1), ptr(cu_q), 0,
                              ptr(ctx_lens), B, int(max_seqlen_q), Hq, Hkv, D, int(bool(causal)), 1, float(scale),

@@ -91,6 +91,17 @@ def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, 
     return q.contiguous()
 
 
+def rope_q(q, positions, cos_sin):
+    """Rotate-half RoPE of q [T, Hq, D] at ``positions`` (what rope_kv_write returns as q)."""
+    D = q.shape[-1]
+    half = D // 2
+    cs = cos_sin[positions.long()]
+    cos, sin = cs[..., 0].unsqueeze(1), cs[..., 1].unsqueeze(1)
+    x = q.float()
+    x1, x2 = x[..., :half], x[..., half:]
+    return torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(q.dtype)
+
+
 def _attend(q, k, v, scale, causal, q_offset):
     # q [Sq, H, D], k/v [Sk, Hkv, D] -> [Sq, H, D] (fp32 math)
     H, Hkv = q.shape[1], k.shape[1]

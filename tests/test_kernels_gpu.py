@@ -553,6 +553,38 @@ def test_index_shuffled_copy_tracks_updates():
     check()
 
 
+@pytest.mark.parametrize("lens", [[700, 129, 1], [1000]])
+def test_flash_rope_on_load_matches_rope_kernel(lens):
+    """Prefill with Q rotated inside the attention (rope_kv_write(write_q=False) + flash(rope=...))
+    equals RoPE/KV-write's rotated q fed to the same attention, bit for bit; the caches match too."""
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    T = sum(lens)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV, generator=g).to(torch.bfloat16)
+    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).to(DEV)
+    inv = ref.llama3_inv_freq(D, 500000.0, None)
+    cs = ref.rope_cos_sin(inv, 4096).to(DEV)
+    nblk = [-(-n // bs) for n in lens]
+    bt = torch.zeros((len(lens), max(nblk)), dtype=torch.int32)
+    slots, b0 = [], 0
+    for i, (n, nb) in enumerate(zip(lens, nblk)):
+        bt[i, :nb] = torch.arange(b0, b0 + nb, dtype=torch.int32)
+        slots.append(b0 * bs + torch.arange(n))
+        b0 += nb
+    bt, slots = bt.to(DEV), torch.cat(slots).to(DEV)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctx = torch.tensor(lens, dtype=torch.int32, device=DEV)
+    caches = [(torch.zeros(b0, Hkv, bs, D, dtype=torch.bfloat16, device=DEV),
+               torch.zeros(b0, Hkv, bs, D, dtype=torch.bfloat16, device=DEV)) for _ in range(2)]
+    q = ops.rope_kv_write(qkv, pos, cs, caches[0][0], caches[0][1], slots, Hq, Hkv, D)
+    a = ops.flash_attention_paged(q, caches[0][0], caches[0][1], bt, cu, ctx, max(lens))
+    assert ops.rope_kv_write(qkv, pos, cs, caches[1][0], caches[1][1], slots, Hq, Hkv, D, write_q=False) is None
+    b = ops.flash_attention_paged(qkv[:, :Hq * D].view(T, Hq, D), caches[1][0], caches[1][1], bt, cu, ctx, max(lens),
+                                  rope=(pos, cs))
+    assert torch.equal(caches[0][0], caches[1][0]) and torch.equal(caches[0][1], caches[1][1])
+    assert torch.equal(a, b)
+
+
 def test_index_threshold_search_overflow_falls_back():
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
