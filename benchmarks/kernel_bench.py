@@ -207,6 +207,16 @@ def attn_suite():
     t = timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True))
     flop = 4.0 * B * Hq * T * T * D / 2
     emit(op="flash-prefill-causal", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    # the model's prefill form: q read from the qkv projection (row stride (Hq + 2 Hkv) D), without
+    # and with RoPE applied on load
+    qkv = torch.randn(B * T, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
+    qs = qkv[:, :Hq * D].view(B * T, Hq, D)
+    pos = torch.arange(T, dtype=torch.int32, device="cuda").repeat(B)
+    cs = ops.reference.rope_cos_sin(ops.reference.llama3_inv_freq(D, 500000.0, None), 8192).cuda()
+    t = timeit(lambda: ops.flash_attention_paged(qs, kc, vc, bt, cu, ctx, T, causal=True))
+    emit(op="flash-prefill-causal-qkv-strided", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    t = timeit(lambda: ops.flash_attention_paged(qs, kc, vc, bt, cu, ctx, T, causal=True, rope=(pos, cs)))
+    emit(op="flash-prefill-causal-rope", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
     # encoder: 256 x 128 tokens, bge-base heads (packed)
     B2, T2, H2, D2 = 256, 128, 12, 64
     qkv = torch.randn(B2 * T2, 3 * H2 * D2, device="cuda").to(torch.bfloat16)

@@ -389,26 +389,32 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
       const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
       qf[st] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
     }
-    if (p.rope_cs && q_valid) {
-      // dims 16 st + 8 hi + j (st < 4) pair with the same lane's dims + 64 (st + 4)
-      const float4* csp = reinterpret_cast<const float4*>(p.rope_cs + (size_t)p.rope_pos[q_start + my_q] * 64);
+  }
+  // RoPE of Q on load (rope_cs): dims 16 st + 8 hi + j (st < 4) pair with the same lane's dims + 64
+  // (st + 4).  Applied after the first K/V tile's DMA is issued, so its loads and math overlap it.
+  const bool rope_q = p.rope_cs && q_valid;
+  // cos/sin rows through a wave-uniform buffer descriptor (empty range without RoPE: the loads
+  // return zeros and touch nothing), so the loads are unconditional and hipcc's wait counting stays
+  // exact across them (a conditional load made it drain the first tile's DMA)
+  const int cs_row = p.rope_cs ? p.rope_pos[q_start + (q_valid ? my_q : 0)] : 0;
+  const auto cs_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.rope_cs ? (const void*)p.rope_cs : (const void*)p.q),
+                                                       (short)0, p.rope_cs ? 0x7ffffff0 : 0, 0x00020000);
+  float4 c4[4][4];
+  auto apply_rope = [&]() DAB_ALWAYS_INLINE {
+    if (!rope_q) return;
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        float4 c4[4];
+    for (int st = 0; st < 4; ++st) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) c4[e] = csp[(16 * st + 8 * hi) / 2 + e];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 cc = c4[j >> 1];
-          const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
-          float x1 = bf2f((uint16_t)qf[st][j]), x2 = bf2f((uint16_t)qf[st + 4][j]);
-          rope_rot(x1, x2, cs);
-          qf[st][j] = (short)f2bf(x1);
-          qf[st + 4][j] = (short)f2bf(x2);
-        }
+      for (int j = 0; j < 8; ++j) {
+        const float4 cc = c4[st][j >> 1];
+        const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
+        float x1 = bf2f((uint16_t)qf[st][j]), x2 = bf2f((uint16_t)qf[st + 4][j]);
+        rope_rot(x1, x2, cs);
+        qf[st][j] = (short)f2bf(x1);
+        qf[st + 4][j] = (short)f2bf(x2);
       }
     }
-  }
+  };
 
   int n_keys = kv_len;
   if (CAUSAL) {
@@ -572,7 +578,16 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
 
   // One tile in flight: tile t + 1 is requested once tile t has landed and streams in under tile
   // t's math.
+  // the cos/sin loads go out after the block-table loads and before the first DMA, so the waits
+  // for them neither drain the DMA nor wait behind it
+#pragma unroll
+  for (int st = 0; st < 4; ++st)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      c4[st][e] = __builtin_bit_cast(
+          float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
   if (n_tiles > 0) issue(0, 0, blk_of(0));
+  apply_rope();
   for (int t = 0; t < n_tiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < n_tiles) {
