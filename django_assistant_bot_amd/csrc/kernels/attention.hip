@@ -345,6 +345,8 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
+constexpr float kDeferLog2 = 8.f;  // flash_d128: rescale only when a row maximum grows by > 2^8
+
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
   constexpr int D = 128, KT = 64, QB = 128;
@@ -532,7 +534,13 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx * sc);
+    // Deferred rescale (cdna_hip_programming.md T13): while no query of the wave sees its maximum
+    // grow by more than kDeferLog2 (log2 units) the running maximum stays, P reaches at most
+    // 2^kDeferLog2 (exact in bf16 up to the usual 8-bit mantissa) and the O / l rescale is skipped;
+    // the decision is taken before this tile's P is exponentiated, so nothing is scaled twice.
+    const float mxs = mx * sc;
+    const bool keep = __all(mxs - m_run <= kDeferLog2);
+    const float m_new = keep ? m_run : fmaxf(m_run, mxs);
     // raw v_exp_f32 (exp2f adds a denormal-range fix-up around each one; results below 2^-126 are
     // irrelevant next to the row maximum's 1)
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
@@ -545,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
     }
     l_run = l_run * alpha + ls;
     m_run = m_new;
-    if (__any(alpha < 1.f)) {  // the running max moved for some query of the wave
+    if (!keep && __any(alpha < 1.f)) {  // the running max moved for some query of the wave
 #pragma unroll
       for (int db = 0; db < 4; ++db) o[db] *= alpha;
     }
