@@ -183,6 +183,47 @@ def test_flash_paged_prefill(causal):
     close(out, exp)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_flash_paged_prefill_forced_rescales(causal):
+    """The deferred online-softmax rescale (flash_d128, running max kept until a row maximum grows
+    by > 2^8) against a full-tensor fp64 reference, with spikes that force both branches: single
+    keys aligned with single query rows raise those rows' scores at chosen tiles by +3 (stays under
+    the threshold: P up to ~2^4.3 without a rescale) or by +12 / +30 (forces the rescale), in
+    different waves and 32-query blocks, the rest of each wave unchanged."""
+    ctx = [700, 300]
+    qlen = [700, 300]
+    Hq, Hkv, D, bs = 8, 2, 128, 64
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 32)
+    q = bf(sum(qlen), Hq, D, scale=0.5)
+    kc.mul_(0.5)
+    btc = bt.cpu()
+    # (sequence, query index, key index, score jump in natural-log units)
+    spikes = [(0, 650, 70, 3.0), (0, 650, 400, 30.0), (0, 300, 130, 12.0), (0, 40, 10, 30.0), (0, 699, 690, 12.0),
+              (1, 250, 200, 3.0), (1, 251, 5, 30.0), (1, 90, 64, 12.0)]
+    for si, qi, kj, jump in spikes:
+        row = sum(qlen[:si]) + qi
+        blk, off = int(btc[si, kj // bs]), kj % bs
+        for hk in range(Hkv):
+            h = hk * (Hq // Hkv)  # the group's first query head gets the exact jump, the others a side effect
+            qv = q[row, h].float()
+            kc[blk, hk, off] = (qv * (jump * math.sqrt(D) / qv.pow(2).sum())).to(torch.bfloat16)
+    cu = torch.tensor([0] + list(torch.tensor(qlen).cumsum(0)), dtype=torch.int32, device=DEV)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(qlen), causal=causal)
+    assert torch.isfinite(out.float()).all()
+    o0 = 0
+    for b, (n, m) in enumerate(zip(ctx, qlen)):  # fp64 reference over the whole output
+        ks = ref.gather_paged(kc, bt[b], n).double().repeat_interleave(Hq // Hkv, dim=1)
+        vs = ref.gather_paged(vc, bt[b], n).double().repeat_interleave(Hq // Hkv, dim=1)
+        sc = torch.einsum("qhd,khd->hqk", q[o0:o0 + m].double(), ks) / math.sqrt(D)
+        if causal:
+            qi = torch.arange(m, device=DEV)[:, None] + (n - m)
+            sc = sc.masked_fill(torch.arange(n, device=DEV)[None, :] > qi, float("-inf"))
+        exp = torch.einsum("hqk,khd->qhd", sc.softmax(-1), vs)
+        close(out[o0:o0 + m], exp.float(), atol=2e-2, rtol=2e-2)
+        o0 += m
+
+
 @pytest.mark.parametrize("Hq,Hkv", [(32, 8), (64, 8), (8, 8)])
 @pytest.mark.parametrize("split", [False, True])
 def test_paged_decode(Hq, Hkv, split):
