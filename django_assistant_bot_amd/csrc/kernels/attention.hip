@@ -70,6 +70,11 @@ struct FlashParams {
 // The K/V tiles of a (sequence, kv head) are re-read by every query block of its GQA heads, so the
 // grid is walked XCD-major: a (sequence, kv head)'s workgroups get ids that share blockIdx % 8 and
 // land on one XCD, whose L2 then serves the re-reads (round-robin dispatch puts block i on XCD i % 8).
+// Deferred online-softmax rescale (cdna_hip_programming.md T13): the running maximum is kept until a
+// row maximum grows by more than 2^kDeferLog2, so P stays <= 2^8 and the O / l rescale is skipped on
+// most tiles; decided before the tile's P is exponentiated (nothing is scaled twice).
+constexpr float kDeferLog2 = 8.f;
+
 template <int D, bool CAUSAL, bool PAGED, int NW, int QT>
 // (QT = 2 with 4 waves is held to 256 registers -- 2 waves per SIMD, no spills -- by the
 // launch bound; unbounded it took 294 and ran at 1 wave per SIMD.)
@@ -224,14 +229,17 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_f
       }
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run[qt], mx);
-      const float alpha = exp2f(m_run[qt] - m_new);
+      // deferred rescale as in flash_d128 (kDeferLog2); raw v_exp_f32 (results below 2^-126 do not
+      // matter next to the row maximum's 1)
+      const bool keep = __all(mx - m_run[qt] <= kDeferLog2);
+      const float m_new = keep ? m_run[qt] : fmaxf(m_run[qt], mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run[qt] - m_new);
       float ls = 0.f;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = exp2f(s[qt][m][r] - m_new);
+          const float e = __builtin_amdgcn_exp2f(s[qt][m][r] - m_new);
           s[qt][m][r] = e;
           ls += e;
         }
@@ -245,8 +253,10 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_f
           pb[qt][ss][j] = (short)f2bf(s[qt][2 * ss][j]);
           pb[qt][ss][j + 4] = (short)f2bf(s[qt][2 * ss + 1][j]);
         }
+      if (!keep) {
 #pragma unroll
-      for (int t = 0; t < NTD; ++t) o[qt][t] *= alpha;
+        for (int t = 0; t < NTD; ++t) o[qt][t] *= alpha;
+      }
     }
     // O^T += V^T P^T: each transposed V fragment feeds QT MFMAs
     const int qq = li >> 2, pp = li & 3;
@@ -344,8 +354,6 @@ __device__ __forceinline__ void ds_tr16_x8(const unsigned (&a)[8], u32x2 (&r)[8]
 __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
-
-constexpr float kDeferLog2 = 8.f;  // flash_d128: rescale only when a row maximum grows by > 2^8
 
 template <bool CAUSAL>
 __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
