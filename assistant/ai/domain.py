@@ -1,7 +1,7 @@
 """AI domain types (reference ai/domain.py:5-30)."""
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import Dict, List, TypedDict, Union
 
 

@@ -12,7 +12,7 @@ from __future__ import annotations
 import dataclasses
 import itertools
 from abc import ABC, abstractmethod
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, Optional, Sequence, Tuple
 
 from assistant.utils.sync import sync_to_async
 

@@ -28,7 +28,6 @@ from dataclasses import dataclass, field
 from datetime import datetime
 
 import numpy as np
-import torch
 
 from ..ops._lib import native
 from ..utils import trace

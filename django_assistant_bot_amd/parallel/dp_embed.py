@@ -7,7 +7,7 @@ variable-length batches (length-sorted, token budget), i.e. the MFMA encoder run
 """
 from __future__ import annotations
 
-from typing import Callable, Optional, Sequence
+from typing import Callable, Optional
 
 import numpy as np
 import torch
