@@ -3,42 +3,55 @@
 The reference scales gpu_service by running ``workers`` copies of one process on one device
 (/root/reference/gpu_service/gunicorn_conf.py:9), each with its own model copy, and keeps vectors in
 PostgreSQL (/root/reference/assistant/rag/services/search_service.py:185-196).  Here the W GPUs of a
-node form ONE service: one process per GPU, RCCL (xGMI) for the data plane, a gloo group for the
+node form ONE service: one process per GPU, RCCL (xGMI) for the data plane, gloo groups for the
 host-side control plane.  The layout comes from the settings (``assistant.conf``):
 
 * ``INDEX_SHARDS`` = S -- ranks 0..S-1 each hold a ``ShardedIndex`` shard (rows by ``id % S``);
   searches scan all shards and gather the partial top-k to rank 0 (12 B per hit).
 * ``EMBED_DP`` = D     -- ranks 0..D-1 hold an encoder replica; a large ``/embeddings/`` batch (ingest)
-  is split D ways and the vectors are gathered to rank 0 over RCCL.
+  is split D ways (each rank receives only its texts) and the vectors are gathered to rank 0.
 * ``GEN_TP`` = T       -- W / T generator replicas; replica g is the TP group of ranks gT..gT+T-1.
-  Requests are placed on the least-loaded replica; every scheduler step runs on all replicas.
 
-(0 for S or D means "every rank".)  Rank 0 serves HTTP.  Every operation that involves other ranks is
-a *command*: rank 0 takes the node lock, broadcasts ``(op, payload)`` on the control group, and then
-every rank -- rank 0 included -- runs ``Node.execute(op, payload)``, so the RCCL collectives inside
-the ops are issued in one order everywhere.  Ranks 1..W-1 sit in ``Node.follow()``.
+(0 for S or D means "every rank".)  Rank 0 serves HTTP.  Two independent control channels:
+
+* **Commands** (index upsert / delete / search / sizes, DP embedding): rank 0 broadcasts an int64
+  header on the node's control group and moves the payload as typed tensors -- an upsert sends each
+  shard only the rows it owns, an embedding batch sends each encoder rank only its texts.  Every
+  rank runs the op in one order, so the RCCL collectives inside line up.  Followers run these on
+  their main thread (``Node.follow``) and on a side HIP stream.
+* **Generation**: every replica steps on its own.  Rank 0 places a request on the least-loaded
+  replica and ships it over that replica's request link (a gloo pair group, one per direction) as a
+  fixed-shape message (``parallel/wire.py``); the replica's leader (TP rank 0) runs its engine loop
+  in a thread of its own and sends each finished output back when it finishes.  Inside a TP group
+  the leader broadcasts the step's adds / aborts (and which models to step) to its peers: lock-step
+  only within the group.  A search or an upsert therefore never waits behind a decode step.
 
 Facades on rank 0 give the serving layer the single-process APIs it already uses:
 ``NodeLLM`` (the ``LLMEngine`` API under ``LLMWorker``), ``NodeEmbedder`` (the ``EmbeddingEngine``
-API under ``EmbedWorker``) and ``NodeIndexes`` (gpu_service's ``/index/*`` backend).
+API under ``EmbedWorker``) and ``NodeIndexes`` (gpu_service's ``/index/*`` backend, which validates
+every payload before it becomes a command: a malformed request is a 400, not a broken group).
 
-Failure model (SURVEY.md 5.3): a follower whose command raises leaves the loop and exits non-zero;
-the launcher (``torch.distributed.run --max-restarts``) then tears the whole group down and restarts
-it, which rebuilds every RCCL communicator.  The index is a cache of the ORM and is reloaded from its
-snapshot / the DB after a restart.
+Failure model: a follower whose command or engine loop raises exits non-zero; rank
+0 sees the broken link or collective, marks the node unhealthy (``/health`` 503) and its watchdog
+exits, so the launcher (``torch.distributed.run --max-restarts``) restarts the whole group with new
+RCCL communicators.  The index is a cache of the ORM and is reloaded from its snapshot / the DB.
 """
 from __future__ import annotations
 
 import itertools
 import logging
 import math
+import queue
 import threading
 import time
+from contextlib import nullcontext
 from dataclasses import dataclass
 
 import numpy as np
 import torch
 import torch.distributed as dist
+
+from . import wire
 
 logger = logging.getLogger(__name__)
 
@@ -83,6 +96,28 @@ def _subgroup(n: int, world: int):
     return None if n == world else dist.new_group(list(range(n)))
 
 
+# command op codes (header word 0 of the control broadcast)
+_OPS = ("stop", "name", "index_upsert", "index_delete", "index_search", "index_sizes", "embed", "fault", "stats")
+_CODE = {op: i for i, op in enumerate(_OPS)}
+_NORM = {None: -1, False: 0, True: 1}
+
+
+def _i64(a) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(np.asarray(a, dtype=np.int64)))
+
+
+def _texts_words(texts) -> tuple[np.ndarray, np.ndarray]:
+    blobs = [t.encode("utf-8") for t in texts]
+    offs = np.zeros(len(blobs) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(b) for b in blobs])
+    return offs, np.frombuffer(b"".join(blobs), dtype=np.uint8).astype(np.int64)
+
+
+def _words_texts(offs, flat) -> list:
+    raw = bytes(np.asarray(flat, dtype=np.int64).astype(np.uint8).tolist())
+    return [raw[int(offs[i]):int(offs[i + 1])].decode("utf-8") for i in range(len(offs) - 1)]
+
+
 class Node:
     """Per-rank state of the node service.  Constructed on every rank (collective: creates groups and
     engines in one order)."""
@@ -96,22 +131,49 @@ class Node:
         self.rank, self.world = info.rank, info.world_size
         self.device = info.device
         assert plan.world == self.world, "plan built for another world size"
-        if ctrl is None and self.world > 1:
-            ctrl = control_group(list(range(self.world)))
+        W, T, R = self.world, plan.gen_tp, plan.gen_replicas
+        if ctrl is None and W > 1:
+            ctrl = control_group(list(range(W)))
         self.ctrl = ctrl
-        self.tp_group, self.tp_rank, self.replica = pdist.tp_groups(plan.gen_tp)
-        self.index_group = _subgroup(plan.index_shards, self.world)
-        self.embed_group = _subgroup(plan.embed_dp, self.world)
+        self.tp_group, self.tp_rank, self.replica = pdist.tp_groups(T)
+        self.index_group = _subgroup(plan.index_shards, W)
+        self.embed_group = _subgroup(plan.embed_dp, W)
         self.in_index = self.rank < plan.index_shards
         self.in_embed = self.rank < plan.embed_dp
+        self.leader = self.replica * T  # global rank of this replica's TP rank 0
+        # request links rank 0 <-> leader of replica g >= 1, one pair group per direction (each used
+        # by one thread per side); TP control groups for the lock-step inside a replica
+        self._down: dict = {}
+        self._up: dict = {}
+        for g in range(1, R):
+            dn, up = control_group([0, g * T]), control_group([0, g * T])
+            if self.rank in (0, g * T):
+                self._down[g], self._up[g] = dn, up
+        self.tp_ctrl = None
+        if T > 1:
+            for g in range(R):
+                grp = control_group(list(range(g * T, (g + 1) * T)))
+                if self.replica == g:
+                    self.tp_ctrl = grp
+        if T > 1 and len(providers) > 1:
+            raise ValueError("GEN_TP > 1 serves one generator model per node")
         self.llms: dict = {}
         self.embeds: dict = {}
         self.indexes: dict = {}
-        self._lock = threading.RLock()
+        self.model_names = [p.lower() for p in providers]
+        self.embed_names = [e.lower() for e in embedders]
+        self.names: list[str] = []  # index names by id (same order on every rank)
+        self._cmd_lock = threading.Lock()
         self._stopped = False
         self.commands = 0
         self.healthy = True
         self.last_error = ""
+        self.stats = {"upsert_bytes_recv": 0, "embed_bytes_recv": 0, "ctrl_s": 0.0, "llm_steps": 0,
+                      "link_bytes_sent": 0}
+        self._side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self._llm_thread: threading.Thread | None = None
+        self._receivers: list[threading.Thread] = []
+        self._outq: dict[int, queue.Queue] = {m: queue.Queue() for m in range(len(self.model_names))}
         from ..engine.embedding_engine import EmbeddingEngine
         from ..engine.llm_engine import LLMEngine
 
@@ -121,26 +183,28 @@ class Node:
         for name in providers:
             kw = dict(llm_kwargs or {})
             if llm_weights is not None:  # callable (name, tp_rank, tp_size) -> this rank's shard
-                kw["weights"] = llm_weights(name, self.tp_rank, plan.gen_tp)
-            eng = LLMEngine(name, self.device, seed=seed, tp_group=self.tp_group, tp_size=plan.gen_tp,
+                kw["weights"] = llm_weights(name, self.tp_rank, T)
+            eng = LLMEngine(name, self.device, seed=seed, tp_group=self.tp_group, tp_size=T,
                             tp_rank=self.tp_rank, **kw)
             eng.auto_expire = False  # deadlines are decided on rank 0 and shipped as aborts
             self.llms[name.lower()] = eng
 
-    # ------------------------------------------------------------------ control plane
+    # ================================================================== command channel
+    def _side_stream(self):
+        return torch.cuda.stream(self._side) if self._side is not None else nullcontext()
+
     def command(self, op: str, payload=None):
         """Rank 0: run ``op`` on every rank; returns rank 0's result."""
         assert self.rank == 0, "only rank 0 issues node commands"
-        with self._lock:
+        with self._cmd_lock:
             if self._stopped:
                 raise RuntimeError("node service is shut down")
             if not self.healthy:
                 raise NodeFault(f"node group is broken ({self.last_error}); waiting for the restart")
             try:
-                if self.world > 1:
-                    dist.broadcast_object_list([(op, payload)], src=0, group=self.ctrl)
-                self.commands += 1
-                return self.execute(op, payload)
+                if op in ("index_upsert", "index_delete", "index_search") and payload[0] not in self.names:
+                    self._run("name", payload[0])
+                return self._run(op, payload)
             except Exception as exc:
                 # A dead peer surfaces here: the control broadcast or a collective inside the op fails.
                 # Results of a half-run command cannot be trusted on any rank, so the group is over.
@@ -149,39 +213,81 @@ class Node:
                 logger.error("node command failed, group marked broken: %s", self.last_error)
                 raise NodeFault(self.last_error) from exc
 
+    def _run(self, op: str, payload):
+        words = getattr(self, "_hdr_" + op)(payload) if hasattr(self, "_hdr_" + op) else []
+        hdr = torch.zeros(wire.HDR, dtype=torch.int64)
+        hdr[0] = _CODE[op]
+        hdr[1:1 + len(words)] = torch.tensor(words, dtype=torch.int64)
+        if self.world > 1:
+            dist.broadcast(hdr, src=0, group=self.ctrl)
+        self.commands += 1
+        with self._side_stream():
+            out = getattr(self, "_op_" + op)(hdr.tolist(), payload)
+        if self._side is not None:
+            self._side.synchronize()
+        return out
+
     def follow(self) -> int:
-        """Ranks 1..W-1: run commands until ``stop``.  Returns the number of commands run.  A command
-        that raises ends the loop with the exception (the launcher restarts the group)."""
+        """Ranks 1..W-1: start this rank's generator loop, then run commands until ``stop``.  Returns
+        the number of commands run.  A command that raises ends the loop with the exception (the
+        launcher restarts the group)."""
+        self._start_llm_loop()
         n = 0
         while True:
-            box = [None]
-            dist.broadcast_object_list(box, src=0, group=self.ctrl)
-            op, payload = box[0]
+            hdr = torch.zeros(wire.HDR, dtype=torch.int64)
+            dist.broadcast(hdr, src=0, group=self.ctrl)
+            h = hdr.tolist()
+            op = _OPS[h[0]]
             if op == "stop":
-                return n
+                break
             try:
-                self.execute(op, payload)
+                with self._side_stream():
+                    getattr(self, "_op_" + op)(h, None)
+                if self._side is not None:
+                    self._side.synchronize()
             except Exception:
                 logger.exception("rank %d: node command %s failed; leaving the group", self.rank, op)
                 raise
             n += 1
+        if self._llm_thread is not None:
+            self._llm_thread.join(120)
+        return n
 
     def shutdown(self) -> None:
         if self.rank == 0 and not self._stopped:
-            with self._lock:
-                if self.world > 1:
-                    dist.broadcast_object_list([("stop", None)], src=0, group=self.ctrl)
+            self._stop_llm_links()
+            with self._cmd_lock:
+                if self.world > 1 and self.healthy:
+                    try:
+                        self._run("stop", None)
+                    except Exception:
+                        logger.exception("stop broadcast failed")
                 self._stopped = True
 
-    def execute(self, op: str, payload):
-        return getattr(self, "_op_" + op)(payload)
-
-    def _op_fault(self, rank):
-        """Fault injection (tests): the given rank fails inside a command."""
-        if self.rank == rank:
-            raise RuntimeError(f"injected fault on rank {rank}")
+    def _bcast(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.broadcast(t, src=0, group=self.ctrl)
+        return t
 
     # ------------------------------------------------------------------ ops (run on every rank)
+    def _op_stop(self, h, p):
+        return None
+
+    def _hdr_name(self, name):
+        return [len(name.encode("utf-8"))]
+
+    def _op_name(self, h, name):
+        buf = _i64(wire.text_words(name)) if self.rank == 0 else torch.zeros(h[1], dtype=torch.int64)
+        self.names.append(wire.words_text(self._bcast(buf).numpy()))
+
+    def _op_fault(self, h, p):
+        """Fault injection (tests): the given rank fails inside a command."""
+        if self.rank == h[1]:
+            raise RuntimeError(f"injected fault on rank {h[1]}")
+
+    def _hdr_fault(self, rank):
+        return [int(rank)]
+
     def _cdev(self, group):
         if self.world == 1:
             return self.device
@@ -203,43 +309,148 @@ class Node:
             dist.all_reduce(t, group=self.index_group)
         return int(t.item())
 
-    def _op_index_upsert(self, p):
+    def _hdr_index_upsert(self, p):
         name, ids, vecs, docs, groups = p
+        return [self.names.index(name), vecs.shape[1], int(docs is not None), int(groups is not None), len(ids)]
+
+    def _op_index_upsert(self, h, p):
+        """Rows are routed by owner (``id % S``): shard r receives exactly its rows, rank 0 keeps its own."""
+        name, dim, has_docs, has_groups, n = self.names[h[1]], h[2], h[3], h[4], h[5]
+        S = self.plan.index_shards
+        counts = torch.zeros(S, dtype=torch.int64)
+        if self.rank == 0:
+            _, ids, vecs, docs, groups = p
+            owner = ids % S
+            sel = [np.nonzero(owner == r)[0] for r in range(S)]
+            counts = _i64([len(s) for s in sel])
+        self._bcast(counts)
+        mine = None
+        if self.rank == 0:
+            for r in range(1, S):
+                if int(counts[r]) == 0:
+                    continue
+                s = sel[r]
+                ints = np.stack([ids[s], docs[s] if has_docs else np.zeros(len(s), np.int64),
+                                 groups[s].astype(np.int64) if has_groups else np.zeros(len(s), np.int64)])
+                dist.send(_i64(ints), dst=r, group=self.ctrl)
+                dist.send(torch.from_numpy(np.ascontiguousarray(vecs[s])), dst=r, group=self.ctrl)
+            s = sel[0]
+            mine = (ids[s], vecs[s], docs[s] if has_docs else None, groups[s] if has_groups else None)
+        elif self.in_index and int(counts[self.rank]):
+            m = int(counts[self.rank])
+            ints = torch.zeros((3, m), dtype=torch.int64)
+            v = torch.zeros((m, dim), dtype=torch.float32)
+            dist.recv(ints, src=0, group=self.ctrl)
+            dist.recv(v, src=0, group=self.ctrl)
+            self.stats["upsert_bytes_recv"] += ints.numel() * 8 + v.numel() * 4
+            a = ints.numpy()
+            mine = (a[0], v.numpy(), a[1] if has_docs else None, a[2].astype(np.int32) if has_groups else None)
         if not self.in_index:
             return None
-        idx = self._index(name, vecs.shape[1])
-        idx.add(ids, torch.from_numpy(vecs), doc_ids=docs, groups=groups)
+        idx = self._index(name, dim)
+        if mine is not None and len(mine[0]):
+            idx.add(mine[0], torch.from_numpy(np.ascontiguousarray(mine[1])), doc_ids=mine[2], groups=mine[3])
         return self._index_total(len(idx.local))
 
-    def _op_index_delete(self, p):
+    def _hdr_index_delete(self, p):
         name, ids = p
+        return [self.names.index(name), len(ids)]
+
+    def _op_index_delete(self, h, p):
+        ids = _i64(p[1]) if self.rank == 0 else torch.zeros(h[2], dtype=torch.int64)
+        ids = self._bcast(ids).numpy()
+        if not self.in_index:
+            return None
+        idx = self._index(self.names[h[1]])
+        return self._index_total(idx.remove(ids) if idx is not None else 0)
+
+    def _hdr_index_search(self, p):
+        name, q, k, groups, allowed, doc_lt = p
+        total = sum(len(a) for a in allowed) if allowed is not None else 0
+        return [self.names.index(name), q.shape[0], q.shape[1], int(k), int(groups is not None),
+                int(allowed is not None), total, int(doc_lt is not None)]
+
+    def _op_index_search(self, h, p):
+        name, nq, dim, k, has_g, has_a, total, has_d = self.names[h[1]], h[2], h[3], h[4], h[5], h[6], h[7], h[8]
+        if self.rank == 0:
+            _, q, _, groups, allowed, doc_lt = p
+            qt = torch.from_numpy(np.ascontiguousarray(q, dtype=np.float32))
+        else:
+            qt = torch.zeros((nq, dim), dtype=torch.float32)
+        self._bcast(qt)
+        groups_t = allowed_l = doc_t = None
+        if has_g:
+            groups_t = self._bcast(_i64(groups) if self.rank == 0 else torch.zeros(nq, dtype=torch.int64))
+        if has_a:
+            if self.rank == 0:
+                offs = np.zeros(nq + 1, dtype=np.int64)
+                offs[1:] = np.cumsum([len(a) for a in allowed])
+                flat = np.concatenate([np.asarray(a, dtype=np.int64).reshape(-1) for a in allowed]) if total else \
+                    np.zeros(0, dtype=np.int64)
+                offs_t, flat_t = _i64(offs), _i64(flat)
+            else:
+                offs_t, flat_t = torch.zeros(nq + 1, dtype=torch.int64), torch.zeros(total, dtype=torch.int64)
+            self._bcast(offs_t)
+            if total:
+                self._bcast(flat_t)
+            o, f = offs_t.numpy(), flat_t.numpy()
+            allowed_l = [f[o[i]:o[i + 1]] for i in range(nq)]
+        if has_d:
+            doc_t = self._bcast(_i64(doc_lt) if self.rank == 0 else torch.zeros(nq, dtype=torch.int64))
         if not self.in_index:
             return None
         idx = self._index(name)
-        return self._index_total(idx.remove(ids) if idx is not None else 0)
-
-    def _op_index_search(self, p):
-        name, queries, k, groups, allowed, doc_lt = p
-        if not self.in_index:
-            return None
-        out = self._index(name).search_replicated(queries, k, q_groups=groups, allowed=allowed, doc_lt=doc_lt,
-                                                  dst=0)
+        out = idx.search_replicated(qt.numpy(), k, q_groups=None if groups_t is None else groups_t.numpy(),
+                                    allowed=allowed_l, doc_lt=None if doc_t is None else doc_t.numpy(), dst=0)
         return None if out is None else tuple(x.cpu() for x in out)
 
-    def _op_index_sizes(self, names):
+    def _hdr_index_sizes(self, names):
+        return [len(names)]
+
+    def _op_index_sizes(self, h, names):
+        ids = _i64([self.names.index(n) if n in self.names else -1 for n in names]) if self.rank == 0 else \
+            torch.zeros(h[1], dtype=torch.int64)
+        ids = self._bcast(ids).tolist()
         if not self.in_index:
             return None
-        return {n: self._index_total(len(self.indexes[n].local) if n in self.indexes else 0) for n in names}
+        totals = []
+        for i in ids:
+            idx = self.indexes.get(self.names[i]) if i >= 0 else None
+            totals.append(self._index_total(len(idx.local) if idx is not None else 0))
+        return dict(zip(names, totals)) if self.rank == 0 else None
 
-    def _op_embed(self, p):
+    def _hdr_embed(self, p):
         name, texts, normalize = p
+        return [self.embed_names.index(name), len(texts), _NORM[normalize]]
+
+    def _op_embed(self, h, p):
+        """Each encoder rank receives only its round-robin share of the texts; vectors are gathered."""
+        name, n, norm = self.embed_names[h[1]], h[2], {-1: None, 0: False, 1: True}[h[3]]
+        D = self.plan.embed_dp
         if not self.in_embed:
             return None
-        D = self.plan.embed_dp
+        if self.rank == 0:
+            texts = p[1]
+            for r in range(1, D):
+                offs, flat = _texts_words(texts[r::D])
+                dist.send(_i64([len(flat)]), dst=r, group=self.embed_ctrl_group())
+                dist.send(_i64(offs), dst=r, group=self.embed_ctrl_group())
+                if len(flat):
+                    dist.send(_i64(flat), dst=r, group=self.embed_ctrl_group())
+            mine = texts[0::D]
+        else:
+            ln = torch.zeros(1, dtype=torch.int64)
+            dist.recv(ln, src=0, group=self.embed_ctrl_group())
+            cnt = len(range(self.rank, n, D))
+            offs = torch.zeros(cnt + 1, dtype=torch.int64)
+            dist.recv(offs, src=0, group=self.embed_ctrl_group())
+            flat = torch.zeros(int(ln), dtype=torch.int64)
+            if int(ln):
+                dist.recv(flat, src=0, group=self.embed_ctrl_group())
+            self.stats["embed_bytes_recv"] += 8 * (1 + offs.numel() + flat.numel())
+            mine = _words_texts(offs.numpy(), flat.numpy())
         eng = self.embeds[name]
-        n = len(texts)
-        mine = texts[self.rank::D]  # round-robin: every rank gets a similar length mix
-        v = eng.embed(mine, normalize=normalize, out_dtype=torch.float32)
+        v = eng.embed(mine, normalize=norm, out_dtype=torch.float32)
         if D == 1:
             return v
         cdev = self._cdev(self.embed_group)
@@ -256,51 +467,191 @@ class Node:
             out[r::D] = parts[r][:cnt]
         return out
 
-    def _op_llm_step(self, p):
-        name, items = p
-        eng = self.llms[name]
-        aborted = []
-        for it in items:
-            if it[1] != self.replica:
-                continue
-            if it[0] == "add":
-                _, _, prompt, params, rid = it
-                eng.add_request(prompt, params, request_id=rid)
-            elif it[0] == "abort":
-                _, _, rid, reason = it
-                if eng.abort(rid, reason):
-                    aborted.append(rid)
-        done = eng.step() if eng.has_unfinished() else []
-        outs = [(rid, eng.pop_output(rid)) for rid in aborted + done]
-        if self.tp_rank != 0:
-            outs = []  # the replica's TP rank 0 reports; the others only free their bookkeeping
-        if self.world == 1:
-            return outs
-        got = [None] * self.world if self.rank == 0 else None
-        dist.gather_object(outs, got, dst=0, group=self.ctrl)
-        return [o for part in got for o in part] if self.rank == 0 else None
+    def embed_ctrl_group(self):
+        return self.ctrl
 
-    def _op_llm_fail(self, name):
-        return self.llms[name].fail_all()
+    def _op_stats(self, h, p):
+        """Per-rank control-plane counters gathered to rank 0: [ctrl_s, llm_steps, upsert bytes, embed bytes]."""
+        t = torch.tensor([self.stats["ctrl_s"], self.stats["llm_steps"], self.stats["upsert_bytes_recv"],
+                          self.stats["embed_bytes_recv"]], dtype=torch.float64)
+        if self.world == 1:
+            return t[None]
+        parts = [torch.zeros_like(t) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(t, parts, dst=0, group=self.ctrl)
+        return torch.stack(parts) if self.rank == 0 else None
+
+    # ================================================================== generation
+    def _engines(self):
+        return [self.llms[n] for n in self.model_names]
+
+    def _start_llm_loop(self):
+        """Followers: the replica leader's request loop, or a TP peer's lock-step loop."""
+        if not self.model_names or self._llm_thread is not None:
+            return
+        if self.rank == self.leader and self.rank != 0:
+            target = self._leader_loop
+        elif self.rank != self.leader:
+            target = self._peer_loop
+        else:
+            return
+        self._llm_thread = threading.Thread(target=self._guard(target), name=f"node-llm-{self.rank}", daemon=True)
+        self._llm_thread.start()
+
+    def _guard(self, fn):
+        def run():
+            try:
+                fn()
+            except Exception as exc:
+                self.healthy = False
+                self.last_error = f"generator loop: {type(exc).__name__}: {exc}"
+                logger.exception("rank %d: generator loop failed; leaving the group", self.rank)
+                import os
+
+                os._exit(1)  # the launcher restarts the group (SURVEY.md 5.3)
+        return run
+
+    def apply_items(self, items, outs: list | None) -> tuple[list, bool]:
+        """Applies a batch of ADD / ABORT / FAIL / STOP items to the local engines.  Returns (models to
+        step, stop); aborted requests' outputs are appended to ``outs`` (leaders) or dropped."""
+        engines = self._engines()
+        steps, stop = [], False
+        for h, p in items:
+            k = int(h[0])
+            if k == wire.ADD:
+                m, rid, prompt, sp = wire.read_add(h, p)
+                engines[m].add_request(prompt, sp, request_id=rid)
+            elif k == wire.ABORT:
+                m, rid, reason = wire.read_abort(h, p)
+                if engines[m].abort(rid, reason):
+                    out = engines[m].pop_output(rid)
+                    if outs is not None:
+                        outs.append(wire.out_item(m, out))
+            elif k == wire.FAIL:
+                engines[int(h[1])].fail_all()
+            elif k == wire.STEP:
+                steps.append(int(h[1]))
+            elif k == wire.STOP:
+                stop = True
+        return steps, stop
+
+    def step_models(self, steps, outs: list | None) -> None:
+        engines = self._engines()
+        for m in steps:
+            for rid in engines[m].step():
+                out = engines[m].pop_output(rid)
+                if outs is not None:
+                    outs.append(wire.out_item(m, out))
+        self.stats["llm_steps"] += 1 if steps else 0
+
+    def _leader_loop(self):
+        """Leader of replica g >= 1: requests arrive on the down link (polled between steps, waited
+        for when idle), outputs leave on the up link as they finish."""
+        g = self.replica
+        down, up = self._down[g], self._up[g]
+        engines = self._engines()
+        meta = torch.zeros(2, dtype=torch.int64)
+        work = dist.irecv(meta, src=0, group=down)
+        while True:
+            busy = any(e.has_unfinished() for e in engines)
+            items = []
+            if not busy:
+                work.wait()  # idle: sleep until rank 0 sends work (not counted as control time)
+            t0 = time.perf_counter()
+            if not busy or work.is_completed():
+                items = wire.recv_batch(0, down, meta)
+                meta = torch.zeros(2, dtype=torch.int64)
+                work = dist.irecv(meta, src=0, group=down)
+            outs: list = []
+            _, stop = self.apply_items(items, outs)
+            steps = [] if stop else [m for m, e in enumerate(engines) if e.has_unfinished()]
+            if self.tp_ctrl is not None and (items or steps):
+                wire.bcast_batch(list(items) + [wire.item([wire.STEP, m]) for m in steps], self.rank, self.tp_ctrl)
+            self.stats["ctrl_s"] += time.perf_counter() - t0
+            if stop:
+                self.stats["link_bytes_sent"] += wire.send_batch(outs + [wire.item([wire.STOP])], 0, up)
+                return
+            self.step_models(steps, outs)
+            if outs:
+                t0 = time.perf_counter()
+                self.stats["link_bytes_sent"] += wire.send_batch(outs, 0, up)
+                self.stats["ctrl_s"] += time.perf_counter() - t0
+
+    def _peer_loop(self):
+        """TP rank > 0: apply what the replica's leader broadcasts, step when it steps."""
+        while True:
+            items = wire.bcast_batch(None, self.leader, self.tp_ctrl)  # waits out the leader's idle time too
+            steps, stop = self.apply_items(items, None)
+            if stop:
+                return
+            self.step_models(steps, None)
+
+    def _ensure_receivers(self):
+        """Rank 0: one thread per remote replica collects its finished outputs."""
+        if self.rank != 0 or self._receivers:
+            return
+        for g, up in self._up.items():
+            t = threading.Thread(target=self._receive, args=(g, up), name=f"node-recv-{g}", daemon=True)
+            t.start()
+            self._receivers.append(t)
+
+    def _receive(self, g, up):
+        src = g * self.plan.gen_tp
+        try:
+            while True:
+                for h, p in wire.recv_batch(src, up):
+                    k = int(h[0])
+                    if k == wire.STOP:
+                        return
+                    if k == wire.OUT:
+                        m = int(h[1])
+                        _, out = wire.read_out(h, p, self.llms[self.model_names[m]].tokenizer)
+                        self._outq[m].put(out)
+        except Exception as exc:
+            if not self._stopped:
+                self.healthy = False
+                self.last_error = f"replica {g} link: {type(exc).__name__}: {exc}"
+                logger.error("node replica link broken: %s", self.last_error)
+
+    def send_items(self, g: int, items) -> None:
+        """Rank 0: ship items to replica g's leader."""
+        t0 = time.perf_counter()
+        self.stats["link_bytes_sent"] += wire.send_batch(items, g * self.plan.gen_tp, self._down[g])
+        self.stats["ctrl_s"] += time.perf_counter() - t0
+
+    def _stop_llm_links(self):
+        if not self.model_names:
+            return
+        for g in self._down:
+            try:
+                self.send_items(g, [wire.item([wire.STOP])])
+            except Exception:
+                logger.exception("stop to replica %d failed", g)
+        for t in self._receivers:
+            t.join(60)
+        if self.tp_ctrl is not None and self.healthy:
+            wire.bcast_batch([wire.item([wire.STOP])], 0, self.tp_ctrl)
 
 
 # ---------------------------------------------------------------------- rank-0 facades
 class NodeLLM:
-    """``LLMEngine`` API over the node's generator replicas (what ``LLMWorker`` drives).  Adds and
-    aborts are queued and shipped with the next step command; finished outputs come back from every
-    replica's TP rank 0 in the same command."""
+    """``LLMEngine`` API over the node's generator replicas (what ``LLMWorker`` drives).  Replica 0 is
+    this rank's engine, stepped in the caller's thread; the other replicas run on their own and their
+    finished outputs arrive through ``Node``'s receiver threads."""
 
     def __init__(self, node: Node, name: str):
         self.node, self.name = node, name.lower()
+        self.m = node.model_names.index(self.name)
         self.engine = node.llms[self.name]  # replica 0's engine (tokenizer, limits, stats)
         self._ids = itertools.count()
-        self._pending: list = []
+        self._local: list = []  # items for replica 0 (applied / broadcast at the next step)
+        self._remote: dict[int, list] = {g: [] for g in range(1, node.plan.gen_replicas)}
         self._where: dict[int, int] = {}
         self._deadline: dict[int, float] = {}
         self._load = [0] * node.plan.gen_replicas
         self.finished: dict = {}
         self._discard: set = set()
         self.stats_node = {"steps": 0, "placed": [0] * node.plan.gen_replicas}
+        node._ensure_receivers()
 
     def add_request(self, prompt_ids, params=None, request_id=None) -> int:
         from ..engine.llm_engine import SamplingParams
@@ -308,7 +659,8 @@ class NodeLLM:
         params = params or SamplingParams()
         rid = next(self._ids) if request_id is None else int(request_id)
         replica = min(range(len(self._load)), key=lambda g: (self._load[g], g))
-        self._pending.append(("add", replica, [int(t) for t in prompt_ids], params, rid))
+        it = wire.add_item(self.m, rid, [int(t) for t in prompt_ids], params)
+        (self._local if replica == 0 else self._remote[replica]).append(it)
         self._where[rid] = replica
         self._load[replica] += 1
         self.stats_node["placed"][replica] += 1
@@ -320,25 +672,48 @@ class NodeLLM:
         g = self._where.get(rid)
         if g is None:
             return False
-        self._pending.append(("abort", g, rid, reason))
+        it = wire.abort_item(self.m, rid, reason)
+        (self._local if g == 0 else self._remote[g]).append(it)
         return True
 
     def has_unfinished(self) -> bool:
-        return bool(self._where) or bool(self._pending)
+        return bool(self._where) or bool(self._local) or any(self._remote.values())
 
     def expired(self) -> list[int]:
         now = time.perf_counter()
         return [rid for rid, t in self._deadline.items() if now > t]
 
     def step(self) -> list[int]:
+        node = self.node
         for rid in self.expired():
             self._deadline.pop(rid, None)
             self.abort(rid, "timeout")
-        items, self._pending = self._pending, []
-        outs = self.node.command("llm_step", (self.name, items))
+        for g, items in self._remote.items():
+            if items:
+                self._remote[g] = []
+                node.send_items(g, items)
+        outs: list = []
+        items, self._local = self._local, []
+        _, _ = node.apply_items(items, outs)
+        steps = [self.m] if self.engine.has_unfinished() else []
+        if node.tp_ctrl is not None and (items or steps):
+            t0 = time.perf_counter()
+            wire.bcast_batch(list(items) + [wire.item([wire.STEP, m]) for m in steps], 0, node.tp_ctrl)
+            node.stats["ctrl_s"] += time.perf_counter() - t0
+        node.step_models(steps, outs)
         self.stats_node["steps"] += 1
+        got = [wire.read_out(h, p, self.engine.tokenizer)[1] for h, p in outs]
+        q = node._outq[self.m]
+        try:  # nothing ran here: wait briefly for a remote replica instead of spinning
+            if not got and not steps:
+                got.append(q.get(timeout=0.002))
+            while True:
+                got.append(q.get_nowait())
+        except queue.Empty:
+            pass
         done = []
-        for rid, out in outs:
+        for out in got:
+            rid = out.request_id
             g = self._where.pop(rid, None)
             if g is None:
                 continue
@@ -362,12 +737,20 @@ class NodeLLM:
 
     def fail_all(self) -> list[int]:
         ids = list(self._where)
-        if self.node.healthy:  # a broken group is restarted as a whole; nothing to clean up remotely
+        node = self.node
+        if node.healthy:  # a broken group is restarted as a whole; nothing to clean up remotely
+            fail = [wire.item([wire.FAIL, self.m])]
             try:
-                self.node.command("llm_fail", self.name)
-            except NodeFault:
-                pass
-        self._pending.clear()
+                node.apply_items(fail, None)
+                if node.tp_ctrl is not None:
+                    wire.bcast_batch(fail, 0, node.tp_ctrl)
+                for g in self._remote:
+                    node.send_items(g, fail)
+            except Exception:
+                logger.exception("fail_all propagation failed")
+        self._local.clear()
+        for g in self._remote:
+            self._remote[g] = []
         self._where.clear()
         self._deadline.clear()
         self._discard.clear()
@@ -402,7 +785,7 @@ class NodeEmbedder:
         self.min_split = min_split
 
     def embed(self, texts, normalize=None, out_dtype=torch.float32):
-        texts = list(texts)
+        texts = [str(t) for t in texts]
         D = self.node.plan.embed_dp
         if D == 1 or len(texts) < self.min_split * D:
             return self.engine.embed(texts, normalize=normalize, out_dtype=out_dtype)
@@ -413,7 +796,11 @@ class NodeEmbedder:
 
 
 class NodeIndexes:
-    """gpu_service ``/index/*`` backend over the sharded index of the node."""
+    """gpu_service ``/index/*`` backend over the sharded index of the node.  Payloads are validated
+    here, before they become commands: a malformed request raises ``ValueError`` (HTTP 400) and the
+    group stays healthy."""
+
+    MAX_K = 1024
 
     def __init__(self, node: Node):
         self.node = node
@@ -424,20 +811,45 @@ class NodeIndexes:
         return self._dims.get(name)
 
     def upsert(self, name, ids, vectors, doc_ids=None, groups=None) -> int:
+        ids = np.asarray(ids)
         vecs = np.asarray(vectors, dtype=np.float32)
-        ids = np.asarray(ids, dtype=np.int64)
-        docs = None if doc_ids is None else np.asarray(doc_ids, dtype=np.int64)
-        grp = None if groups is None else np.asarray(groups, dtype=np.int32)
+        if ids.ndim != 1 or (len(ids) and not np.issubdtype(ids.dtype, np.integer)):
+            raise ValueError("ids must be a list of integers")
+        ids = ids.astype(np.int64)
+        if vecs.ndim != 2 or vecs.shape[0] != len(ids) or vecs.shape[1] < 1:
+            raise ValueError("vectors must be a [len(ids), dim] matrix")
+        if (ids < 0).any():
+            raise ValueError("ids must be >= 0")
+        if not np.isfinite(vecs).all():
+            raise ValueError("vectors must be finite")
+        dim = self._dims.get(name)
+        if dim is not None and vecs.shape[1] != dim:
+            raise ValueError(f"index {name} has dim {dim}")
+        docs = None if doc_ids is None else np.asarray(doc_ids)
+        if docs is not None and (docs.shape != ids.shape or (len(docs) and not np.issubdtype(docs.dtype, np.integer))):
+            raise ValueError("doc_ids must be one integer per id")
+        grp = None if groups is None else np.asarray(groups)
+        if grp is not None:
+            if grp.shape != ids.shape or (len(grp) and not np.issubdtype(grp.dtype, np.integer)):
+                raise ValueError("groups must be one integer per id")
+            if (grp < 0).any() or (grp >= 2 ** 31).any():
+                raise ValueError("groups must be in [0, 2^31)")
+        if len(ids) == 0:
+            return self._counts.get(name, 0)
         self._dims.setdefault(name, vecs.shape[1])
-        n = self.node.command("index_upsert", (name, ids, vecs, docs, grp))
+        n = self.node.command("index_upsert", (name, ids, vecs, None if docs is None else docs.astype(np.int64),
+                                               None if grp is None else grp.astype(np.int32)))
         self._counts[name] = n
         return n
 
     def delete(self, name, ids) -> int:
         if name not in self._dims:
             return 0
+        ids = np.asarray(ids)
+        if ids.ndim != 1 or (len(ids) and not np.issubdtype(ids.dtype, np.integer)):
+            raise ValueError("ids must be a list of integers")
         before = self._counts.get(name, 0)
-        n = self.node.command("index_delete", (name, np.asarray(ids, dtype=np.int64)))
+        n = self.node.command("index_delete", (name, ids.astype(np.int64)))
         self._counts[name] = before - n
         return n
 
@@ -448,7 +860,28 @@ class NodeIndexes:
         if name not in self._dims:
             return None
         q = np.asarray(queries, dtype=np.float32)
-        return self.node.command("index_search", (name, q, int(k), groups, allowed, doc_lt))
+        if q.ndim != 2 or q.shape[1] != self._dims[name]:
+            raise ValueError(f"queries must be a [n, {self._dims[name]}] matrix")
+        nq = q.shape[0]
+        if not np.isfinite(q).all():
+            raise ValueError("queries must be finite")
+        k = int(k)
+        if not 1 <= k <= self.MAX_K:
+            raise ValueError(f"k must be in [1, {self.MAX_K}]")
+        if groups is not None:
+            groups = np.asarray(groups)
+            if groups.shape != (nq,) or not np.issubdtype(groups.dtype, np.integer):
+                raise ValueError("groups must be one integer per query")
+        if allowed is not None:
+            if len(allowed) != nq:
+                raise ValueError("allowed must hold one id list per query")
+            allowed = [np.asarray(list(a) if isinstance(a, (set, frozenset)) else a, dtype=np.int64).reshape(-1)
+                       for a in allowed]
+        if doc_lt is not None:
+            doc_lt = np.asarray(doc_lt)
+            if doc_lt.shape != (nq,) or not np.issubdtype(doc_lt.dtype, np.integer):
+                raise ValueError("doc_lt must be one integer per query")
+        return self.node.command("index_search", (name, q, k, groups, allowed, doc_lt))
 
     def sizes(self) -> dict:
         return dict(self._counts)

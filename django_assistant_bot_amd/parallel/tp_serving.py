@@ -12,9 +12,9 @@ follow:
   local engine, step.  Sampled tokens are already identical on all ranks, because the engine
   broadcasts TP rank 0's tokens inside every step.
 
-The control messages go over a gloo group: host objects on the CPU, independent of the RCCL data
-plane.  The leader can therefore sit in an asyncio server thread without touching the GPU
-collectives.
+The control messages go over a gloo group as fixed-shape int64 tensors (``parallel/wire.py``: one
+header table + payload per step, no pickles), independent of the RCCL data plane.  The leader can
+therefore sit in an asyncio server thread without touching the GPU collectives.
 
     leader = TPLeader(engine, ctrl_group)        # rank 0: hand to LLMWorker / gpu_service
     follow(engine, ctrl_group)                   # ranks 1..N-1: blocks until leader.shutdown()
@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import torch.distributed as dist
 
-_STEP, _STOP, _FAIL = "step", "stop", "fail_all"
+from . import wire
 
 
 def control_group(ranks: list[int] | None = None, timeout_s: float = 30 * 24 * 3600):
@@ -42,7 +42,7 @@ class TPLeader:
     def __init__(self, engine, group=None):
         self.engine = engine
         self.group = group
-        self._pending: list = []  # ("add", prompt, params, rid) / ("abort", rid, reason)
+        self._pending: list = []  # wire ADD / ABORT items of the next step
         self._stopped = False
         engine.auto_expire = False  # deadlines are decided here and mirrored as aborts
 
@@ -50,33 +50,32 @@ class TPLeader:
     def add_request(self, prompt_ids, params=None, request_id=None) -> int:
         rid = self.engine.add_request(prompt_ids, params, request_id)
         r = self.engine.waiting[-1]  # the request just queued: ship the normalised prompt + params
-        self._pending.append(("add", list(r.prompt), r.params, rid))
+        self._pending.append(wire.add_item(0, rid, list(r.prompt), r.params))
         return rid
 
     def abort(self, rid: int, reason: str = "abort") -> bool:
-        self._pending.append(("abort", rid, reason))
+        self._pending.append(wire.abort_item(0, rid, reason))
         return self.engine.abort(rid, reason)
 
     def step(self) -> list[int]:
         for rid in self.engine.expired():
             self.abort(rid, "timeout")
-        self._send((_STEP, self._pending))
+        self._send(self._pending + [wire.item([wire.STEP, 0])])
         self._pending = []
         return self.engine.step()
 
     def fail_all(self) -> list[int]:
-        self._send((_FAIL, []))
+        self._send([wire.item([wire.FAIL, 0])])
         self._pending = []
         return self.engine.fail_all()
 
     def shutdown(self) -> None:
         if not self._stopped:
             self._stopped = True
-            self._send((_STOP, []))
+            self._send([wire.item([wire.STOP])])
 
-    def _send(self, msg) -> None:
-        box = [msg]
-        dist.broadcast_object_list(box, src=_src(self.group), group=self.group)
+    def _send(self, items) -> None:
+        wire.bcast_batch(items, _src(self.group), self.group)
 
     def __getattr__(self, name):  # read-only state (stats, tokenizer, finished, has_unfinished ...)
         return getattr(self.engine, name)
@@ -88,20 +87,23 @@ def follow(engine, group=None) -> int:
     steps = 0
     engine.auto_expire = False
     while True:
-        box = [None]
-        dist.broadcast_object_list(box, src=_src(group), group=group)
-        cmd, items = box[0]
-        if cmd == _STOP:
-            return steps
-        if cmd == _FAIL:
-            engine.fail_all()
-            continue
-        for it in items:
-            if it[0] == "add":
-                _, prompt, params, rid = it
+        stepping = False
+        for h, p in wire.bcast_batch(None, _src(group), group):
+            k = int(h[0])
+            if k == wire.STOP:
+                return steps
+            if k == wire.FAIL:
+                engine.fail_all()
+            elif k == wire.ADD:
+                _, rid, prompt, params = wire.read_add(h, p)
                 engine.add_request(prompt, params, request_id=rid)
-            elif it[0] == "abort":
-                engine.abort(it[1], it[2])
-        for rid in engine.step():
-            engine.pop_output(rid)  # outputs are served by the leader only
-        steps += 1
+            elif k == wire.ABORT:
+                _, rid, reason = wire.read_abort(h, p)
+                if engine.abort(rid, reason):
+                    engine.pop_output(rid)
+            elif k == wire.STEP:
+                stepping = True
+        if stepping:
+            for rid in engine.step():
+                engine.pop_output(rid)  # outputs are served by the leader only
+            steps += 1

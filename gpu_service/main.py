@@ -153,6 +153,11 @@ class LocalIndexes:
         return None if idx is None else idx.dim
 
     def upsert(self, name, ids, vectors, doc_ids=None, groups=None) -> int:
+        for what, v in (("doc_ids", doc_ids), ("groups", groups)):
+            if v is not None and len(v) != len(ids):
+                raise ValueError(f"{what} must hold one entry per id")
+        if groups is not None and any(g < 0 for g in groups):
+            raise ValueError("groups must be >= 0")
         with self._lock:
             idx = self.indexes.get(name)
             if idx is None:
@@ -176,6 +181,12 @@ class LocalIndexes:
         return 0 if idx is None else len(idx)
 
     def search(self, name, queries, k, groups=None, allowed=None, doc_lt=None):
+        nq = len(queries)
+        if not 1 <= int(k) <= 1024:
+            raise ValueError("k must be in [1, 1024]")
+        for what, v in (("groups", groups), ("allowed", allowed), ("doc_lt", doc_lt)):
+            if v is not None and len(v) != nq:
+                raise ValueError(f"{what} must hold one entry per query")
         with self._lock:
             idx = self.indexes.get(name)
             if idx is None or len(idx) == 0:
@@ -200,6 +211,16 @@ def _index_guard():
                                                     "(one process group over the node's GPUs) or one worker")
 
 
+async def _call_index(fn, *args):
+    """Index backends raise ValueError for a malformed payload (lengths, dims, k, negative groups):
+    that is the caller's error (400), and in node mode it is raised before anything reaches the
+    other ranks, so the group stays healthy."""
+    try:
+        return await run_in_threadpool(fn, *args)
+    except ValueError as e:
+        raise HTTPException(status_code=400, detail=str(e))
+
+
 @app.post("/index/{name}/upsert")
 async def index_upsert(name: str, request: UpsertRequest):
     _index_guard()
@@ -210,15 +231,14 @@ async def index_upsert(name: str, request: UpsertRequest):
     dim = index_backend.dim(name)
     if dim is not None and len(request.vectors[0]) != dim:
         raise HTTPException(status_code=400, detail=f"index {name} has dim {dim}")
-    n = await run_in_threadpool(index_backend.upsert, name, request.ids, request.vectors, request.doc_ids,
-                                request.groups)
+    n = await _call_index(index_backend.upsert, name, request.ids, request.vectors, request.doc_ids, request.groups)
     return {"count": n}
 
 
 @app.post("/index/{name}/delete")
 async def index_delete(name: str, request: DeleteRequest):
     _index_guard()
-    return {"removed": await run_in_threadpool(index_backend.delete, name, request.ids)}
+    return {"removed": await _call_index(index_backend.delete, name, request.ids)}
 
 
 @app.post("/index/{name}/search")
@@ -227,8 +247,8 @@ async def index_search(name: str, request: SearchRequest):
     nq = len(request.queries)
     got = None
     if nq:
-        got = await run_in_threadpool(index_backend.search, name, request.queries, request.k, request.groups,
-                                      request.allowed, request.doc_lt)
+        got = await _call_index(index_backend.search, name, request.queries, request.k, request.groups,
+                                request.allowed, request.doc_lt)
     if got is None:
         return {"ids": [[] for _ in range(nq)], "distances": [[] for _ in range(nq)],
                 "doc_ids": [[] for _ in range(nq)]}
