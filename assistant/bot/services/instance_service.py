@@ -97,8 +97,25 @@ class InstanceLockAsync(BaseInstanceLock, AbstractAsyncContextManager):
         while not lk.acquire(blocking=False):
             await asyncio.sleep(self.poll_interval)
         self._held = lk
+        # The DB acquire runs on the shared thread-sensitive connection.  A cancelled coroutine
+        # (timeout, client gone) must not walk away while that thread still takes the session lock:
+        # the acquire is shielded, and on cancellation we wait for it to finish, release it on the
+        # same thread, and only then re-raise.
+        acquire = asyncio.ensure_future(sync_to_async(self._db_acquire, thread_sensitive=True)())
         try:
-            await sync_to_async(self._db_acquire, thread_sensitive=True)()
+            await asyncio.shield(acquire)
+        except asyncio.CancelledError:
+            try:
+                await acquire
+            except BaseException:
+                pass  # the acquire itself failed: nothing is held
+            else:
+                try:
+                    await sync_to_async(self._db_release, thread_sensitive=True)(None, None, None)
+                except BaseException:
+                    logger.exception("instance lock %s: release after cancellation failed", self.lock_key)
+            self._drop_key()
+            raise
         except BaseException:
             self._drop_key()
             raise

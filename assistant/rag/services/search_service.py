@@ -73,7 +73,7 @@ async def _objects_embedding_search(query_embedding, qs, n: int = 10, field: str
         hits = get_index_service().search(qs, query_embedding, n, field)
         if not hits:
             return []
-        objs = qs.model.objects.in_bulk([pk for pk, _ in hits])
+        objs = _load_within(qs, [pk for pk, _ in hits])
         out = []
         for pk, dist in hits:
             o = objs.get(pk)
@@ -83,3 +83,14 @@ async def _objects_embedding_search(query_embedding, qs, n: int = 10, field: str
         return out
 
     return await sync_to_async(run)()
+
+
+def _load_within(qs, pks):
+    """{pk: obj} for the hits that still satisfy ``qs``: the QuerySet, not the index's mirrored
+    metadata, decides membership (a row whose wiki moved to another bot or whose processing run was
+    edited since it was mirrored is dropped here)."""
+    try:
+        return {o.pk: o for o in qs.filter(pk__in=pks)}
+    except (TypeError, AssertionError, NotImplementedError):  # sliced / combined QuerySets
+        keep = set(qs.values_list("pk", flat=True))
+        return {pk: o for pk, o in qs.model.objects.in_bulk([p for p in pks if p in keep]).items()}

@@ -105,9 +105,16 @@ def with_index_filter(qs, *, bot=None, completed=None, doc_lt=None):
 
 
 def index_filter_of(qs):
-    """IndexFilter for the two QuerySet shapes the framework searches with (reference
-    steps/embeddings.py:26-29 and processing steps/questions.py:121-126), IndexFilter() for an
-    unfiltered QuerySet, None for anything else."""
+    """IndexFilter for a QuerySet the index can evaluate itself: the ``with_index_filter`` hint of the
+    framework's own call sites (bot + COMPLETED group, reference steps/embeddings.py:26-29), an
+    unfiltered QuerySet, or a document-id bound on the model's own table (reference processing
+    steps/questions.py:121-126).  None for anything else (generic pk allow-list path).
+
+    Filters that go through joins are never guessed from the WHERE tree: ``document__wiki__bot``
+    looks like ``document__wiki__processing__...__bot`` or ``wiki__bot`` at the target field, so only
+    the explicit hint selects the group path.  Hits are re-checked against the QuerySet by the caller
+    (search_service loads them with ``qs.filter(pk__in=...)``), so the database stays authoritative
+    even if a mirrored group bit is stale."""
     hint = getattr(qs, HINT_ATTR, None)
     if hint is not None:
         return hint
@@ -120,33 +127,35 @@ def index_filter_of(qs):
         return None
 
 
+def _base_alias(query):
+    base = getattr(query, "base_table", None)
+    if base is None:
+        alias_map = getattr(query, "alias_map", None) or {}
+        base = next(iter(alias_map), None)
+    return base
+
+
 def _recognise(qs, where):
+    """Only a join-free ``<fk document>__lt`` / ``id__lt`` on the searched model's own table."""
     if where.negated or where.connector != "AND" or qs.query.low_mark or qs.query.high_mark is not None:
         return None
-    bot = completed = doc_lt = None
-    for child in where.children:
-        if not hasattr(child, "lhs") or not hasattr(child, "rhs"):
-            return None
-        target = getattr(child.lhs, "target", None)
-        if target is None:
-            return None
-        label, name, lookup = target.model._meta.label_lower, target.name, child.lookup_name
-        rhs = getattr(child.rhs, "pk", child.rhs)
-        if label == "assistant_storage.wikidocument" and name == "bot" and lookup == "exact":
-            bot = int(rhs)
-        elif (label == "assistant_storage.wikidocumentprocessing" and name == "status" and lookup == "exact"
-              and rhs == "completed"):
-            completed = True
-        elif ((label == "assistant_storage.document" and name == "id")
-              or (label in ("assistant_storage.question", "assistant_storage.sentence") and name == "document")) \
-                and lookup == "lt":
-            doc_lt = int(rhs)
-        else:
-            return None
-    if bot is not None and completed and doc_lt is None:
-        return IndexFilter(group=int(row_group(bot, 1)))
-    if doc_lt is not None and bot is None and completed is None:
-        return IndexFilter(doc_lt=doc_lt)
+    if len(where.children) != 1:
+        return None
+    child = where.children[0]
+    if not hasattr(child, "lhs") or not hasattr(child, "rhs") or child.lookup_name != "lt":
+        return None
+    alias = getattr(child.lhs, "alias", None)
+    if alias is None or alias != _base_alias(qs.query):
+        return None
+    target = getattr(child.lhs, "target", None)
+    if target is None:
+        return None
+    label, name = target.model._meta.label_lower, target.name
+    if label != qs.model._meta.label_lower:
+        return None
+    if (label == "assistant_storage.document" and name == "id") or \
+            (label in ("assistant_storage.question", "assistant_storage.sentence") and name == "document"):
+        return IndexFilter(doc_lt=int(getattr(child.rhs, "pk", child.rhs)))
     return None
 
 

@@ -2,6 +2,7 @@
 from django.db import migrations, models
 
 import assistant.storage.fields
+from assistant.bot.migrations._schema import upgrade_safe
 
 LABELS = {
     "url": (models.URLField, {"blank": True, "null": True}, "URL"),
@@ -17,8 +18,9 @@ class Migration(migrations.Migration):
     dependencies = [("assistant_storage", "0001_initial")]
 
     operations = [
-        migrations.AddField("document", "content_embedding",
-                            assistant.storage.fields.VectorField(blank=True, dimensions=768, null=True)),
+        # upgrade_safe: databases of an earlier revision already have the column (bot _schema.py)
+        upgrade_safe(migrations.AddField("document", "content_embedding",
+                                         assistant.storage.fields.VectorField(blank=True, dimensions=768, null=True))),
     ] + [
         migrations.AlterField("wikidocument", name, cls(verbose_name=label, **kw))
         for name, (cls, kw, label) in LABELS.items()

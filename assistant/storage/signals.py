@@ -1,9 +1,10 @@
-"""Keeps the HBM index in sync with single-row saves / deletes (cascades included)."""
-from django.db.models.signals import post_delete, post_save
+"""Keeps the HBM index in sync with single-row saves / deletes (cascades included), and the rows'
+group bits (bot, COMPLETED run) in sync with the wiki they belong to."""
+from django.db.models.signals import post_delete, post_save, pre_save
 from django.dispatch import receiver
 
 from assistant.storage.index import get_index_service
-from assistant.storage.models import Document, Question, Sentence
+from assistant.storage.models import Document, Question, Sentence, WikiDocument, WikiDocumentProcessing
 
 
 @receiver(post_save, sender=Question)
@@ -28,3 +29,22 @@ def _embedding_deleted(sender, instance, **kwargs):
 @receiver(post_delete, sender=Document)
 def _document_deleted(sender, instance, **kwargs):
     get_index_service().remove(sender, [instance.pk], "content_embedding")
+
+
+@receiver(post_save, sender=WikiDocumentProcessing)
+def _processing_saved(sender, instance, **kwargs):
+    """A run's status changed (finalize, or an admin edit): re-mirror the wiki's completed bit."""
+    get_index_service().refresh_wiki(instance.wiki_document_id)
+
+
+@receiver(pre_save, sender=WikiDocument)
+def _wiki_stash_bot(sender, instance, **kwargs):
+    old = sender.objects.filter(pk=instance.pk).values_list("bot_id", flat=True).first() if instance.pk else None
+    instance._dab_old_bot_id = old
+
+
+@receiver(post_save, sender=WikiDocument)
+def _wiki_saved(sender, instance, created=False, **kwargs):
+    """A wiki moved to another bot: its rows change group."""
+    if not created and getattr(instance, "_dab_old_bot_id", instance.bot_id) != instance.bot_id:
+        get_index_service().refresh_wiki(instance.pk)

@@ -455,6 +455,11 @@ class LLMEngine:
             toks = self._sample(logits, reqs, to_host=not self.is_gpu)
         for r, s, n in chunks:
             r.computed = s + n
+            # register the chunk's full blocks in the prefix cache at launch: the hashes depend only
+            # on the tokens, and any forward that reuses them is enqueued behind this one on the
+            # stream, so a request admitted while this chunk's read-back is deferred already hits
+            # the shared prefix (e.g. the system prompt) instead of recomputing it
+            self.blocks.commit_prefix(r.seq, s + n)
         pend = (chunks, reqs, toks, t0)
         if self.is_gpu and _DEFER_PREFILL:
             self._pending_prefill = pend  # read back after the next launch (step)

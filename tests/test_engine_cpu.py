@@ -198,3 +198,32 @@ def test_split_prefill_matches_single_forward():
             eng.step()
         outs.append([eng.pop_output(r).token_ids for r in rids])
     assert outs[0] == outs[1]
+
+
+def test_prefix_blocks_are_shared_from_the_launch_of_their_chunk():
+    """full blocks of a prompt chunk enter the prefix cache when the chunk is launched, not
+    when the whole prompt (or the deferred read-back) completes.  A request that shares a long
+    prompt's first chunk and arrives while that prompt is still being prefilled reuses those blocks;
+    its tokens equal a cold run's."""
+    w = _weights()
+    greedy = SamplingParams(max_new_tokens=6, do_sample=False, temperature=0.0, ignore_eos=True)
+    shared = list(range(7, 7 + 128))
+    long_prompt = shared + list(range(400, 400 + 300))  # 428 tokens: two 256-token prefill chunks
+    other = shared + [900, 901, 902]
+    eng = LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(w), max_batch=8, block_size=16,
+                    num_blocks=96, max_prefill_tokens=256, use_graphs=False)
+    r1 = eng.add_request(long_prompt, greedy)
+    eng.step()  # first chunk (256 tokens) launched; the prompt is not complete yet
+    assert eng.stats["prefill_tokens"] == 256
+    r2 = eng.add_request(other, greedy)
+    before = eng.blocks.prefix_hits()
+    while eng.has_unfinished():
+        eng.step()
+    assert eng.blocks.prefix_hits() - before >= 128  # the shared 8 blocks came from the cache
+    cold = LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(w), max_batch=8, block_size=16,
+                     num_blocks=96, max_prefill_tokens=256, use_graphs=False, prefix_cache=False)
+    c2 = cold.add_request(other, greedy)
+    while cold.has_unfinished():
+        cold.step()
+    assert eng.pop_output(r2).token_ids == cold.pop_output(c2).token_ids
+    assert len(eng.pop_output(r1).token_ids) == 6

@@ -255,6 +255,41 @@ def test_paged_decode(Hq, Hkv, split):
         assert torch.equal(ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws), out)
 
 
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 4, 2)])
+@pytest.mark.parametrize("src", ["slabs", "bf16"])
+@pytest.mark.parametrize("split", [False, True])
+def test_paged_decode_rope_fused(D, Hq, Hkv, src, split):
+    """paged_decode_rope (RoPE + KV write in the decode attention's prologue) against the two-launch
+    form (rope_kv_write, then paged_decode): same attention output and same cache contents, bitwise,
+    and against the fp32 reference.  Contexts straddle block and 512-key partition edges; one padding
+    row (slot -1) must leave the cache untouched."""
+    ctx = [1, 64, 65, 511, 512, 513, 1300, 2049]
+    bs = 64
+    B = len(ctx)
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 160)
+    btc = bt.cpu()
+    slots = torch.tensor([int(btc[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctx)],
+                         dtype=torch.int64, device=DEV)
+    slots[2] = -1  # a padding row of a graph batch: no cache write
+    pos = torch.tensor([c - 1 for c in ctx], dtype=torch.int32, device=DEV)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    inv = ref.llama3_inv_freq(D, 500000.0, {"factor": 8.0})
+    cs = ref.rope_cos_sin(inv, 4096).to(DEV)
+    W = (Hq + 2 * Hkv) * D
+    qkv = torch.randn(4, B, W, device=DEV) if src == "slabs" else bf(B, W)
+    ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / 512), DEV) if split else None
+    kc1, vc1 = kc.clone(), vc.clone()
+    q = ops.rope_kv_write(qkv, pos, cs, kc1, vc1, slots, Hq, Hkv, D)
+    exp = ops.paged_decode(q, kc1, vc1, bt, ctxt, 512, ws)
+    kc2, vc2 = kc.clone(), vc.clone()
+    got = ops.paged_decode_rope(qkv, pos, cs, slots, kc2, vc2, bt, ctxt, Hq, 512, ws)
+    assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1)
+    assert torch.equal(got, exp)
+    close(got, ref.paged_decode(q, kc1, vc1, bt, ctxt, 1 / math.sqrt(D)))
+    if split:
+        assert int(ws.cnt.abs().sum()) == 0
+
+
 @pytest.mark.parametrize("M,N,K", [(200, 384, 256), (1, 2304, 768), (513, 1000, 64), (128, 128, 4096)])
 def test_gemm_epilogues(M, N, K):
     A, B = bf(M, K), bf(N, K, scale=0.05)

@@ -201,3 +201,53 @@ def test_storage_migration_chain_matches_models(stub):
 def test_broadcasting_depends_on_last_bot_migration(stub):
     m = _load(ROOT / "assistant" / "broadcasting" / "migrations" / "0001_initial.py", "_mig_bc")
     assert ("assistant_bot", BOT_CHAIN[-1]) in m.Migration.dependencies
+
+
+def test_upgrade_guard_keeps_a_collapsed_schema_and_replays_a_fresh_one(stub):
+    """a database created by this package's earlier collapsed bot 0001 (final tables
+    already there, 0001_initial recorded) must not lose its Message / Dialog / Instance tables when
+    0002+ run, and 0003 / 0004 / 0006 / storage 0002 must not fail on objects that exist.  A fresh
+    database still gets every operation.  Replays the guard decisions against both schemas."""
+    sch = _load(ROOT / "assistant" / "bot" / "migrations" / "_schema.py", "_mig_bot")
+    final = {"assistant_bot_bot": {"id", "codename", "telegram_token"},
+             "assistant_bot_role": {"id", "name"},
+             "assistant_bot_botuser": {"id", "user_id", "platform", "phone_number"},
+             "assistant_bot_instance": {"id", "bot_id", "user_id", "state", "is_unavailable"},
+             "assistant_bot_dialog": {"id", "instance_id"},
+             "assistant_bot_message": {"id", "dialog_id", "photo"}}
+    fresh_after_0001 = {"assistant_bot_bot": {"id"}, "assistant_bot_role": {"id"},
+                        "assistant_bot_instance": {"id", "user_id"}, "assistant_bot_dialog": {"id"},
+                        "assistant_bot_message": {"id"}}
+
+    def run(schema):
+        tables = dict(schema)
+        cols = tables.__getitem__
+        ran = []
+        for name in ("Message", "Dialog", "Instance"):  # 0002
+            if sch.op_needed("DeleteModel", tables, cols):
+                tables.pop(f"assistant_bot_{name.lower()}")
+                ran.append(f"drop {name}")
+        for name in ("BotUser", "Instance", "Dialog", "Message"):  # 0003
+            if sch.op_needed("CreateModel", tables, cols, model=name):
+                tables[f"assistant_bot_{name.lower()}"] = {"id"}
+                ran.append(f"create {name}")
+        for model, col in (("message", "photo"), ("botuser", "phone_number"), ("instance", "is_unavailable")):
+            if sch.op_needed("AddField", tables, cols, model=model, column=col):  # 0004, 0006
+                tables[f"assistant_bot_{model}"].add(col)
+                ran.append(f"add {model}.{col}")
+        return ran, tables
+
+    ran, tables = run(final)
+    assert ran == [] and tables == final  # nothing dropped, nothing re-created
+    ran, tables = run(fresh_after_0001)
+    assert ran == ["drop Message", "drop Dialog", "drop Instance", "create BotUser", "create Instance",
+                   "create Dialog", "create Message", "add message.photo", "add botuser.phone_number",
+                   "add instance.is_unavailable"]
+    assert set(tables) == set(final)
+    # storage 0002 on a schema that already has the column
+    doc = {"assistant_storage_document": {"id", "content_embedding"}}
+    assert not sch.op_needed("AddField", doc, doc.__getitem__, app_label="assistant_storage", model="document",
+                             column="content_embedding")
+    assert sch.op_needed("AddField", {"assistant_storage_document": {"id"}},
+                         {"assistant_storage_document": {"id"}}.__getitem__, app_label="assistant_storage",
+                         model="document", column="content_embedding")

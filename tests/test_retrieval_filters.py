@@ -114,8 +114,10 @@ def _field(label, name):
     return types.SimpleNamespace(model=types.SimpleNamespace(_meta=_Meta(label)), name=name)
 
 
-def _lookup(label, name, lookup, rhs):
-    return types.SimpleNamespace(lhs=types.SimpleNamespace(target=_field(label, name)), lookup_name=lookup, rhs=rhs)
+def _lookup(label, name, lookup, rhs, alias="T0"):
+    """A WHERE-tree leaf as Django builds it: ``lhs`` is a Col with the table alias it reads."""
+    return types.SimpleNamespace(lhs=types.SimpleNamespace(target=_field(label, name), alias=alias),
+                                 lookup_name=lookup, rhs=rhs)
 
 
 class _Where(list):
@@ -130,7 +132,7 @@ class _Where(list):
 class StubQS:
     def __init__(self, children, pks=()):
         self.model = types.SimpleNamespace(_meta=_Meta("assistant_storage.question"))
-        self.query = types.SimpleNamespace(where=_Where(children), low_mark=0, high_mark=None)
+        self.query = types.SimpleNamespace(where=_Where(children), low_mark=0, high_mark=None, base_table="T0")
         self._pks = list(pks)
         self.values_list_calls = 0
 
@@ -139,19 +141,25 @@ class StubQS:
         return list(self._pks)
 
 
-def test_recognises_the_two_framework_filter_shapes():
+def test_recognises_only_join_free_document_bounds():
+    """Join-free ``document__id__lt`` (ingest dedup) is evaluated in the index.  Filters through joins
+    are never guessed from the WHERE tree (``document__wiki__bot`` and
+    ``document__processing__status`` share target fields with the framework's hot filter but not its
+    meaning): they take the pk allow-list path unless the call site attached the hint."""
     bot = types.SimpleNamespace(pk=3)
-    hot = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot),
-                  _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed")])
-    f = index_mod.index_filter_of(hot)
-    assert f.group == int(index_mod.row_group(3, 1)) and f.doc_lt is None
+    hot = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot, alias="T2"),
+                  _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed", alias="T3")])
+    assert index_mod.index_filter_of(hot) is None
+    doc_status = StubQS([_lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed",
+                                 alias="T4")])
+    assert index_mod.index_filter_of(doc_status) is None
     dedup = StubQS([_lookup("assistant_storage.question", "document", "lt", 41)])
     assert index_mod.index_filter_of(dedup).doc_lt == 41
+    joined_lt = StubQS([_lookup("assistant_storage.question", "document", "lt", 41, alias="T7")])
+    assert index_mod.index_filter_of(joined_lt) is None
     assert index_mod.index_filter_of(StubQS([])).group is None
     other = StubQS([_lookup("assistant_storage.question", "text", "icontains", "x")])
     assert index_mod.index_filter_of(other) is None
-    mixed = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", 3)])  # bot without status
-    assert index_mod.index_filter_of(mixed) is None
 
 
 def test_hint_wins_over_recognition():
@@ -166,8 +174,10 @@ def test_service_fast_and_generic_paths_equal_oracle(data, monkeypatch):
     monkeypatch.setattr(svc, "ensure_loaded", lambda *a: None)
     q = np.random.default_rng(5).standard_normal(DIM).astype(np.float32)
     bot = 2
-    hot = StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot),
-                  _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed")])
+    hot = index_mod.with_index_filter(
+        StubQS([_lookup("assistant_storage.wikidocument", "bot", "exact", bot, alias="T2"),
+                _lookup("assistant_storage.wikidocumentprocessing", "status", "exact", "completed", alias="T3")]),
+        bot=bot, completed=True)
     got = svc.search(hot, q, 250)
     assert hot.values_list_calls == 0 and svc.stats["fast"] == 1
     exp, _ = oracle(vecs, ids, q, 250, groups == index_mod.row_group(bot, 1))
@@ -179,3 +189,30 @@ def test_service_fast_and_generic_paths_equal_oracle(data, monkeypatch):
     got2 = svc.search(gen, q, 250)
     assert gen.values_list_calls == 1 and svc.stats["generic"] == 1
     assert [p for p, _ in got2] == [p for p, _ in got]
+
+
+class _Obj:
+    def __init__(self, pk):
+        self.pk = pk
+
+
+class _FilterQS:
+    """QuerySet stub whose ``filter(pk__in=...)`` applies its own membership (the DB's answer)."""
+
+    def __init__(self, members):
+        self.members = set(members)
+        self.model = types.SimpleNamespace(objects=self)
+
+    def filter(self, pk__in):
+        return [_Obj(p) for p in pk__in if p in self.members]
+
+    def in_bulk(self, pks):  # pragma: no cover - must not be used when filter works
+        raise AssertionError("in_bulk bypasses the QuerySet filter")
+
+
+def test_hits_are_rechecked_against_the_queryset():
+    """A row the index returns but the QuerySet excludes (stale group bit) never reaches the caller."""
+    from assistant.rag.services.search_service import _load_within
+
+    got = _load_within(_FilterQS({1, 2, 5}), [5, 9, 1])
+    assert sorted(got) == [1, 5]

@@ -139,3 +139,37 @@ def test_sync_lock_serialises_threads(instance_service):
     for t in ts:
         t.join()
     assert not overlap
+
+
+def test_cancelled_acquire_releases_the_session_lock(instance_service):
+    """a coroutine cancelled while the thread-sensitive worker is still inside
+    pg_advisory_lock must not leak that session lock: the acquire completes, is released on the
+    same thread, the in-process key lock is dropped, and CancelledError still reaches the caller."""
+    mod, calls = instance_service
+    inst = types.SimpleNamespace(id=7)
+    real = mod.BaseInstanceLock._db_acquire
+
+    def slow_acquire(self):
+        import time
+
+        time.sleep(0.2)
+        real(self)
+
+    mod.BaseInstanceLock._db_acquire = slow_acquire
+    try:
+        async def main():
+            task = asyncio.ensure_future(mod.InstanceLockAsync(inst).__aenter__())
+            await asyncio.sleep(0.05)
+            task.cancel()
+            with pytest.raises(asyncio.CancelledError):
+                await task
+            # the key lock is free again: a new holder gets through at once
+            async with mod.InstanceLockAsync(inst):
+                pass
+
+        asyncio.run(main())
+    finally:
+        mod.BaseInstanceLock._db_acquire = real
+    names = [c[0] for c in calls]
+    assert names == ["SELECT pg_advisory_lock", "SELECT pg_advisory_unlock"] * 2
+    assert calls[0][1] == calls[1][1]
