@@ -33,9 +33,14 @@ def rand(shape, scale=1.0):
     return ((torch.rand(shape, device="cuda") * 2 - 1) * scale).to(torch.bfloat16)
 
 
-def run_native(a, w, b, kind, out):
-    epi = {"none": ops.EPI_NONE, "bias": ops.EPI_NONE, "gelu": ops.EPI_GELU, "swiglu": ops.EPI_SWIGLU}[kind]
-    return ops.gemm_bt(a, w, bias=b if kind in ("bias", "gelu") else None, epilogue=epi, out=out)
+EPI = {"none": ops.EPI_NONE, "bias": ops.EPI_NONE, "gelu": ops.EPI_GELU, "swiglu": ops.EPI_SWIGLU8}
+
+
+def run_native(a, w, b, kind, out, shuffled):
+    """The layer's own call: the decoder keeps every projection in the fragment layout
+    (``shuffle_weights``) and gate/up interleaved in 8-row groups (EPI_SWIGLU8)."""
+    return ops.gemm_bt(a, w, bias=b if kind in ("bias", "gelu") else None, epilogue=EPI[kind], out=out,
+                       shuffled=shuffled)
 
 
 def run_lib(a, w, b, kind):
@@ -51,8 +56,7 @@ def run_lib(a, w, b, kind):
 def check(a, w, b, kind, out, rows):
     idx = torch.cat([torch.arange(0, min(rows, a.shape[0]), device="cuda"),
                      torch.arange(max(0, a.shape[0] - rows), a.shape[0], device="cuda")]).unique()
-    ref = ops.reference.gemm_bt(a[idx], w, b if kind in ("bias", "gelu") else None, None,
-                                {"none": 0, "bias": 0, "gelu": ops.EPI_GELU, "swiglu": ops.EPI_SWIGLU}[kind],
+    ref = ops.reference.gemm_bt(a[idx], w, b if kind in ("bias", "gelu") else None, None, EPI[kind],
                                 out_f32=True)
     got = out[idx].float()
     err = (got - ref).abs().max().item()
@@ -67,10 +71,9 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
     ap.add_argument("--only", default="", help="comma list of op names to run")
-    ap.add_argument("--gm", default="", help="comma list of tile-group sizes to A/B (DAB_GEMM256_GM)")
-    ap.add_argument("--ab-persist", action="store_true", help="also time one-workgroup-per-tile launches")
+    ap.add_argument("--ab-layout", action="store_true",
+                    help="llama shapes: also time the row-major weight layout (arm 'rowmajor')")
     args = ap.parse_args()
-    os.environ.setdefault("DAB_GEMM256", "1")
     torch.manual_seed(0)
     for group in args.shapes.split(","):
         for name, M, N, K, kind in SHAPES[group]:
@@ -81,31 +84,18 @@ def main():
             b = rand((N,), 0.5)
             n_out = N // 2 if kind == "swiglu" else N
             out = torch.empty((M, n_out), dtype=torch.bfloat16, device="cuda")
-            run_native(a, w, b, kind, out)
+            frag = group == "llama"
+            ws = ops.shuffle_weights(w) if frag else w
+            run_native(a, ws, b, kind, out, frag)
             torch.cuda.synchronize()
             err, scale = check(a, w, b, kind, out, 256)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
             nat, lib = [], []
-            arms = [("nat", lambda: run_native(a, w, b, kind, out)), ("lib", lambda: run_lib(a, w, b, kind))]
+            arms = [("nat", lambda: run_native(a, ws, b, kind, out, frag)), ("lib", lambda: run_lib(a, w, b, kind))]
             if args.native_only:
                 arms = arms[:1]
-            for gm in [int(x) for x in args.gm.split(",") if x]:
-                def gm_arm(gm=gm):
-                    os.environ["DAB_GEMM256_GM"] = str(gm)
-                    try:
-                        run_native(a, w, b, kind, out)
-                    finally:
-                        os.environ.pop("DAB_GEMM256_GM", None)
-                arms.append((f"gm{gm}", gm_arm))
-            if args.ab_persist:
-                def nonp():
-                    os.environ["DAB_GEMM256_PERSIST"] = "0"
-                    try:
-                        run_native(a, w, b, kind, out)
-                    finally:
-                        os.environ["DAB_GEMM256_PERSIST"] = "1"
-                arms.append(("np", nonp))
-            npers = []
+            if args.ab_layout and frag:
+                arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
             extra = {}
             for _ in range(args.rounds):
                 for arm, fn in arms:
@@ -116,8 +106,8 @@ def main():
                     ev[1].record()
                     torch.cuda.synchronize()
                     t = ev[0].elapsed_time(ev[1]) / args.iters * 1e3
-                    extra.setdefault(arm, []).append(t) if arm not in ("nat", "lib", "np") else \
-                        {"nat": nat, "lib": lib, "np": npers}[arm].append(t)
+                    extra.setdefault(arm, []).append(t) if arm not in ("nat", "lib") else \
+                        {"nat": nat, "lib": lib}[arm].append(t)
             nat.sort()
             lib.sort()
             lib = lib or [float("nan")]
@@ -129,10 +119,9 @@ def main():
                               "native_tflops": round(flop / tn / 1e6, 1), "lib_tflops": round(flop / tl / 1e6, 1),
                               "speedup": round(tl / tn, 3), "max_abs_err": round(err, 5),
                               "ref_max": round(scale, 3), "ok": err <= 0.02 * max(scale, 1.0),
-                              **({"nonpersist_us": round(sorted(npers)[len(npers) // 2], 1)} if npers else {}),
                               **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()}}),
                   flush=True)
-            del a, w, b, out
+            del a, w, ws, b, out
             torch.cuda.empty_cache()
 
 

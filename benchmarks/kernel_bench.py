@@ -1,6 +1,6 @@
 """Per-kernel timings on the real model shapes (bf16, random data).
 
-GEMM: native MFMA ``gemm_bt`` vs hipBLASLt (torch.nn.functional.linear) on the Llama-3-8B decode /
+GEMM: native MFMA ``gemm_bt`` (row-major B) vs hipBLASLt (torch.nn.functional.linear) on the Llama-3-8B decode /
 prefill and bge-base encoder projections; attention: flash prefill, paged decode; selection kernels.
 Prints one JSON line per measurement (TFLOP/s and effective GB/s).
 """
@@ -52,26 +52,6 @@ def gemm_suite(which):
         flop = 2.0 * M * N * K
         byts = 2.0 * (M * K + N * K + M * N)
         res = {"op": name, "M": M, "N": N, "K": K}
-        if M <= ops.SKINNY_MAX_M and name.startswith("llama8b"):
-            S = ops.skinny_splits(N, K)
-            slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
-            t_sk = timeit(lambda: ops.skinny_gemm(a, b, splits=S, out=slabs))
-            res.update(skinny_splits=S, skinny_us=round(t_sk * 1e6, 1), skinny_gbps=round(byts / t_sk / 1e9))
-            # cold weights (decode streams 16 GB per step, nothing stays in L2/MALL): rotate copies
-            ncopy = max(2, int(2e9 // (N * K * 2)) + 1)
-            ws = [b] + [b.clone() for _ in range(ncopy - 1)]
-            it = [0]
-
-            def nxt():
-                it[0] = (it[0] + 1) % ncopy
-                return ws[it[0]]
-            t_c = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=False), iters=ncopy * 2)
-            t_cn = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=True), iters=ncopy * 2)
-            t_cl = timeit(lambda: F.linear(a, nxt()), iters=ncopy * 2)
-            res.update(cold_skinny_us=round(t_c * 1e6, 1), cold_skinny_nt_us=round(t_cn * 1e6, 1),
-                       cold_hipblaslt_us=round(t_cl * 1e6, 1), cold_skinny_gbps=round(byts / t_c / 1e9),
-                       cold_hipblaslt_gbps=round(byts / t_cl / 1e9))
-            del ws
         if name == "index-scan":
             t_nat = timeit(lambda: ops.gemm_bt(a, b, epilogue=ops.EPI_SCORES, out_f32=True), iters=5)
             t_lib = timeit(lambda: torch.mm(a, b.t()).float(), iters=5)
@@ -84,41 +64,6 @@ def gemm_suite(which):
                    native_gbps=round(byts / t_nat / 1e9), hipblaslt_gbps=round(byts / t_lib / 1e9))
         emit(**res)
         del a, b
-
-
-def skinny_sweep(which):
-    """Split-count sweep of the weight-streaming GEMM at decode batch sizes (cold weights), with the
-    slab reduction timed separately (in the model the consumer kernel sums the slabs)."""
-    for M in (64, 96, 128):
-        for name, N, K in (("llama8b-qkv", 6144, 4096), ("llama8b-o", 4096, 4096), ("llama8b-gateup", 28672, 4096),
-                           ("llama8b-down", 4096, 14336)):
-            if which and which not in name:
-                continue
-            a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
-            ncopy = max(2, int(2e9 // (N * K * 2)) + 1)
-            ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
-            it = [0]
-
-            def nxt():
-                it[0] = (it[0] + 1) % ncopy
-                return ws[it[0]]
-            byts = 2.0 * N * K
-            res = {"op": name, "M": M, "N": N, "K": K,
-                   "cold_hipblaslt_us": round(timeit(lambda: F.linear(a, nxt()), iters=ncopy * 2) * 1e6, 1)}
-            for S in (1, 2, 4, 8):
-                if K % (S * 256):
-                    continue
-                slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
-                for nt in (False, True):
-                    t = timeit(lambda: ops.skinny_gemm(a, nxt(), splits=S, out=slabs, nt=nt), iters=ncopy * 2)
-                    res[f"S{S}{'nt' if nt else ''}_us"] = round(t * 1e6, 1)
-                if S > 1:
-                    t_r = timeit(lambda: ops.skinny_reduce(slabs))
-                    res[f"S{S}_reduce_us"] = round(t_r * 1e6, 1)
-            res["weights_tbps_best"] = round(byts / min(v for k, v in res.items() if k.startswith("S") and
-                                                        k.endswith("_us") and "reduce" not in k) / 1e6, 2)
-            emit(**res)
-            del ws
 
 
 def graph_time(calls, reps=5):
@@ -151,8 +96,8 @@ def graph_time(calls, reps=5):
 
 def stream_sweep(which, Ms=(128,)):
     """Decode projections of Llama-3-8B (+ LM head) at decode batch M with cold weights (a rotation
-    of > 2 GB of weight copies, as in a decode step that streams 16 GB): hipBLASLt vs the split-K
-    skinny kernel vs the warp-specialised stream kernel per configuration and split count.  Graph-
+    of > 2 GB of weight copies, as in a decode step that streams 16 GB): hipBLASLt vs the
+    warp-specialised stream kernel per configuration and split count.  Graph-
     timed, microseconds per call."""
     shapes = (("qkv", 6144, 4096), ("o", 4096, 4096), ("gate_up", 28672, 4096), ("down", 4096, 14336),
               ("lm_head", 128256, 4096))
@@ -169,11 +114,6 @@ def stream_sweep(which, Ms=(128,)):
             ws = [(torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16) for _ in range(ncopy)]
             res = {"op": name, "M": M, "N": N, "K": K, "weights_mb": round(N * K * 2 / 1e6, 1)}
             res["hipblaslt_us"] = round(graph_time([lambda w=w: F.linear(a, w) for w in ws]) * 1e6, 1)
-            if M <= ops.SKINNY_MAX_M and N % 64 == 0:
-                S = ops.skinny_splits(N, K)
-                slabs = torch.empty((S, M, N), dtype=torch.float32, device="cuda") if S > 1 else None
-                res[f"skinny_S{S}_us"] = round(graph_time(
-                    [lambda w=w: ops.skinny_gemm(a, w, splits=S, out=slabs) for w in ws]) * 1e6, 1)
             for cfg in cfgs:
                 bn, mm = ops.native().stream_gemm_bn(cfg), ops.native().stream_gemm_max_m(cfg)
                 if M > mm or N % bn:
@@ -306,8 +246,6 @@ def select_suite():
 
 if __name__ == "__main__":
     which = sys.argv[1] if len(sys.argv) > 1 else "all"
-    if which == "skinny":
-        skinny_sweep(sys.argv[2] if len(sys.argv) > 2 else None)
     if which == "stream":
         stream_sweep(sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "all" else None,
                      tuple(int(m) for m in sys.argv[3].split(",")) if len(sys.argv) > 3 else (128,))

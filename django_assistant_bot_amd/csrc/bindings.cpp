@@ -130,27 +130,38 @@ PYBIND11_MODULE(_native, m) {
   m.def("destroy_stream", [](u s) { check(hipStreamDestroy(ST(s)), "hipStreamDestroy"); });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
                                      u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
-                                     float scale, u s, u order) {
+                                     float scale, u s, u order, u rope_qkv, u rope_slabs, int rope_S,
+                                     long rope_slab_stride, int rope_ld, u rope_pos, u rope_cs, u rope_slots) {
+    dab::DecodeRopeArgs rope{CVP(rope_qkv), (const float*)rope_slabs, rope_S, rope_slab_stride, rope_ld,
+                             (const int*)rope_pos, CVP(rope_cs), (const int64_t*)rope_slots};
     check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
                                       (float*)po, (float*)pm, (float*)pl, (int*)cnt, batch, Hq, Hkv, D, part_size,
-                                      max_parts, scale, ST(s), (const int*)order),
+                                      max_parts, scale, ST(s), (const int*)order, rope_pos ? &rope : nullptr),
           "paged_decode_attention");
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("max_blocks"), py::arg("bs"), py::arg("ctx"),
      py::arg("out"), py::arg("po"), py::arg("pm"), py::arg("pl"), py::arg("cnt"), py::arg("batch"), py::arg("Hq"),
      py::arg("Hkv"), py::arg("D"), py::arg("part_size"), py::arg("max_parts"), py::arg("scale"), py::arg("s"),
-     py::arg("order") = 0);
+     py::arg("order") = 0, py::arg("rope_qkv") = 0, py::arg("rope_slabs") = 0, py::arg("rope_S") = 0,
+     py::arg("rope_slab_stride") = 0, py::arg("rope_ld") = 0, py::arg("rope_pos") = 0, py::arg("rope_cs") = 0,
+     py::arg("rope_slots") = 0);
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
-                      int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s) {
+                      int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s, int b_rows) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
-                       (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s)),
+                       (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s), b_rows),
           "gemm_bt");
-  });
+  }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
+     py::arg("residual"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"),
+     py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
+     py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
   m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
-                      int epilogue, u s) {
-    check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s)),
+                      int epilogue, u s, int b_shuf) {
+    check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s),
+                       b_shuf),
           "gemm256");
-  });
+  }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
+     py::arg("residual"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("s"),
+     py::arg("b_shuf") = 0);
   m.def("gemm_score_candidates", [](u A, long lda, u B, long ldb, int M, int N, int K, u row_group, u q_group, u thr,
                                     u cnt, u cand_val, u cand_idx, int cap, u s) {
     check(dab::gemm_score_candidates(CVP(A), lda, CVP(B), ldb, M, N, K, reinterpret_cast<const int*>(row_group),
@@ -159,10 +170,10 @@ PYBIND11_MODULE(_native, m) {
                                      reinterpret_cast<int*>(cand_idx), cap, ST(s)),
           "gemm_score_candidates");
   });
-  // candidates over a shuffle_weights copy of the rows: 1..16 queries on the persistent scan,
-  // 17..128 on the weight-streaming kernel
+  // candidates over a shuffle_weights copy of the rows (b_rows of them): 1..16 queries on the
+  // persistent scan, 17..128 on the weight-streaming kernel, more on the 8-phase GEMM
   m.def("score_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
-                                    u cnt, u cand_val, u cand_idx, int cap, u s) {
+                                    u cnt, u cand_val, u cand_idx, int cap, u s, int b_rows) {
     auto* rg = reinterpret_cast<const int*>(row_group);
     auto* qg = reinterpret_cast<const int*>(q_group);
     auto* th = reinterpret_cast<const float*>(thr);
@@ -170,19 +181,16 @@ PYBIND11_MODULE(_native, m) {
     auto* cv = reinterpret_cast<float*>(cand_val);
     auto* ci = reinterpret_cast<int*>(cand_idx);
     int rc = hipErrorInvalidValue;
-    if (M <= 16)
+    if (M <= 16 && K % 256 == 0 && K <= 1024)
       rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
     else if (M <= 128)
       rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
+    else
+      rc = dab::gemm_score_candidates(CVP(A), lda, CVP(Wshuf), K, M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s), b_rows);
     check(rc, "score_candidates_shuf");
-  });
-  m.def("skinny_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
-                          int S, int epilogue, u s, int nt) {
-    check(dab::skinny_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt),
-          "skinny_gemm");
-  }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
-     py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
-     py::arg("nt") = 0);
+  }, py::arg("A"), py::arg("lda"), py::arg("Wshuf"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("row_group"),
+     py::arg("q_group"), py::arg("thr"), py::arg("cnt"), py::arg("cand_val"), py::arg("cand_idx"), py::arg("cap"),
+     py::arg("s"), py::arg("b_rows") = 0);
   m.def("stream_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
                           int S, int epilogue, u s, int nt, int cfg) {
     check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
@@ -192,8 +200,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
   m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);
-  m.def("skinny_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
-    check(dab::skinny_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "skinny_reduce");
+  m.def("slab_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
+    check(dab::slab_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "slab_reduce");
   });
   m.def("sample_tokens", [](u logits, int f32, long ld, int rows, int vocab, u temp, u top_k, u top_p,
                             unsigned long long seed, u counters, u out_tokens, u out_logprobs, u s) {

@@ -14,7 +14,9 @@
 //     involution applied on the ds_read_b128 side -> conflict-free fragment reads;
 //   * operands swapped in the MFMA (B rows feed the A slot) so each lane ends with 4 consecutive
 //     output columns of one row -> 8-B / 16-B epilogue stores;
-//   * bijective XCD-aware block remap (T1) so neighbouring tiles share an XCD's L2.
+//   * bijective XCD-aware block remap (T1) so neighbouring tiles share an XCD's L2;
+//   * SHUF: B in the ops.shuffle_weights fragment layout (the one weight copy the decode GEMM also
+//     streams): each 1 KB staging piece is one 16-row x 32-k block, read back lane-linearly.
 #include <cstdlib>
 
 #include "common.h"
@@ -22,7 +24,8 @@
 
 namespace dab {
 
-enum EpiMode { EPI_NONE = 0, EPI_GELU = 1, EPI_SWIGLU = 2, EPI_SCORES = 3, EPI_CANDIDATES = 4 };
+// EPI_SWIGLU8 = ops EPI_SWIGLU8 (4); EPI_CANDIDATES is internal (gemm_score_candidates)
+enum EpiMode { EPI_NONE = 0, EPI_GELU = 1, EPI_SWIGLU = 2, EPI_SCORES = 3, EPI_SWIGLU8 = 4, EPI_CANDIDATES = 5 };
 
 struct GemmParams {
   const bf16* A;
@@ -44,11 +47,12 @@ struct GemmParams {
   float* cand_val;   // [M, cap]
   int* cand_idx;     // [M, cap] column n
   int cap;
+  int rows_b;  // SHUF: rows of the B copy (>= N, multiple of 16)
 };
 
 __device__ __forceinline__ int gsw(int r) { return 2 * ((r >> 1) & 3); }
 
-template <int EPI, int BM, int BN, int WGM, int WGN>
+template <int EPI, int BM, int BN, int WGM, int WGN, bool SHUF = false>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
   constexpr int BK = 64;
   constexpr int NW = WGM * WGN;            // waves
@@ -85,12 +89,19 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
     }
 #pragma unroll
     for (int c = 0; c < BN / (8 * NW); ++c) {
-      const int e = (c * NW + w) * 64 + lane;
-      const int r = e >> 3, pos = e & 7;
-      const int rb = min(n0 + r, p.N - 1);
-      const bf16* gb = p.B + (size_t)rb * p.ldb + k0 + (pos ^ gsw(r)) * 8;
+      const int idx = c * NW + w;
+      const bf16* gb;
+      if constexpr (SHUF) {  // piece idx = 16-row block idx / 2, 32-k block idx % 2 (clamped past the copy)
+        const int blk = min(n0 / 16 + (idx >> 1), p.rows_b / 16 - 1);
+        gb = p.B + ((size_t)blk * (p.K / 32) + k0 / 32 + (idx & 1)) * 512 + lane * 8;
+      } else {
+        const int e = idx * 64 + lane;
+        const int r = e >> 3, pos = e & 7;
+        const int rb = min(n0 + r, p.N - 1);
+        gb = p.B + (size_t)rb * p.ldb + k0 + (pos ^ gsw(r)) * 8;
+      }
       __builtin_amdgcn_global_load_lds((const void*)gb,
-                                       (__attribute__((address_space(3))) void*)(Bs + (c * NW + w) * 1024), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(Bs + idx * 1024), 16, 0, 0);
     }
   };
 
@@ -118,8 +129,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
       }
 #pragma unroll
       for (int i = 0; i < NI; ++i) {
-        const int rb = wn * TN + 16 * i + li;
-        bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + 16 * ((4 * ks + g) ^ gsw(rb)));
+        if constexpr (SHUF) {
+          bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + (2 * ((wn * TN) / 16 + i) + ks) * 1024 + lane * 16);
+        } else {
+          const int rb = wn * TN + 16 * i + li;
+          bfr[i] = *reinterpret_cast<const bf16x8*>(Bs + rb * 128 + 16 * ((4 * ks + g) ^ gsw(rb)));
+        }
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -131,6 +146,33 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
   }
 
   // epilogue: acc[ni][mi][r] = C[m = m0 + wm*TM + 16 mi + li][n = n0 + wn*TN + 16 ni + 4 g + r]
+  if constexpr (EPI == EPI_SWIGLU8) {
+    // 8-row [gate | up] groups inside each 16-row block: v_permlane32_swap of blocks (2 pi, 2 pi + 1)
+    // hands lanes 0-31 block 2 pi's gate / up rows and lanes 32-63 block 2 pi + 1's (gemm256.hip);
+    // the swap runs with every lane active, the row / column bounds only guard the stores
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m = m0 + wm * TM + 16 * mi + li;
+#pragma unroll
+      for (int pi = 0; pi < NI / 2; ++pi) {
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[2 * pi][mi][r]),
+                                                           __float_as_uint(acc[2 * pi + 1][mi][r]), false, false);
+          o[r] = silu_f(__uint_as_float(sw[0])) * __uint_as_float(sw[1]);
+        }
+        const int oc = (n0 + wn * TN) / 2 + 16 * pi + 4 * g;
+        if (m < p.M && 2 * oc < p.N) {
+          u32x2 v;
+          v[0] = pack2bf(o[0], o[1]);
+          v[1] = pack2bf(o[2], o[3]);
+          *reinterpret_cast<u32x2*>((bf16*)p.C + (size_t)m * p.ldc + oc) = v;
+        }
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi) {
     const int m = m0 + wm * TM + 16 * mi + li;
@@ -219,24 +261,31 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
   }
 }
 
-template <int EPI>
+template <int EPI, bool SHUF>
 static int launch_gemm(const GemmParams& p, bool big, hipStream_t s) {
   if (big) {
     const int nwg = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 256, 256, 2, 4>), dim3(nwg), dim3(512), 0, s, p);
+    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 256, 256, 2, 4, SHUF>), dim3(nwg), dim3(512), 0, s, p);
   } else {
     const int nwg = ((p.M + 127) / 128) * ((p.N + 127) / 128);
-    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 128, 128, 2, 2>), dim3(nwg), dim3(256), 0, s, p);
+    hipLaunchKernelGGL((gemm_bt_kernel<EPI, 128, 128, 2, 2, SHUF>), dim3(nwg), dim3(256), 0, s, p);
   }
   return hipGetLastError();
 }
 
+template <int EPI>
+static int launch_gemm(const GemmParams& p, bool big, hipStream_t s, bool shuf) {
+  return shuf ? launch_gemm<EPI, true>(p, big, s) : launch_gemm<EPI, false>(p, big, s);
+}
+
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
-            const uint32_t* allow, int allow_words, hipStream_t s) {
+            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 64 || N % 4 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
   if (epilogue == EPI_SWIGLU && (N % 32 || out_f32)) return hipErrorInvalidValue;
+  if (epilogue == EPI_SWIGLU8 && (N % 32 || out_f32 || bias || residual)) return hipErrorInvalidValue;
+  if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
   GemmParams p;
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
@@ -255,44 +304,41 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   p.ldr = ldr;
   p.allow_words = allow_words;
   p.out_f32 = out_f32;
+  p.rows_b = b_rows;
+  const bool sh = b_rows > 0;
   // large problems: 256x256 tiles, 8 waves of 128x64 (half the LDS fragment traffic per MFMA of the
   // 64x64 wave tile); small M or N: 128x128 tiles, 4 waves (less padding, more workgroups)
   const bool big = M >= 2048 && N >= 512 && ((long)((M + 255) / 256) * ((N + 255) / 256)) >= 160;
   switch (epilogue) {
-    case EPI_NONE: return launch_gemm<EPI_NONE>(p, big, s);
-    case EPI_GELU: return launch_gemm<EPI_GELU>(p, big, s);
-    case EPI_SWIGLU: return launch_gemm<EPI_SWIGLU>(p, big, s);
-    case EPI_SCORES: return launch_gemm<EPI_SCORES>(p, big, s);
+    case EPI_NONE: return launch_gemm<EPI_NONE>(p, big, s, sh);
+    case EPI_GELU: return launch_gemm<EPI_GELU>(p, big, s, sh);
+    case EPI_SWIGLU: return launch_gemm<EPI_SWIGLU>(p, big, s, sh);
+    case EPI_SCORES: return launch_gemm<EPI_SCORES>(p, big, s, sh);
+    case EPI_SWIGLU8: return launch_gemm<EPI_SWIGLU8>(p, big, s, sh);
     default: return hipErrorInvalidValue;
   }
 }
 
+// b_rows > 0: B is a shuffle_weights copy of b_rows >= N rows (the index's one row layout).
 int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                          hipStream_t s) {
+                          hipStream_t s, int b_rows) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 64 || N % 4 || lda % 8 || ldb % 8 || cap <= 0 || !thr || !cnt || !cand_val || !cand_idx)
     return hipErrorInvalidValue;
+  if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
   // query batches that fill 256-row tiles: the persistent 8-phase kernel (a 10M-row scan at K 768 is
   // 39k short-K tiles per 256 queries; the one-tile-per-workgroup kernel below pays its prologue and
-  // epilogue on every one of them).  DAB_CAND256=0 keeps the 128x128 kernel (A/B runs).
-  static const bool use256 = [] {
-    const char* v = getenv("DAB_CAND256");
-    return v == nullptr || v[0] != '0';
-  }();
-  if (use256 && M >= 128 && K % 128 == 0)
-    return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
-  // 32..64 queries: the index streams through the decode GEMM's weight ring (64 queries x 10M rows:
-  // 5.88 -> 5.05 ms).  Below 32 it loses (1 query: 4.22 vs 3.70 ms): every 64-row workgroup re-stages
-  // the padded 64-row query block, as many L2 bytes as the index rows it scans.
-  // DAB_CAND_STREAM=0 keeps the 128x128 kernel.
-  static const bool use_stream = [] {
-    const char* v = getenv("DAB_CAND_STREAM");
-    return v == nullptr || v[0] != '0';
-  }();
-  if (use_stream && M <= 16 && K % 256 == 0 && K <= 1024)
+  // epilogue on every one of them)
+  if (M >= 128 && K % 128 == 0)
+    return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s,
+                              b_rows);
+  // 1..16 queries: the persistent scan with the queries in LDS; 32..64: the index streams through the
+  // decode GEMM's weight ring (64 queries x 10M rows: 5.88 -> 5.05 ms).  Row-major copies only here;
+  // shuffled copies go through score_candidates_shuf (VectorIndex picks).
+  if (b_rows == 0 && M <= 16 && K % 256 == 0 && K <= 1024)
     return index_scan_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
-  if (use_stream && M >= 32 && M <= 64 && K % 128 == 0)
+  if (b_rows == 0 && M >= 32 && M <= 64 && K % 128 == 0)
     return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   GemmParams p{};
   p.A = (const bf16*)A;
@@ -309,8 +355,9 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   p.cand_val = cand_val;
   p.cand_idx = cand_idx;
   p.cap = cap;
+  p.rows_b = b_rows;
   const bool big = M >= 2048 && N >= 512 && ((long)((M + 255) / 256) * ((N + 255) / 256)) >= 160;
-  return launch_gemm<EPI_CANDIDATES>(p, big, s);
+  return launch_gemm<EPI_CANDIDATES>(p, big, s, b_rows > 0);
 }
 
 }  // namespace dab

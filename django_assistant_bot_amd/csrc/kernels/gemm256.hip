@@ -25,7 +25,11 @@
 //     lane-linearly, so the swizzle is applied to the per-lane SOURCE address (rule 21);
 //   * buffer descriptors clamp the tile edges: rows >= M (or >= N) read zeros, no per-lane clamp;
 //   * bijective XCD-aware block remap (T1) + grouped tile order so the 32 tiles an XCD runs at once
-//     share A / B panels in that XCD's L2.
+//     share A / B panels in that XCD's L2;
+//   * SHUF: B (the weights) in the ops.shuffle_weights fragment layout [N/16][K/32][64 lanes][8] --
+//     the one copy the decode GEMM (stream_gemm.hip) streams too.  A 16-row x 32-k block is one
+//     contiguous 1 KB piece in MFMA A-fragment lane order, so each wave's LDS-DMA instruction copies
+//     a whole block and the fragment read is lane-linear (ds_read_b128 at lane * 16, no swizzle).
 #include "common.h"
 #include "launchers.h"
 
@@ -36,7 +40,7 @@ namespace dab {
 
 namespace {
 
-enum { G_NONE = 0, G_GELU = 1, G_SWIGLU = 2, G_CAND = 3 };
+enum { G_NONE = 0, G_GELU = 1, G_SWIGLU = 2, G_CAND = 3, G_SWIGLU8 = 4 };
 
 struct G256 {
   const bf16* A;
@@ -47,6 +51,7 @@ struct G256 {
   int M, N, K;
   long lda, ldb, ldc, ldr;
   int gm;  // tile rows per group of the grouped tile order
+  int rows_b;  // SHUF: rows of the B copy (>= N)
   // G_CAND (index threshold search, see gemm.hip EPI_CANDIDATES): filtered scores >= thr[m] are
   // appended to row m's candidate list; no C is written and N need not be a multiple of 256
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -93,7 +98,7 @@ __device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int G
   n0 = (inner / gsz) << 8;
 }
 
-template <int EPI, bool BIAS, bool RES>
+template <int EPI, bool BIAS, bool RES, bool SHUF = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
 
@@ -127,33 +132,43 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // the K offset goes in SOFFSET
   const unsigned vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2), vA1 = vA0 + (unsigned)(64 * p.lda * 2);
   const unsigned vA2 = vA0 + (unsigned)(128 * p.lda * 2), vA3 = vA0 + (unsigned)(192 * p.lda * 2);
-  const unsigned vB0 = (unsigned)((srow * p.ldb + 8 * cc) * 2), vB1 = vB0 + (unsigned)(64 * p.ldb * 2);
-  const unsigned vB2 = vB0 + (unsigned)(128 * p.ldb * 2), vB3 = vB0 + (unsigned)(192 * p.ldb * 2);
+  // SHUF: wave w copies 16-row block w of each 128-row half, both 32-k blocks of the K-tile
+  // (1 KB each, lane-linear); block (rb, kb) of a K-tile sits at byte (K / 32 rb + kb) 1 KB
+  const unsigned kblk = (unsigned)(p.K / 32) * 1024u;
+  const unsigned vB0 = SHUF ? (unsigned)(lane * 16) + (unsigned)w * kblk : (unsigned)((srow * p.ldb + 8 * cc) * 2);
+  const unsigned vB1 = SHUF ? vB0 + 1024u : vB0 + (unsigned)(64 * p.ldb * 2);
+  const unsigned vB2 = SHUF ? vB0 + 8u * kblk : vB0 + (unsigned)(128 * p.ldb * 2);
+  const unsigned vB3 = SHUF ? vB2 + 1024u : vB0 + (unsigned)(192 * p.ldb * 2);
   auto rsrc_a = [&](int mm) {
     const long rows = min(256, p.M - mm);
     return make_rsrc(p.A + (size_t)mm * p.lda, (unsigned)(((rows - 1) * p.lda + p.K) * 2));
   };
   auto rsrc_b = [&](int nn) {
-    const long rows = min(256, p.N - nn);
+    // SHUF (G_CAND over an index copy): rows past the copy read zeros; they are masked as n >= N
+    const long rows = SHUF ? min(256, p.rows_b - nn) : min(256, p.N - nn);
+    if (SHUF) return make_rsrc(p.B + (size_t)nn * p.K, (unsigned)(rows > 0 ? rows * p.K * 2 : 0));
     return make_rsrc(p.B + (size_t)nn * p.ldb, (unsigned)(((rows - 1) * p.ldb + p.K) * 2));
   };
   __amdgpu_buffer_rsrc_t rA = rsrc_a(m0), rB = rsrc_b(n0);
 
   // slot: 0 = A rows 0-127, 1 = A rows 128-255, 2 = B rows 0-127, 3 = B rows 128-255
   auto stage = [&](int buf, int slot, int kt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb) {
-    char* dst = smem + buf * kBuf + slot * kHalf + w * 1024;
-    const unsigned so = (unsigned)kt * 128u;
+    const bool shb = SHUF && slot >= 2;  // (slot is a compile-time constant at every call)
+    char* dst = smem + buf * kBuf + slot * kHalf + w * (shb ? 2048 : 1024);
+    const unsigned so = (unsigned)kt * (shb ? 2048u : 128u);
     const __amdgpu_buffer_rsrc_t r = slot < 2 ? ra : rb;
     const unsigned v0 = slot == 0 ? vA0 : slot == 1 ? vA2 : slot == 2 ? vB0 : vB2;
     const unsigned v1 = slot == 0 ? vA1 : slot == 1 ? vA3 : slot == 2 ? vB1 : vB3;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)dst, 16, v0, so, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + 8192), 16, v1, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dst + (shb ? 1024 : 8192)), 16, v1, so, 0, 0);
   };
 
   // ---- fragment reads (per-lane byte offsets inside a half-tile, k-steps 0 / 1)
   const int swr = li >> 1;
   const int rdA0 = (64 * wr + li) * 128 + 16 * (g ^ swr), rdA1 = (64 * wr + li) * 128 + 16 * ((4 + g) ^ swr);
-  const int rdB0 = (32 * wc + li) * 128 + 16 * (g ^ swr), rdB1 = (32 * wc + li) * 128 + 16 * ((4 + g) ^ swr);
+  // SHUF: block (2 wc + j) of the half at 2 KB strides (the j * 2048 below), k-step ks at + 1 KB
+  const int rdB0 = SHUF ? wc * 4096 + lane * 16 : (32 * wc + li) * 128 + 16 * (g ^ swr);
+  const int rdB1 = SHUF ? rdB0 + 1024 : (32 * wc + li) * 128 + 16 * ((4 + g) ^ swr);
 
   bf16x8 af[4][2];
   bf16x8 bfr[2][2][2];  // [jh][jn][ks]
@@ -370,8 +385,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             }
           }
         }
-    } else if constexpr (EPI == G_SWIGLU) {
-      // weight rows interleaved in 16-row groups [gate 16 | up 16]: jn = 0 gate, jn = 1 up
+    } else if constexpr (EPI == G_SWIGLU || EPI == G_SWIGLU8) {
+      // G_SWIGLU: weight rows interleaved in 16-row groups [gate 16 | up 16]: jn = 0 gate, jn = 1 up.
+      // G_SWIGLU8: 8-row groups [gate 8 | up 8] inside every 16-row MFMA block (the decode layout:
+      // any 16-row multiple tiles it): lane g holds rows 4g..4g+3 of both blocks, so one
+      // v_permlane32_swap of the (jn 0, jn 1) pair gives lanes 0-31 block 0's gate / up rows and
+      // lanes 32-63 block 1's -- the same output column 16 wc + 4 g as the 16-row form.
       float bg[2][4], bu[2][4];
       if constexpr (BIAS) {
 #pragma unroll
@@ -396,6 +415,11 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               float gt = acc[ih][jh][i][0][r], up = acc[ih][jh][i][1][r];
+              if constexpr (EPI == G_SWIGLU8) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(gt), __float_as_uint(up), false, false);
+                gt = __uint_as_float(sw[0]);
+                up = __uint_as_float(sw[1]);
+              }
               if constexpr (BIAS) {
                 gt += bg[jh][r];
                 up += bu[jh][r];
@@ -502,12 +526,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 
 // Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
 // index rows B [N, K], any N; K % 128 == 0.
+// b_rows > 0: B is a shuffle_weights copy of b_rows >= N rows (b_rows % 16 == 0, ldb == K).
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                        const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                       hipStream_t s) {
+                       hipStream_t s, int b_rows) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 128 || K <= 0 || lda % 8 || ldb % 8 || cap <= 0) return hipErrorInvalidValue;
   if ((255L * lda + K) * 2 >= (1L << 31) || (255L * ldb + K) * 2 >= (1L << 31)) return hipErrorInvalidValue;
+  if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
   G256 p{};
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
@@ -524,11 +550,13 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   p.cand_val = cand_val;
   p.cand_idx = cand_idx;
   p.cap = cap;
+  p.rows_b = b_rows;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
   const int nwg = tiles > cus ? cus : (int)tiles;
-  hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false>), dim3(nwg), dim3(512), 0, s, p);
+  if (b_rows > 0) hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false, true>), dim3(nwg), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false>), dim3(nwg), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 
@@ -540,10 +568,14 @@ int gemm256_ok(int M, int N, int K, long lda, long ldb) {
   return 1;
 }
 
+// b_shuf: B is in the shuffle_weights layout (ldb == K).  Epilogues: 0 none, 1 GELU, 2 SwiGLU over
+// 16-row [gate | up] groups, 4 SwiGLU over 8-row groups (no bias); bias / residual optional.
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s) {
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf) {
   if (!gemm256_ok(M, N, K, lda, ldb)) return hipErrorInvalidValue;
-  if (epilogue == G_SWIGLU && residual) return hipErrorInvalidValue;
+  if ((epilogue == G_SWIGLU || epilogue == G_SWIGLU8) && residual) return hipErrorInvalidValue;
+  if (epilogue == G_SWIGLU8 && bias) return hipErrorInvalidValue;
+  if (b_shuf && ldb != K) return hipErrorInvalidValue;
   G256 p;
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
@@ -557,18 +589,19 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   p.ldb = ldb;
   p.ldc = ldc;
   p.ldr = ldr;
+  p.rows_b = N;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = ((M + 255) / 256) * (N / 256);
-  // persistent: one workgroup (128 KB of LDS) per CU; DAB_GEMM256_PERSIST=0 launches one per tile
-  const char* ge = getenv("DAB_GEMM256_GM");
-  p.gm = ge ? atoi(ge) : 4;
-  if (p.gm < 1) p.gm = 1;
-  const char* pe = getenv("DAB_GEMM256_PERSIST");
-  const bool persist = !(pe && pe[0] == '0');
-  const int nwg = (persist && tiles > cus) ? cus : tiles;
+  p.gm = 4;  // grouped tile order: 4 tile rows per group
+  // persistent: one workgroup (128 KB of LDS) per CU walks a strided tile list
+  const int nwg = tiles > cus ? cus : tiles;
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define G256_LAUNCH(E, B, R) hipLaunchKernelGGL((gemm256_kernel<E, B, R>), dim3(nwg), dim3(512), 0, s, p)
+#define G256_LAUNCH(E, B, R)                                                                            \
+  do {                                                                                                   \
+    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);  \
+    else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);       \
+  } while (0)
   switch (epilogue) {
     case G_NONE:
       if (hb && hr) G256_LAUNCH(G_NONE, true, true);
@@ -582,9 +615,11 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
       else G256_LAUNCH(G_GELU, false, false);
       break;
     case G_SWIGLU:
-      if (hr) return hipErrorInvalidValue;
       if (hb) G256_LAUNCH(G_SWIGLU, true, false);
       else G256_LAUNCH(G_SWIGLU, false, false);
+      break;
+    case G_SWIGLU8:
+      G256_LAUNCH(G_SWIGLU8, false, false);
       break;
     default: return hipErrorInvalidValue;
   }

@@ -40,38 +40,50 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
                     int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s,
                     const int* rope_pos = nullptr, const void* rope_cs = nullptr);
+// decode prologue inputs of the fused RoPE + KV-write form (q == nullptr then): the step's QKV
+// projection as bf16 rows (`qkv`) or S fp32 split-K slabs, row width ld = (Hq + 2 Hkv) D
+struct DecodeRopeArgs {
+  const void* qkv;
+  const float* slabs;
+  int S;
+  long slab_stride;
+  int ld;
+  const int* positions;
+  const void* cos_sin;
+  const int64_t* slots;
+};
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
                            int part_size, int max_parts, float scale, hipStream_t s,
-                           const int* order = nullptr);
+                           const int* order = nullptr, const DecodeRopeArgs* rope = nullptr);
 
 // gemm.hip
+// b_rows > 0: B is an ops.shuffle_weights copy of b_rows (>= N) rows; epilogue 4 = SwiGLU over 8-row
+// [gate | up] groups
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
-            const uint32_t* allow, int allow_words, hipStream_t s);
+            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows = 0);
 
 // gemm256.hip (large-M prefill / encoder GEMM, 256x256 8-phase schedule; epilogue 0 none, 1 GELU,
 // 2 SwiGLU on [gate 16 | up 16]-interleaved weight rows; bias / residual optional)
 int gemm256_ok(int M, int N, int K, long lda, long ldb);
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                        const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                       hipStream_t s);
+                       hipStream_t s, int b_rows = 0);
+// b_shuf: B in the ops.shuffle_weights layout (the decode GEMM's copy); epilogue 4 = SwiGLU over
+// 8-row [gate | up] groups
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s);
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
 
-// skinny_gemm.hip (decode-sized M <= 64; S K-slices: S == 1 -> bf16 out with epilogue, S > 1 -> fp32
-// slabs [S][M][N] reduced by the consumer or by skinny_reduce)
-int skinny_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
-                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights = 0);
-int skinny_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
-                  hipStream_t s);
-
-// stream_gemm.hip (warp-specialised decode GEMM, M <= 128; same outputs as skinny_gemm; cfg selects
+// stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
 int stream_gemm_bn(int cfg);
+// fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
+int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
+                hipStream_t s);
 // index_scan.hip: persistent scan for 1..16 queries (queries staged in LDS once), K % 256 == 0, K <= 1024
 int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
@@ -106,7 +118,7 @@ int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float
 // gemm.hip: scores >= thr[m] appended per query (exact threshold top-k of the vector index)
 int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
-                          hipStream_t s);
+                          hipStream_t s, int b_rows = 0);
 
 // allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers (TP decode on one node)
 size_t allreduce_signal_bytes();

@@ -1,7 +1,8 @@
 // Warp-specialised weight-streaming MFMA GEMM for decode batches:  C[M, N] = X[M, K] . W[N, K]^T,
-// M <= 128.  Successor of skinny_gemm.hip at M 65..128 (and an alternative at M <= 64).
+// M <= 256 (decode batches; also the LM head of prefill last tokens and the index scan of 17-128 queries).
 //
-// Why a second decode kernel: at M = 128 the single-queue design of skinny_gemm waits, every stage,
+// Why warp specialisation: at M = 128 a single-queue design (weights and X on the same waves) waits,
+// every stage,
 // for an X load that sits behind the newest weight loads in the wave's in-order vmcnt queue, so at
 // most ~1.5 stages of weights are ever in flight and each 16-33 MB projection runs at 2-3 TB/s
 // (profiles/decode_gemm_m128_study.md).  Here the two operands travel on different waves:
@@ -17,10 +18,10 @@
 //   * waves = KG k-groups x (4 / KG) row groups of RT 16-row tiles; v_mfma_f32_16x16x32_bf16 with W
 //     as A and X as B (one LDS fragment feeds RT MFMAs); partial tiles of the k-groups meet in LDS.
 //
-// Outputs as skinny_gemm: S == 1 -> bf16 (optional residual add, or SwiGLU over 16-row interleaved
-// [gate | up] weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue
-// (rmsnorm / rope+KV write) or by skinny_reduce.  Block -> (tile, slice) keeps a tile's slices on
-// one XCD (bijective remap, slice-minor).
+// Outputs: S == 1 -> bf16 (optional residual add, or SwiGLU over 16- / 8-row interleaved [gate | up]
+// weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue (rmsnorm /
+// the decode attention's RoPE + KV-write prologue) or by slab_reduce below.  Block -> (tile, slice)
+// keeps a tile's slices on one XCD (bijective remap, slice-minor).
 #include <cstdlib>
 #include <type_traits>
 
@@ -42,7 +43,6 @@ struct StreamParams {
   long ldr;
   int M, N, K, S, kc;
   int epi;       // 0 none, 2 swiglu (16-row gate | up groups), 4 swiglu (8-row groups), 8 candidates
-  int slab_wt;   // split-K slabs stored write-through (sc1)
   // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
   // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -262,23 +262,17 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   constexpr int NT = 64 * (NWC + NL);
   if (p.S > 1) {
     float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
-    if (p.slab_wt) {
-      // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
-      // instead of sitting dirty until the kernel-end write-back, which the next kernel's start
-      // would wait for (MI355X_MICROARCH.md price list: +2.8-3.8 us behind 12.6-16.8 MB of fp32
-      // partials); the consumer reads them once from the Infinity Cache either way
-      const auto srd = __builtin_amdgcn_make_buffer_rsrc(slab + n0, 0, (p.M - 1) * p.N * 4 + BN * 4, 0x00020000);
-      for (int e = tid; e < MP * (BN / 4); e += NT) {
-        const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
-        if (m < p.M)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile4(m, c4)), srd, (m * p.N + c4) * 4, 0,
-                                                 16);
-      }
-      return;
-    }
+    // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
+    // instead of sitting dirty until the kernel-end write-back, which the next kernel's start
+    // would wait for (MI355X_MICROARCH.md price list: +2.8-3.8 us behind 12.6-16.8 MB of fp32
+    // partials; o 14.6 -> 13.2 us, qkv 18.0 -> 16.6 us in the decode layer, profiles/decode_round2.md);
+    // the consumer reads them once from the Infinity Cache either way
+    const auto srd = __builtin_amdgcn_make_buffer_rsrc(slab + n0, 0, (p.M - 1) * p.N * 4 + BN * 4, 0x00020000);
     for (int e = tid; e < MP * (BN / 4); e += NT) {
       const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
-      if (m < p.M) *reinterpret_cast<f32x4*>(slab + (size_t)m * p.N + n0 + c4) = tile4(m, c4);
+      if (m < p.M)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile4(m, c4)), srd, (m * p.N + c4) * 4, 0,
+                                               16);
     }
     return;
   }
@@ -445,12 +439,44 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   p.S = S;
   p.kc = K / S;
   p.epi = epilogue;
-  static const int slab_wt = [] {
-    const char* v = getenv("DAB_SLAB_WT");
-    return v == nullptr ? 1 : atoi(v);
-  }();
-  p.slab_wt = slab_wt;
   launch_any(cfg, p, s, nt_weights != 0);
+  return hipGetLastError();
+}
+
+// Sum S fp32 slabs -> bf16 (optionally + residual), rounded like a bf16 GEMM output before the add:
+// the TP path hands bf16 partial sums to the all-reduce.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(bf16* out, long ldo, const float* slabs, int S, int M, int N,
+                                                          const bf16* residual, long ldr) {
+  const size_t e = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  const size_t total = (size_t)M * N;
+  if (e >= total) return;
+  const int m = (int)(e / N), n = (int)(e % N);
+  float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(slabs + (size_t)s * total + e);
+    const f32x4 a = src[0], b = src[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[j] += a[j];
+      o[4 + j] += b[j];
+    }
+  }
+  if (residual) {
+    float r[8];
+    unpack8(*reinterpret_cast<const u32x4*>(residual + (size_t)m * ldr + n), r);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = bf2f(f2bf(o[j])) + r[j];
+  }
+  *reinterpret_cast<u32x4*>(out + (size_t)m * ldo + n) = pack8(o);
+}
+
+int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
+                hipStream_t s) {
+  if (M <= 0 || N <= 0) return 0;
+  if (N % 8 || ldo % 8 || (residual && ldr % 8)) return hipErrorInvalidValue;
+  const size_t total8 = (size_t)M * N / 8;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, (bf16*)out, ldo,
+                     slabs, S, M, N, (const bf16*)residual, ldr);
   return hipGetLastError();
 }
 

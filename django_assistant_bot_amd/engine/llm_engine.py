@@ -86,8 +86,6 @@ class _Req:
         return self.prompt + self.out if self.preempted else self.prompt
 
 
-# DAB_PREFILL_DEFER=0: read every prefill chunk's tokens back before the next launch (A/B runs)
-_DEFER_PREFILL = os.environ.get("DAB_PREFILL_DEFER", "1") != "0"
 
 
 def _bucket_sizes(max_batch):
@@ -102,7 +100,7 @@ class LLMEngine:
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
                  tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
                  part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0,
-                 pipeline_decode: bool | None = None, prefill_streams: int | None = None):
+                 pipeline_decode: bool = True):
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
@@ -131,15 +129,6 @@ class LLMEngine:
         self.max_blocks_per_seq = math.ceil(self.max_model_len / block_size)
         self.max_prefill_tokens = max_prefill_tokens
         self.mixed_prefill_tokens = mixed_prefill_tokens
-        # Opt-in: large prefill steps as two sub-batches on two HIP streams (forward_overlapped), so
-        # the memory-bound kernels of one can overlap the GEMMs of the other.  Measured slower on the
-        # headline bench (prefill 1528 ms per 128-question batch with 2 streams vs 1452 with 1; 1492
-        # with 2 streams of 32K tokens each): the concurrent kernels slow hipBLASLt's GEMMs by more
-        # than they hide.  TP keeps one stream: its all-reduces must be issued in one order on every rank.
-        if prefill_streams is None:
-            prefill_streams = int(os.environ.get("DAB_PREFILL_STREAMS", "1"))
-        self.prefill_streams = prefill_streams if tp_size == 1 else 1
-        self.prefill_split_min = int(os.environ.get("DAB_PREFILL_SPLIT_MIN", "4096"))
         self.part_size = part_size
         # Key partition of the split-K decode attention per step size: partitions of 2048 keys (one
         # per sequence at RAG context lengths) stream 12 % faster than 512 at batch 128 (fewer
@@ -183,7 +172,6 @@ class LLMEngine:
         self._d_cnt = torch.zeros(mb, dtype=torch.int64, device=dev)
         self._d_tokens = torch.zeros(mb, dtype=torch.int32, device=dev)
         self._d_order = torch.arange(mb, dtype=torch.int32, device=dev)  # decode attention dispatch order
-        self.lpt_order = os.environ.get("DAB_DECODE_ORDER", "1") == "1"
         pin = self.is_gpu
         mk = lambda *a, **k: torch.zeros(*a, **k, pin_memory=pin)  # noqa: E731
         self._h_ids = mk(mb, dtype=torch.int32)
@@ -201,8 +189,6 @@ class LLMEngine:
         # its input ids copied on the device from step t's sampled tokens, so the host's per-step
         # bookkeeping overlaps the GPU instead of idling it.  Two alternating host buffer sets: the
         # H2D copies of step t may still be pending while step t+1's are filled.
-        if pipeline_decode is None:
-            pipeline_decode = os.environ.get("DAB_PIPELINE_DECODE", "1") == "1"
         self.pipeline_decode = bool(pipeline_decode) and tp_size == 1
         self._h_alt = {k: mk(*(getattr(self, k).shape,), dtype=getattr(self, k).dtype)
                        for k in ("_h_ids", "_h_pos", "_h_slots", "_h_ctx", "_h_bt", "_h_temp", "_h_topk", "_h_topp",
@@ -392,24 +378,6 @@ class LLMEngine:
     def _build_block_tables(self, seqs, out_host):
         self.blocks.block_table_into(seqs, self.max_blocks_per_seq, out_host.data_ptr())
 
-    def _prefill_groups(self, sizes):
-        """Contiguous chunk ranges [(a, b), ...] of a prefill step, one per HIP stream of
-        ``LlamaModel.forward_overlapped``: split at the chunk boundary nearest to equal token counts
-        when the step is large enough that each half still runs its GEMMs at full MFMA rate."""
-        T, B = sum(sizes), len(sizes)
-        if self.prefill_streams < 2 or B < 2 or T < 2 * self.prefill_split_min:
-            return [(0, B)]
-        acc, best, cut = 0, None, 1
-        for i in range(1, B):
-            acc += sizes[i - 1]
-            d = abs(2 * acc - T)
-            if best is None or d < best:
-                best, cut = d, i
-        lo = sum(sizes[:cut])
-        if min(lo, T - lo) < self.prefill_split_min:
-            return [(0, B)]
-        return [(0, cut), (cut, B)]
-
     def _run_prefill(self, chunks):
         t0 = time.perf_counter()
         dev = self.device
@@ -432,18 +400,10 @@ class LLMEngine:
         bt = torch.zeros((B, self.max_blocks_per_seq), dtype=torch.int32)
         self._build_block_tables([r.seq for r, _, _ in chunks], bt)
         to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
-        parts = []
-        for a, b in self._prefill_groups([n for _, _, n in chunks]):
-            t0_, t1_ = int(cu[a]), int(cu[b])
-            meta = AttnMeta(decode=False, positions=to(pos[t0_:t1_]), slots=to(slots[t0_:t1_]),
-                            block_tables=to(bt[a:b]), ctx_lens=to(ctx[a:b]), cu_q=to(cu[a:b + 1] - cu[a]),
-                            max_q=max(n for _, _, n in chunks[a:b]))
-            parts.append((to(ids[t0_:t1_]), meta))
+        meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
+                        cu_q=to(cu), max_q=max(n for _, _, n in chunks))
         with self.timer.phase("prefill"):
-            if len(parts) == 1:
-                hidden = self.model.forward(parts[0][0], parts[0][1], self.kv)
-            else:
-                hidden = self.model.forward_overlapped(parts, self.kv)
+            hidden = self.model.forward(to(ids), meta, self.kv)
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
         self.stats["prefill_tokens"] += T
         self.stats["prefill_steps"] += 1
@@ -461,7 +421,7 @@ class LLMEngine:
             # the shared prefix (e.g. the system prompt) instead of recomputing it
             self.blocks.commit_prefix(r.seq, s + n)
         pend = (chunks, reqs, toks, t0)
-        if self.is_gpu and _DEFER_PREFILL:
+        if self.is_gpu:
             self._pending_prefill = pend  # read back after the next launch (step)
         else:
             self._finish_prefill(pend)
@@ -823,9 +783,6 @@ class LLMEngine:
     def _fill_order(self, Bp: int) -> None:
         """Host: the decode attention's dispatch order for this step, longest context first (LPT
         balance of the two workgroup rounds per CU; benchmarks/decode_attn_bench.py)."""
-        if not self.lpt_order:
-            self._h_order[:Bp] = torch.arange(Bp, dtype=torch.int32)
-            return
         ctx = self._h_ctx[:Bp].numpy()
         self._h_order[:Bp] = torch.from_numpy(np.argsort(-ctx, kind="stable").astype(np.int32))
 

@@ -11,10 +11,15 @@ Recall is 1.0 by construction.  Distance semantics match pgvector: ``1 - cos``.
 
 The index is a cache of the ORM (source of truth); it supports upsert, delete (tombstone + lazy
 compaction), growth, and safetensors snapshots for warm starts.
+
+On the GPU (bf16, dim % 128 == 0) the rows are held ONCE, in the ``ops.shuffle_weights`` fragment
+layout: every 16-row x 32-k block is one coalesced 1 KB load for the 1..128-query scans
+(index_scan.hip / the streaming GEMM's candidate epilogue) and one LDS-DMA piece for the 8-phase
+GEMM at >= 128 queries and the generic-filter score GEMM.  (Round 2 kept a row-major copy beside
+it: 2x the index HBM.)  Only the 1/16 row sample of the threshold search is gathered row-major, and
+cached until the next update.
 """
 from __future__ import annotations
-
-import os
 
 import numpy as np
 import torch
@@ -34,21 +39,27 @@ class VectorIndex:
         self.vecs = self.row_ids = self.row_docs = self.row_group = None
         self._row_of: dict[int, int] = {}
         self._sorted = None  # lazily built (sorted ids, rows) for vectorised id -> row lookups
-        self._shuf = None  # the rows in the shuffle_weights layout (see shuffled_scan), or None
+        # fragment layout (see the module docstring) for bf16 GPU indexes of a 128-multiple width
+        self.frag = self.device.type == "cuda" and dtype == torch.bfloat16 and dim % 128 == 0
+        self._version = 0  # bumped by every update: invalidates the cached threshold sample
+        self._sample = None
         self._dead = 0
         self._grow(max(64, capacity))
 
     # ------------------------------------------------------------------ storage
     def _grow(self, cap: int):
-        self._shuf = None
-        cap = (cap + 127) // 128 * 128  # whole 128-row tiles for the shuffled-copy scans
+        cap = (cap + 255) // 256 * 256  # whole 256-row tiles for the fragment-layout scans / GEMMs
         dev = self.device
         vecs = torch.zeros((cap, self.dim), dtype=self.dtype, device=dev)
         ids = torch.full((cap,), -1, dtype=torch.int64, device=dev)
         docs = torch.full((cap,), -1, dtype=torch.int64, device=dev)
         grp = torch.full((cap,), -1, dtype=torch.int32, device=dev)
         if self.n:
-            vecs[: self.n] = self.vecs[: self.n]
+            if self.frag:  # the first ceil(n / 16) 16-row blocks are a contiguous prefix
+                e = -(-self.n // 16) * 16 * self.dim
+                vecs.view(-1)[:e] = self.vecs.view(-1)[:e]
+            else:
+                vecs[: self.n] = self.vecs[: self.n]
             ids[: self.n] = self.row_ids[: self.n]
             docs[: self.n] = self.row_docs[: self.n]
             grp[: self.n] = self.row_group[: self.n]
@@ -59,10 +70,21 @@ class VectorIndex:
     threshold_search = True
     threshold_min_rows = 1 << 19
     sample_stride = 16
-    # searches of up to 128 queries scan a second copy of the rows in the decode-stream layout (every
-    # 16-row x 32-k fragment one coalesced 1 KB load: index_scan.hip SHUF).  It is built at the
-    # first such search, kept current by add(), and costs one more copy of the vectors in HBM.
-    shuffled_scan = os.environ.get("DAB_INDEX_SHUF", "1") != "0"
+
+    def _put(self, rows: torch.Tensor, v: torch.Tensor) -> None:
+        if self.frag:
+            ops.shuffle_rows_into(self.vecs, rows, v)
+        else:
+            self.vecs[rows] = v
+
+    def rows_data(self, rows) -> torch.Tensor:
+        """Row-major copy of the given rows (any layout)."""
+        rows = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
+        if not self.frag:
+            return self.vecs[rows]
+        R, K = self.vecs.shape
+        v5 = self.vecs.view(R // 16, K // 32, 4, 16, 8)
+        return v5[rows // 16, :, :, rows % 16, :].reshape(rows.numel(), K)
 
     def __len__(self) -> int:
         return len(self._row_of)
@@ -115,9 +137,8 @@ class VectorIndex:
             x = torch.from_numpy(np.ascontiguousarray(a))
             return (x.pin_memory() if pin else x).to(self.device, non_blocking=True)
         r = dev(rows)
-        self.vecs[r] = v
-        if self._shuf is not None:
-            ops.shuffle_rows_into(self._shuf, r, v)
+        self._put(r, v)
+        self._version += 1
         self.row_ids[r] = dev(ids)
         self.row_docs[r] = dev(docs)
         self.row_group[r] = dev(grp)
@@ -127,6 +148,7 @@ class VectorIndex:
         if rows:
             self._sorted = None
             r = torch.as_tensor(rows, dtype=torch.int64, device=self.device)
+            self._version += 1
             self.row_group[r] = -1
             self.row_ids[r] = -1
             self._dead += len(rows)
@@ -137,8 +159,8 @@ class VectorIndex:
     def compact(self) -> None:
         live = (self.row_group[: self.n] >= 0).nonzero().flatten()
         m = live.numel()
-        self.vecs[:m] = self.vecs[live]
-        self._shuf = None
+        self._put(torch.arange(m, device=self.device), self.rows_data(live))
+        self._version += 1
         self.row_ids[:m] = self.row_ids[live]
         self.row_docs[:m] = self.row_docs[live]
         self.row_group[:m] = self.row_group[live]
@@ -209,6 +231,9 @@ class VectorIndex:
             allow = dm if allow is None else allow & dm
         n = max(self.n, 4)
         n = (n + 3) // 4 * 4
+        if self.frag:
+            return ops.gemm_bt(q, self.vecs, epilogue=ops.EPI_SCORES, out_f32=True, row_group=self.row_group[:n],
+                               q_group=qg, allow=allow, shuffled=True, n=n)
         return ops.gemm_bt(q, self.vecs[:n], epilogue=ops.EPI_SCORES, out_f32=True, row_group=self.row_group[:n],
                            q_group=qg, allow=allow)
 
@@ -254,18 +279,15 @@ class VectorIndex:
         if ns < k:  # the sample's k-th best is a valid bound only if the sample holds k rows
             return None
         kk = k
-        samp = self.vecs[: ns * self.sample_stride: self.sample_stride]
+        samp = self._sample_rows(ns)
         samp_group = self.row_group[: ns * self.sample_stride: self.sample_stride].contiguous()
         s_scores = ops.gemm_bt(q, samp, epilogue=ops.EPI_SCORES, out_f32=True, row_group=samp_group, q_group=qg)
         tv, _ = ops.topk_rows(s_scores, kk)
         del s_scores
         thr = tv[:, kk - 1].contiguous()
         cap = max(4096, 64 * k * self.sample_stride // 16)
-        if self._use_shuffled(q.shape[0]):
-            if self._shuf is None:
-                with torch.inference_mode(False):  # a normal tensor: add() updates it in place later
-                    self._shuf = ops.shuffle_weights(self.vecs)
-            cand_val, cand_idx, cnt = ops.score_candidates_shuffled(q, self._shuf, n4, thr, cap, self.row_group[:n4], qg)
+        if self.frag:
+            cand_val, cand_idx, cnt = ops.score_candidates_shuffled(q, self.vecs, n4, thr, cap, self.row_group[:n4], qg)
         else:
             cand_val, cand_idx, cnt = ops.score_candidates(q, self.vecs[:n4], thr, cap, self.row_group[:n4], qg)
         if int(cnt.max()) > cap:
@@ -276,18 +298,22 @@ class VectorIndex:
         rows = torch.gather(cand_idx, 1, pos.long())
         return vals, rows.masked_fill(torch.isinf(vals), 0)
 
-    def _use_shuffled(self, m: int) -> bool:
-        # 128 queries and up fill the persistent 256x256 GEMM's tiles: row-major is faster there
-        # (10M rows: 5.00 vs 5.44 ms at 128)
-        return (self.shuffled_scan and self.device.type == "cuda" and self.dtype == torch.bfloat16 and m < 128
-                and ops.kernels.shuffled_scan_ok(m, self.dim))
+    def _sample_rows(self, ns: int) -> torch.Tensor:
+        """The strided 1/16 row sample (row-major), cached until the next update."""
+        key = (ns, self._version)
+        if self._sample is None or self._sample[0] != key:
+            rows = torch.arange(0, ns * self.sample_stride, self.sample_stride, device=self.device)
+            with torch.inference_mode(False):
+                self._sample = (key, self.rows_data(rows).contiguous())
+        return self._sample[1]
 
     # ------------------------------------------------------------------ persistence
     def save(self, path: str) -> None:
         from safetensors.torch import save_file
 
         n = self.n
-        save_file({"vecs": self.vecs[:n].contiguous().cpu(), "ids": self.row_ids[:n].cpu(),
+        save_file({"vecs": self.rows_data(torch.arange(n, device=self.device)).contiguous().cpu(),
+                   "ids": self.row_ids[:n].cpu(),
                    "docs": self.row_docs[:n].cpu(), "group": self.row_group[:n].cpu()}, path,
                   metadata={"dim": str(self.dim)})
 
@@ -298,8 +324,7 @@ class VectorIndex:
         st = load_file(path)
         idx = cls(st["vecs"].shape[1], device, capacity=max(64, st["vecs"].shape[0]), dtype=st["vecs"].dtype)
         n = st["vecs"].shape[0]
-        idx.vecs[:n] = st["vecs"].to(idx.device)
-        idx._shuf = None
+        idx._put(torch.arange(n, device=idx.device), st["vecs"].to(idx.device))
         idx.row_ids[:n] = st["ids"].to(idx.device)
         idx.row_docs[:n] = st["docs"].to(idx.device)
         idx.row_group[:n] = st["group"].to(idx.device)

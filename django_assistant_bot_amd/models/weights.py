@@ -60,9 +60,23 @@ def random_encoder_weights(cfg: EncoderConfig, device="cpu", dtype=torch.bfloat1
     return w
 
 
-def _interleave16(gate: torch.Tensor, up: torch.Tensor) -> torch.Tensor:
+MLP_GROUP = 8  # gate|up row groups of the fused SwiGLU GEMMs (EPI_SWIGLU8: any 16-row tile holds pairs)
+
+
+def _mlp_group(interleave_mlp) -> int:
+    """``interleave_mlp``: False / 0 = stacked [gate; up], True = the engine's 8-row groups, or an
+    explicit group size (8 / 16)."""
+    if interleave_mlp is True:
+        return MLP_GROUP
+    return int(interleave_mlp or 0)
+
+
+def _gate_up(gate: torch.Tensor, up: torch.Tensor, interleave_mlp) -> torch.Tensor:
+    grp = _mlp_group(interleave_mlp)
+    if not grp:
+        return torch.cat([gate, up], 0)
     Fd, H = gate.shape
-    return torch.stack([gate.view(Fd // 16, 16, H), up.view(Fd // 16, 16, H)], dim=1).reshape(2 * Fd, H)
+    return torch.stack([gate.reshape(Fd // grp, grp, H), up.reshape(Fd // grp, grp, H)], dim=1).reshape(2 * Fd, H)
 
 
 def random_decoder_weights(cfg: DecoderConfig, device="cpu", dtype=torch.bfloat16, seed=0, tp_rank=0, tp_size=1,
@@ -90,7 +104,7 @@ def random_decoder_weights(cfg: DecoderConfig, device="cpu", dtype=torch.bfloat1
         w[f"l{i}.mlp_norm"] = torch.ones(H, device=device, dtype=dtype)
         gate = _randn((f, H), g, device, dtype)
         up = _randn((f, H), g, device, dtype)
-        w[f"l{i}.gate_up_w"] = _interleave16(gate, up) if interleave_mlp else torch.cat([gate, up], 0)
+        w[f"l{i}.gate_up_w"] = _gate_up(gate, up, interleave_mlp)
         del gate, up
         w[f"l{i}.down_w"] = _randn((H, f), g, device, dtype)
     return w
@@ -114,7 +128,7 @@ def shard_decoder_weights(full: dict, cfg: DecoderConfig, tp_rank: int, tp_size:
         gu = full[f"l{i}.gate_up_w"]
         gate = gu[:F][tp_rank * f:(tp_rank + 1) * f]
         up = gu[F:][tp_rank * f:(tp_rank + 1) * f]
-        out[f"l{i}.gate_up_w"] = (_interleave16(gate, up) if interleave_mlp else torch.cat([gate, up], 0)).contiguous()
+        out[f"l{i}.gate_up_w"] = _gate_up(gate, up, interleave_mlp).contiguous()
         out[f"l{i}.down_w"] = full[f"l{i}.down_w"][:, tp_rank * f:(tp_rank + 1) * f].contiguous()
         out[f"l{i}.attn_norm"] = full[f"l{i}.attn_norm"]
         out[f"l{i}.mlp_norm"] = full[f"l{i}.mlp_norm"]
@@ -125,16 +139,45 @@ def shard_decoder_weights(full: dict, cfg: DecoderConfig, tp_rank: int, tp_size:
 # HF checkpoints (safetensors only: nothing executable is ever loaded)
 
 
-def _read_safetensors(path: str) -> dict:
-    from safetensors.torch import load_file
+class SafetensorsDir:
+    """Lazy reader over the ``*.safetensors`` files of a checkpoint (``safe_open``: memory-mapped,
+    nothing executable).  ``get`` materialises a whole tensor, ``rows`` / ``cols`` only a slice, so
+    a tensor-parallel rank reads about 1/tp of every sharded projection.  ``bytes_read`` counts the
+    bytes materialised (tests / logs)."""
 
-    files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
-    if not files:
-        raise FileNotFoundError(f"no .safetensors files under {path}")
-    state = {}
-    for f in files:
-        state.update(load_file(f))
-    return state
+    def __init__(self, path: str):
+        from safetensors import safe_open
+
+        files = sorted(glob.glob(os.path.join(path, "*.safetensors"))) if os.path.isdir(path) else [path]
+        if not files:
+            raise FileNotFoundError(f"no .safetensors files under {path}")
+        self._handles = [safe_open(f, framework="pt") for f in files]
+        self._where = {k: h for h in self._handles for k in h.keys()}
+        self.bytes_read = 0
+
+    def keys(self):
+        return self._where.keys()
+
+    def __contains__(self, name):
+        return name in self._where
+
+    def _count(self, t):
+        self.bytes_read += t.numel() * t.element_size()
+        return t
+
+    def get(self, name):
+        return self._count(self._where[name].get_tensor(name))
+
+    def rows(self, name, a: int, b: int):
+        return self._count(self._where[name].get_slice(name)[a:b])
+
+    def cols(self, name, a: int, b: int):
+        return self._count(self._where[name].get_slice(name)[:, a:b])
+
+
+def _read_safetensors(path: str) -> dict:
+    st = SafetensorsDir(path)
+    return {k: st.get(k) for k in st.keys()}
 
 
 def load_encoder_checkpoint(path: str, cfg: EncoderConfig, dtype=torch.bfloat16) -> dict:
@@ -166,18 +209,31 @@ def load_encoder_checkpoint(path: str, cfg: EncoderConfig, dtype=torch.bfloat16)
 
 
 def load_decoder_checkpoint(path: str, cfg: DecoderConfig, dtype=torch.bfloat16, tp_rank=0, tp_size=1,
-                            interleave_mlp=False) -> dict:
-    st = _read_safetensors(path)
-    get = lambda k: st[k].to(dtype)  # noqa: E731
-    full = {"embed": get("model.embed_tokens.weight"), "final_norm": get("model.norm.weight")}
+                            interleave_mlp=False, reader: SafetensorsDir | None = None) -> dict:
+    """The rank's tensor-parallel shard of an HF Llama checkpoint, read slice by slice: q / k / v /
+    gate / up by output rows (column parallel), o / down by input columns (row parallel), so a rank
+    of a 70B TP-8 group materialises ~1/8 of every projection (~17.5 GB) instead of the whole
+    140 GB state.  Replicated tensors (embedding, LM head, norms) are read whole.  Same result as
+    ``shard_decoder_weights`` of the full state (tests/test_models_cpu.py)."""
+    st = reader or SafetensorsDir(path)
+    H, F, D = cfg.hidden, cfg.intermediate, cfg.head_dim
+    hq, hkv, f = cfg.heads // tp_size, cfg.kv_heads // tp_size, F // tp_size
+    cast = lambda t: t.to(dtype).contiguous()  # noqa: E731
+    w = {"embed": cast(st.get("model.embed_tokens.weight")), "final_norm": cast(st.get("model.norm.weight"))}
     if not cfg.tie_embeddings:
-        full["lm_head"] = get("lm_head.weight")
+        w["lm_head"] = cast(st.get("lm_head.weight"))
+    r = tp_rank
     for i in range(cfg.layers):
         p = f"model.layers.{i}."
-        full[f"l{i}.attn_norm"] = get(p + "input_layernorm.weight")
-        full[f"l{i}.qkv_w"] = torch.cat([get(p + f"self_attn.{n}_proj.weight") for n in ("q", "k", "v")], 0)
-        full[f"l{i}.o_w"] = get(p + "self_attn.o_proj.weight")
-        full[f"l{i}.mlp_norm"] = get(p + "post_attention_layernorm.weight")
-        full[f"l{i}.gate_up_w"] = torch.cat([get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")], 0)
-        full[f"l{i}.down_w"] = get(p + "mlp.down_proj.weight")
-    return shard_decoder_weights(full, cfg, tp_rank, tp_size, interleave_mlp)
+        w[f"l{i}.attn_norm"] = cast(st.get(p + "input_layernorm.weight"))
+        w[f"l{i}.mlp_norm"] = cast(st.get(p + "post_attention_layernorm.weight"))
+        q = st.rows(p + "self_attn.q_proj.weight", r * hq * D, (r + 1) * hq * D)
+        k = st.rows(p + "self_attn.k_proj.weight", r * hkv * D, (r + 1) * hkv * D)
+        v = st.rows(p + "self_attn.v_proj.weight", r * hkv * D, (r + 1) * hkv * D)
+        w[f"l{i}.qkv_w"] = cast(torch.cat([q, k, v], 0))
+        w[f"l{i}.o_w"] = cast(st.cols(p + "self_attn.o_proj.weight", r * hq * D, (r + 1) * hq * D))
+        gate = st.rows(p + "mlp.gate_proj.weight", r * f, (r + 1) * f).to(dtype)
+        up = st.rows(p + "mlp.up_proj.weight", r * f, (r + 1) * f).to(dtype)
+        w[f"l{i}.gate_up_w"] = _gate_up(gate, up, interleave_mlp).contiguous()
+        w[f"l{i}.down_w"] = cast(st.cols(p + "mlp.down_proj.weight", r * f, (r + 1) * f))
+    return w

@@ -34,7 +34,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     also returned (fused residual stream).  Returns (out, residual_out).
 
     ``x`` may also be fp32 split-K slabs [S, rows, cols] of the producing projection
-    (``skinny_gemm(..., splits=S)``): they are summed (and rounded to bf16) inside the kernel."""
+    (``stream_gemm(..., splits=S)``): they are summed (and rounded to bf16) inside the kernel."""
     slabs = x.dtype == torch.float32 and x.dim() == 3
     if not x.is_cuda:
         if slabs:
@@ -134,20 +134,23 @@ def gelu(x, bias=None, out=None):
     return out
 
 
-def silu_mul(x, interleaved=False):
-    """x [..., 2F] = [gate | up] -> silu(gate) * up  [..., F].  ``interleaved``: x columns are
-    16-wide [gate | up] groups (the projection of ``interleave_gate_up`` weights)."""
+def silu_mul(x, interleaved=False, group: int | None = None):
+    """x [..., 2F] = [gate | up] -> silu(gate) * up  [..., F].  ``group`` (or ``interleaved`` = 16):
+    x columns are ``group``-wide [gate | up] groups (the projection of ``interleave_gate_up``
+    weights; 0 = stacked halves)."""
+    group = (16 if interleaved else 0) if group is None else int(group)
     if not x.is_cuda:
-        if interleaved:
+        if group:
             F2 = x.shape[-1]
-            v = x.reshape(*x.shape[:-1], F2 // 32, 2, 16)
+            v = x.reshape(*x.shape[:-1], F2 // (2 * group), 2, group)
             x = torch.cat([v[..., 0, :].reshape(*x.shape[:-1], F2 // 2), v[..., 1, :].reshape(*x.shape[:-1], F2 // 2)], -1)
         return ref.silu_mul(x)
+    expect(group in (0, 16), "the GPU silu_mul takes stacked or 16-column groups (8-row groups: EPI_SWIGLU8)")
     expect_bf16_contig(x)
     F2 = x.shape[-1]
     rows = x.numel() // F2
     out = torch.empty((*x.shape[:-1], F2 // 2), dtype=x.dtype, device=x.device)
-    native().silu_mul(ptr(out), ptr(x), rows, F2 // 2, stream(x), int(interleaved))
+    native().silu_mul(ptr(out), ptr(x), rows, F2 // 2, stream(x), int(group == 16))
     return out
 
 
@@ -322,42 +325,104 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
     return out
 
 
+def paged_decode_rope(qkv, positions, cos_sin, slots, k_cache, v_cache, block_tables, ctx_lens, Hq, part_size=512,
+                      workspace: DecodeWorkspace | None = None, scale=None, out=None, order=None):
+    """``rope_kv_write`` + ``paged_decode`` in ONE launch: the decode attention builds q from the step's
+    QKV projection (bf16 [B, (Hq+2Hkv)D] or fp32 split-K slabs [S, B, (Hq+2Hkv)D]) with RoPE, and the
+    workgroup covering each sequence's last position writes the new rotated key and value into the
+    cache before it streams that partition.  Returns the attention output [B, Hq, D]; the cache
+    holds the new token afterwards, bitwise as after ``rope_kv_write``."""
+    Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
+    slabs = qkv.dtype == torch.float32 and qkv.dim() == 3
+    B = qkv.shape[-2]
+    if not qkv.is_cuda:
+        q = rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D)
+        return paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size, workspace, scale, out, order)
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    ld = (Hq + 2 * Hkv) * D
+    expect(qkv.shape[-1] == ld, "qkv width mismatch")
+    _i32(positions)
+    _i32(ctx_lens)
+    _i32(block_tables)
+    expect(slots.dtype == torch.int64 and slots.is_contiguous() and slots.numel() >= B, "slots must be int64 [B]")
+    expect(positions.numel() >= B, "positions shorter than the batch")
+    expect(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos/sin table")
+    expect_bf16_contig(k_cache, v_cache)
+    expect(k_cache.shape == v_cache.shape, "cache shape mismatch")
+    expect(D in (64, 128), "decode head dim must be 64 or 128")
+    expect(Hq % Hkv == 0 and Hq // Hkv <= 16, "GQA group must be <= 16")
+    expect(part_size % 128 == 0, "part_size must be a multiple of 128")
+    expect(block_tables.shape[0] >= B and ctx_lens.numel() >= B, "block table / ctx_lens rows < batch")
+    if slabs:
+        expect(qkv.is_contiguous(), "slabs must be contiguous")
+    else:
+        expect_bf16_contig(qkv)
+    max_parts = workspace.max_parts if workspace is not None else 1
+    if workspace is None:
+        part_size = max(part_size, ((block_tables.shape[1] * bs + 127) // 128) * 128)
+        ws_o = ws_m = ws_l = ws_c = None
+    else:
+        expect(workspace.o.numel() >= B * Hq * max_parts * D and workspace.cnt.numel() >= B * Hkv,
+               "decode workspace too small")
+        ws_o, ws_m, ws_l, ws_c = workspace.o, workspace.m, workspace.l, workspace.cnt
+    out = torch.empty((B, Hq, D), dtype=torch.bfloat16, device=qkv.device) if out is None else out
+    if order is not None:
+        _i32(order)
+        expect(order.is_cuda and order.numel() >= B, "decode order must hold the batch")
+    native().paged_decode_attention(0, ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
+                                    ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
+                                    D, int(part_size), int(max_parts), float(scale), stream(qkv), ptr(order),
+                                    0 if slabs else ptr(qkv), ptr(qkv) if slabs else 0,
+                                    qkv.shape[0] if slabs else 0, B * ld if slabs else 0, ld, ptr(positions),
+                                    ptr(cos_sin), ptr(slots))
+    return out
+
+
 # ----------------------------------------------------------------------------------------------
 # GEMM
 
 
-GEMM256_MIN_M = int(os.environ.get("DAB_GEMM256_MIN_M", "1024"))
+GEMM256_MIN_M = 1024  # the 8-phase 256x256 kernel from here on; the 128x128 kernel below
 
 
 def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    """Large-M shapes go to the 256x256 8-phase kernel (gemm256.hip); DAB_GEMM256=0 disables it,
-    =1 forces it for every eligible shape."""
-    mode = os.environ.get("DAB_GEMM256", "auto")
-    if mode == "0":
-        return False
-    if mode != "1" and M < GEMM256_MIN_M:
-        return False
-    return bool(native().gemm256_ok(M, N, K, lda, ldb))
+    """Large-M shapes go to the 256x256 8-phase kernel (gemm256.hip)."""
+    return M >= GEMM256_MIN_M and bool(native().gemm256_ok(M, N, K, lda, ldb))
 
 
 def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, row_group=None, q_group=None,
-            allow=None, out=None):
-    """C = A . B^T (+bias) (+act) (+residual) on MFMA; A [M, K], B [N, K] (K-contiguous rows)."""
+            allow=None, out=None, shuffled=False, n=None):
+    """C = A . B^T (+bias) (+act) (+residual) on MFMA; A [M, K], B [N, K] (K-contiguous rows).
+
+    ``shuffled``: B is a ``shuffle_weights`` copy (the layout the decode GEMM streams, so a model
+    keeps ONE copy of every projection) of ``B.shape[0]`` rows, of which the first ``n`` (default:
+    all) are the matrix."""
+    if shuffled:
+        R = B.shape[0]
+        N = R if n is None else int(n)
+        expect(R % 16 == 0 and B.shape[1] % 32 == 0 and B.is_contiguous() and R >= N,
+               "shuffled B: contiguous [R, K] copy, R % 16 == 0, K % 32 == 0, R >= n")
+        if not A.is_cuda:
+            Bu = unshuffle_weights(B)[:N]
+            return ref.gemm_bt(A, Bu, bias, residual, epilogue, out_f32, row_group, q_group, allow)
     if not A.is_cuda:
         return ref.gemm_bt(A, B, bias, residual, epilogue, out_f32, row_group, q_group, allow)
     expect(A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 operands required")
     expect(A.stride(-1) == 1 and B.stride(-1) == 1, "operands must be K-contiguous")
     M, K = A.shape
-    N = B.shape[0]
+    N = (B.shape[0] if n is None else int(n)) if shuffled else B.shape[0]
     expect(B.shape[1] == K, "inner dims mismatch")
     expect(K % 64 == 0 and N % 4 == 0, "gemm_bt needs K % 64 == 0 and N % 4 == 0")
     expect(A.stride(0) % 8 == 0 and B.stride(0) % 8 == 0, "row strides must be multiples of 8")
     if bias is not None:
         expect_bf16_contig(bias)
         expect(bias.numel() == N, "bias size mismatch")
-    n_out = N // 2 if epilogue == EPI_SWIGLU else N
+    n_out = N // 2 if epilogue in (EPI_SWIGLU, EPI_SWIGLU8) else N
     if epilogue == EPI_SWIGLU:
         expect(N % 32 == 0 and not out_f32, "swiglu epilogue needs N % 32 == 0 and bf16 output")
+    if epilogue == EPI_SWIGLU8:
+        expect(N % 32 == 0 and not out_f32 and bias is None and residual is None,
+               "swiglu8 epilogue needs N % 32 == 0, bf16 output, no bias / residual")
     if residual is not None:
         expect(residual.dtype == torch.bfloat16 and residual.stride(-1) == 1, "residual must be bf16 row-major")
         expect(tuple(residual.shape) == (M, n_out), "residual shape mismatch")
@@ -376,15 +441,36 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     if out is None:
         out = torch.empty((M, n_out), dtype=dtype, device=A.device)
     expect(out.dtype == dtype and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output buffer")
-    if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU) and not out_f32 and row_group is None and q_group is None
-            and allow is None and use_gemm256(M, N, K, A.stride(0), B.stride(0))):
-        native().gemm256(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
-                         residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), stream(A))
-        return out
+    if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SWIGLU8) and not out_f32 and row_group is None
+            and q_group is None and allow is None and (not shuffled or N == B.shape[0])
+            and use_gemm256(M, N, K, A.stride(0), B.stride(0))):
+        return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
     native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
                      residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), int(out_f32),
-                     ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A))
+                     ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A),
+                     B.shape[0] if shuffled else 0)
     return out
+
+
+def _gemm256_into(A, B, out, bias, residual, epilogue, shuffled):
+    M, K = A.shape
+    native().gemm256(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
+                     residual.stride(0) if residual is not None else 0, M, B.shape[0], K, int(epilogue), stream(A),
+                     int(shuffled))
+    return out
+
+
+def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
+    """The 8-phase 256x256 kernel directly, for any M (``gemm_bt`` takes it from M >= 1024):
+    tests and benchmarks.  N % 256 == 0, K % 128 == 0."""
+    M, K = A.shape
+    N = B.shape[0]
+    expect(A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 CUDA operands required")
+    expect(bool(native().gemm256_ok(M, N, K, A.stride(0), B.stride(0))), "gemm256: N % 256, K % 128, 16-B rows")
+    expect(not shuffled or (B.is_contiguous() and B.shape[1] == K), "shuffled B must be a contiguous [N, K] copy")
+    n_out = N // 2 if epilogue in (EPI_SWIGLU, EPI_SWIGLU8) else N
+    out = torch.empty((M, n_out), dtype=torch.bfloat16, device=A.device)
+    return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
 
 
 def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
@@ -413,13 +499,14 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
 
 
 def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=None):
-    """``score_candidates`` for 1..128 queries over a copy of the rows in the ``shuffle_weights``
-    layout (``B_shuf`` [R, K], R >= round_up(N, 128), R % 16 == 0): every 16-row x 32-k fragment
-    is one coalesced 1 KB load (1..16 queries: the persistent scan of index_scan.hip; 17..128: the
-    weight-streaming kernel's candidate epilogue)."""
+    """``score_candidates`` over a copy of the rows in the ``shuffle_weights`` layout (``B_shuf``
+    [R, K], R >= round_up(N, 128), R % 16 == 0): every 16-row x 32-k fragment is one coalesced 1 KB
+    load (1..16 queries: the persistent scan of index_scan.hip; 17..128: the weight-streaming
+    kernel's candidate epilogue; more: the 8-phase GEMM's candidate epilogue, 128x128 kernel when
+    K % 128)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
     M, K = A.shape
-    expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "1..128 queries, K % 128 (K % 256, K <= 1024 for <= 16)")
+    expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "queries need K % 128 == 0")
     expect(B_shuf.is_contiguous() and B_shuf.shape[1] == K, "shuffled copy [R, K]")
     expect(B_shuf.shape[0] % 16 == 0 and B_shuf.shape[0] >= -(-N // 128) * 128, "shuffled copy needs round_up(N, 128) rows")
     expect(thr.dtype == torch.float32 and thr.is_contiguous() and thr.numel() >= M, "thr must be fp32 [M]")
@@ -433,13 +520,14 @@ def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=No
     cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
     cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
     native().score_candidates_shuf(ptr(A), A.stride(0), ptr(B_shuf), M, int(N), K, ptr(row_group), ptr(q_group),
-                                   ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
+                                   ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A),
+                                   B_shuf.shape[0])
     return cand_val, cand_idx, cnt
 
 
 def shuffled_scan_ok(M: int, K: int) -> bool:
     """Query counts / widths ``score_candidates_shuffled`` serves."""
-    return (1 <= M <= 16 and K % 256 == 0 and K <= 1024) or (16 < M <= 128 and K % 128 == 0)
+    return M >= 1 and K % 128 == 0
 
 
 def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor) -> None:
@@ -451,86 +539,45 @@ def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor)
     v5[rows // 16, :, :, rows % 16, :] = vals.to(dst.dtype).reshape(-1, K // 32, 4, 8)
 
 
-SKINNY_MAX_M = 128
-_SK_KSTAGE = 256
-
-
-def skinny_splits(N: int, K: int, target_wgs: int = 256, max_splits: int = 16) -> int:
-    """K-slices for the weight-streaming GEMM: the fewest that give ~target_wgs workgroups (each
-    workgroup streams 64 weight rows of one slice)."""
-    tiles = N // 64
-    best = 1
-    for s in range(1, max_splits + 1):
-        if K % (s * _SK_KSTAGE):
-            continue
-        best = s
-        if tiles * s >= target_wgs:
-            break
-    return best
-
-
-SKINNY_NT_WEIGHTS = os.environ.get("DAB_SKINNY_NT", "0") == "1"
-
-
-def skinny_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=None):
-    """Decode GEMM y = x w^T for M <= 64 rows on the weight-streaming MFMA kernel.
-
-    splits == 1 -> bf16 [M, N] (or [M, N/2] with EPI_SWIGLU on 16-row interleaved gate|up weights),
-    optional fused residual add.  splits > 1 -> fp32 K-slice slabs [splits, M, N] (sum them with
-    ``skinny_reduce`` or hand them to a slab-aware consumer)."""
-    if not x.is_cuda:
-        y = ref.gemm_bt(x, w, None, None, epilogue, out_f32=splits > 1)
-        if splits > 1:
-            return torch.cat([y[None], torch.zeros((splits - 1,) + tuple(y.shape), dtype=y.dtype)], 0)
-        return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
-    expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
-    expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
-    M, K = x.shape
-    N = w.shape[0]
-    expect(w.shape[1] == K and M <= SKINNY_MAX_M, "skinny_gemm: inner dims mismatch or M > 128")
-    expect(N % 64 == 0 and K % (splits * _SK_KSTAGE) == 0, "skinny_gemm needs N % 64 == 0 and K % (256*splits) == 0")
-    expect(x.stride(0) % 8 == 0 and w.stride(0) % 8 == 0, "row strides must be multiples of 8")
+def _ref_stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None):
+    """CPU semantics of ``stream_gemm`` (row-major ``w``): bf16 [M, N] / SwiGLU / fp32 slabs
+    [S, M, N] whose sum is the product (slab 0 holds it, the others are zero)."""
+    y = ref.gemm_bt(x, w, None, None, epilogue, out_f32=splits > 1)
     if splits > 1:
-        expect(epilogue == EPI_NONE and residual is None, "split-K writes raw slabs")
-        if out is None:
-            out = torch.empty((splits, M, N), dtype=torch.float32, device=x.device)
-        expect(out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
-        ldo = N
-    else:
-        n_out = N // 2 if epilogue == EPI_SWIGLU else N
-        if residual is not None:
-            expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
-                   and tuple(residual.shape) == (M, N), "residual must be bf16 [M, N]")
-        if out is None:
-            out = torch.empty((M, n_out), dtype=torch.bfloat16, device=x.device)
-        expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
-        ldo = out.stride(0)
-    native().skinny_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
-                         residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
-                         int(SKINNY_NT_WEIGHTS if nt is None else nt))
-    return out
+        return torch.cat([y[None], torch.zeros((splits - 1,) + tuple(y.shape), dtype=y.dtype)], 0)
+    return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
 
 
 STREAM_KS = 128
+STREAM_MAX_M = 256  # decode batches / prefill last-token LM heads up to this many rows stream the weights
 
 
 def shuffle_weights(w: torch.Tensor) -> torch.Tensor:
-    """[N, K] row-major -> the same values in the decode-stream layout [N/16][K/32][64 lanes][8]: the
+    """[N, K] row-major -> the same values in the fragment layout [N/16][K/32][64 lanes][8]: the
     16 x 32 tile an MFMA A fragment covers is 1 KB contiguous, in lane order (lane l = row l & 15,
     k 8 (l >> 4) .. + 8), so every weight load of the streaming kernel is one fully coalesced 1 KB
-    read.  Returned with shape [N, K] (only the memory order changes)."""
+    read, and the prefill GEMMs' LDS-DMA copies whole blocks (gemm256 / gemm_bt ``shuffled``).
+    Returned with shape [N, K] (only the memory order changes)."""
     N, K = w.shape
     expect(N % 16 == 0 and K % 32 == 0, "shuffle_weights needs N % 16 == 0 and K % 32 == 0")
     return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
 
 
-def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=None, cfg=0):
-    """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): same
-    contract and outputs as ``skinny_gemm`` (bf16 [M, N] / SwiGLU [M, N/2] / fp32 slabs [S, M, N]);
-    ``cfg`` picks the tile / ring configuration (``native().stream_gemm_bn(cfg)`` weight rows per
-    workgroup)."""
+def unshuffle_weights(w: torch.Tensor) -> torch.Tensor:
+    """Inverse of ``shuffle_weights``."""
+    N, K = w.shape
+    return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
+
+
+def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0):
+    """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): bf16
+    [M, N] (optional residual add), SwiGLU [M, N/2] over 16- / 8-row interleaved [gate | up] rows, or
+    fp32 K-slice slabs [S, M, N] (their sum is the product; consumers sum them in their prologue or
+    ``slab_reduce`` does).  ``cfg`` picks the tile / ring configuration
+    (``native().stream_gemm_bn(cfg)`` weight rows per workgroup); ``nt`` streams the weights with
+    non-temporal loads.  On the CPU ``w`` is row-major."""
     if not x.is_cuda:
-        return skinny_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual, out=out)
+        return _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual)
     expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
     expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
     M, K = x.shape
@@ -561,11 +608,11 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=N
         ldo = out.stride(0)
     native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
                          residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
-                         int(SKINNY_NT_WEIGHTS if nt is None else nt), int(cfg))
+                         int(bool(nt)), int(cfg))
     return out
 
 
-def skinny_reduce(slabs, residual=None, out=None):
+def slab_reduce(slabs, residual=None, out=None):
     """fp32 slabs [S, M, N] -> bf16 [M, N] (sum rounded to bf16, then + residual)."""
     if not slabs.is_cuda:
         y = slabs.sum(0).to(torch.bfloat16)
@@ -577,8 +624,8 @@ def skinny_reduce(slabs, residual=None, out=None):
     if residual is not None:
         expect(residual.dtype == torch.bfloat16 and tuple(residual.shape) == (M, N) and residual.stride(-1) == 1,
                "residual must be bf16 [M, N]")
-    native().skinny_reduce(ptr(out), out.stride(0), ptr(slabs), S, M, N, ptr(residual),
-                           residual.stride(0) if residual is not None else 0, stream(slabs))
+    native().slab_reduce(ptr(out), out.stride(0), ptr(slabs), S, M, N, ptr(residual),
+                         residual.stride(0) if residual is not None else 0, stream(slabs))
     return out
 
 

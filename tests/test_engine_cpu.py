@@ -167,39 +167,6 @@ def test_pipelined_decode_matches_synchronous():
     assert outs[True] == outs[False]
 
 
-def test_prefill_stream_groups():
-    """Large prefill steps split into two contiguous chunk ranges of near-equal tokens; small steps,
-    single chunks and halves under the minimum stay whole."""
-    eng = _engine(0, _weights())
-    eng.prefill_streams, eng.prefill_split_min = 2, 100
-    assert eng._prefill_groups([150, 60, 50, 140]) == [(0, 2), (2, 4)]
-    assert eng._prefill_groups([300, 20, 20]) == [(0, 3)]  # best cut leaves 40 tokens
-    assert eng._prefill_groups([400]) == [(0, 1)]
-    assert eng._prefill_groups([90, 90]) == [(0, 2)]  # 180 < 2 * 100
-    assert eng._prefill_groups([250, 10]) == [(0, 2)]  # the smaller half would be 10 tokens
-    eng.prefill_streams = 1
-    assert eng._prefill_groups([150, 60, 50, 140]) == [(0, 4)]
-
-
-def test_split_prefill_matches_single_forward():
-    """Two-stream prefill (sub-batches with their own metadata) gives the same greedy tokens as one
-    forward over the whole step."""
-    w = _weights()
-    prompts = [list(range(11, 11 + n)) for n in (40, 25, 60, 33, 18)]
-    outs = []
-    for streams in (1, 2):
-        eng = LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(w), max_batch=8, block_size=16,
-                        num_blocks=64, max_prefill_tokens=256, use_graphs=False, prefill_streams=streams)
-        eng.prefill_split_min = 32
-        assert eng._prefill_groups([len(p) for p in prompts]) == ([(0, 5)] if streams == 1 else [(0, 2), (2, 5)])
-        rids = [eng.add_request(p, SamplingParams(max_new_tokens=8, do_sample=False, temperature=0.0,
-                                                  ignore_eos=True)) for p in prompts]
-        while eng.has_unfinished():
-            eng.step()
-        outs.append([eng.pop_output(r).token_ids for r in rids])
-    assert outs[0] == outs[1]
-
-
 def test_prefix_blocks_are_shared_from_the_launch_of_their_chunk():
     """full blocks of a prompt chunk enter the prefix cache when the chunk is launched, not
     when the whole prompt (or the deferred read-back) completes.  A request that shares a long

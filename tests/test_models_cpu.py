@@ -146,15 +146,15 @@ def test_tensor_parallel_shards_reconstruct_full_model():
 
 
 def test_llama_interleaved_mlp_layout_matches():
-    """16-row interleaved gate|up weights (fused SwiGLU layout) give the same model."""
-    from django_assistant_bot_amd.models.weights import _interleave16
+    """8-row interleaved gate|up weights (the engine's fused-SwiGLU layout) give the same model."""
+    from django_assistant_bot_amd.models.weights import _gate_up
 
     cfg, full = _llama_pair(3)
     inter = dict(full)
     F = cfg.intermediate
     for i in range(cfg.layers):
         gu = full[f"l{i}.gate_up_w"]
-        inter[f"l{i}.gate_up_w"] = _interleave16(gu[:F], gu[F:])
+        inter[f"l{i}.gate_up_w"] = _gate_up(gu[:F], gu[F:], True)
     ids = list(range(5, 40))
     h_a, _ = _prefill(LlamaModel(cfg, full, "cpu"), cfg, ids)
     h_b, _ = _prefill(LlamaModel(cfg, inter, "cpu", interleaved_mlp=True), cfg, ids)
@@ -187,3 +187,52 @@ def test_gate_up_regroup_and_swiglu8_reference():
     got16 = ref.gemm_bt(x, w16, epilogue=ops.EPI_SWIGLU, out_f32=True)
     torch.testing.assert_close(got8, exp, atol=1e-4, rtol=1e-4)
     torch.testing.assert_close(got16, exp, atol=1e-4, rtol=1e-4)
+
+
+def _hf_checkpoint(tmp_path, cfg, full):
+    """The state in HF Llama tensor names, split over two safetensors files."""
+    from safetensors.torch import save_file
+
+    H, D, F = cfg.hidden, cfg.head_dim, cfg.intermediate
+    hf = {"model.embed_tokens.weight": full["embed"], "model.norm.weight": full["final_norm"]}
+    if "lm_head" in full:
+        hf["lm_head.weight"] = full["lm_head"]
+    for i in range(cfg.layers):
+        p = f"model.layers.{i}."
+        qkv = full[f"l{i}.qkv_w"]
+        hf[p + "self_attn.q_proj.weight"] = qkv[: cfg.heads * D]
+        hf[p + "self_attn.k_proj.weight"] = qkv[cfg.heads * D:(cfg.heads + cfg.kv_heads) * D]
+        hf[p + "self_attn.v_proj.weight"] = qkv[(cfg.heads + cfg.kv_heads) * D:]
+        hf[p + "self_attn.o_proj.weight"] = full[f"l{i}.o_w"]
+        hf[p + "mlp.gate_proj.weight"] = full[f"l{i}.gate_up_w"][:F]
+        hf[p + "mlp.up_proj.weight"] = full[f"l{i}.gate_up_w"][F:]
+        hf[p + "mlp.down_proj.weight"] = full[f"l{i}.down_w"]
+        hf[p + "input_layernorm.weight"] = full[f"l{i}.attn_norm"]
+        hf[p + "post_attention_layernorm.weight"] = full[f"l{i}.mlp_norm"]
+    keys = sorted(hf)
+    half = len(keys) // 2
+    save_file({k: hf[k].contiguous() for k in keys[:half]}, str(tmp_path / "model-00001-of-00002.safetensors"))
+    save_file({k: hf[k].contiguous() for k in keys[half:]}, str(tmp_path / "model-00002-of-00002.safetensors"))
+    return hf
+
+
+def test_tp_checkpoint_load_reads_only_the_rank_slices(tmp_path):
+    """VERDICT r2 "next" #4: each TP rank materialises ~1/tp of the projection bytes of a multi-file
+    checkpoint (safetensors get_slice), and its shard equals shard_decoder_weights(full state)."""
+    from django_assistant_bot_amd.models.weights import SafetensorsDir, load_decoder_checkpoint
+
+    cfg = decoder_config("tiny-llama-70b-layout")
+    full = random_decoder_weights(cfg, dtype=torch.float32, seed=11)
+    hf = _hf_checkpoint(tmp_path, cfg, full)
+    proj = sum(v.numel() * 4 for k, v in hf.items() if "_proj" in k)
+    repl = sum(v.numel() * 4 for k, v in hf.items() if "_proj" not in k)
+    for tp in (2, 4, 8):
+        for r in (0, tp - 1):
+            st = SafetensorsDir(str(tmp_path))
+            got = load_decoder_checkpoint(str(tmp_path), cfg, dtype=torch.float32, tp_rank=r, tp_size=tp,
+                                          interleave_mlp=True, reader=st)
+            want = shard_decoder_weights(full, cfg, r, tp, interleave_mlp=True)
+            assert set(got) == set(want)
+            for k in want:
+                assert torch.equal(got[k], want[k]), (tp, r, k)
+            assert st.bytes_read <= repl + proj / tp * 1.001, (tp, st.bytes_read, repl, proj)

@@ -1,6 +1,7 @@
-"""Model-level GPU checks: the decode step through the weight-streaming split-K GEMM (slab-summing
-RoPE / RMSNorm consumers, fused SwiGLU, skinny LM head) against the same model on the hipBLASLt
-path and against the fp32 CPU reference."""
+"""Model-level GPU checks: the decode step through the weight-streaming split-K GEMM over the
+fragment-layout weights (slab-summing RMSNorm and RoPE/KV-write-in-attention consumers, fused
+SwiGLU, streamed LM head) against the same model with row-major weights on the MFMA GEMMs, and
+against the fp32 CPU reference; plus production-width layers (Llama-3-8B / bge-large)."""
 import pytest
 import torch
 
@@ -33,31 +34,27 @@ def _run(model, cfg, prompts, device, dtype):
     return h, model.logits(h)
 
 
-@pytest.mark.parametrize("mode", ["stream", "skinny"])
 @pytest.mark.parametrize("B", [3, 20, 64, 128, 200, 256])
-def test_decode_skinny_matches_library_path_and_reference(B, mode, monkeypatch):
-    """Decode projections on the warp-specialised stream kernel (shuffled weights) or the split-K
-    skinny kernel vs hipBLASLt vs the fp32 reference."""
-    monkeypatch.setenv("DAB_DECODE_GEMM", mode)
+def test_decode_stream_matches_row_major_path_and_reference(B):
+    """Decode projections on the warp-specialised stream kernel (fragment-layout weights) vs the
+    row-major MFMA GEMM path vs the fp32 reference."""
     cfg = decoder_config("tiny-llama")
     w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True)
     gen = torch.Generator().manual_seed(B)
     prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
                for n in torch.randint(10, 150, (B,), generator=gen)]
     wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
-    m_sk = LlamaModel(cfg, wbf, DEV, interleaved_mlp=True)
-    assert m_sk.stream == (mode == "stream")
-    m_sk.skinny_for = {"qkv", "o", "gate_up", "down", "lm_head"}  # every decode projection
-    m_sk.use_skinny = True
-    h_sk, lg_sk = _run(m_sk, cfg, prompts, DEV, torch.bfloat16)
-    m_lib = LlamaModel(cfg, wbf, DEV, interleaved_mlp=True)
-    m_lib.use_skinny = False
-    h_lib, lg_lib = _run(m_lib, cfg, prompts, DEV, torch.bfloat16)
-    torch.testing.assert_close(h_sk.float(), h_lib.float(), atol=6e-2, rtol=5e-2)
-    torch.testing.assert_close(lg_sk.float(), lg_lib.float(), atol=6e-2, rtol=5e-2)
+    m_fr = LlamaModel(cfg, wbf, DEV, interleaved_mlp=True)
+    assert m_fr.frag
+    h_fr, lg_fr = _run(m_fr, cfg, prompts, DEV, torch.bfloat16)
+    m_rm = LlamaModel(cfg, wbf, DEV, interleaved_mlp=True, fragment_layout=False)
+    assert not m_rm.frag
+    h_rm, lg_rm = _run(m_rm, cfg, prompts, DEV, torch.bfloat16)
+    torch.testing.assert_close(h_fr.float(), h_rm.float(), atol=6e-2, rtol=5e-2)
+    torch.testing.assert_close(lg_fr.float(), lg_rm.float(), atol=6e-2, rtol=5e-2)
     m_ref = LlamaModel(cfg, {k: v.bfloat16().float() for k, v in w32.items()}, "cpu", interleaved_mlp=True)
     h_ref, _ = _run(m_ref, cfg, prompts, "cpu", torch.float32)
-    err = (h_sk.float().cpu() - h_ref).abs().max().item()
+    err = (h_fr.float().cpu() - h_ref).abs().max().item()
     assert err < 0.15, err
 
 
@@ -167,58 +164,6 @@ def test_engine_pipelined_decode_matches_synchronous_on_gpu():
         assert eng.stats["graph_replays"] > 0
         outs[pipe] = (sampled, free_run, stopped)
     assert outs[True] == outs[False]
-
-
-def test_overlapped_prefill_matches_single_forward():
-    """Prefill split into two sub-batches on two HIP streams (forward_overlapped) == one forward over
-    the whole step: final hidden states and the K/V written to the paged cache."""
-    cfg = decoder_config("tiny-llama")
-    w = {k: v.to(torch.bfloat16) for k, v in
-         random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True).items()}
-    model = LlamaModel(cfg, w, DEV, interleaved_mlp=True)
-    bs, nbp = 64, 8
-    gen = torch.Generator().manual_seed(1)
-    prompts = [torch.randint(0, 900, (int(n),), generator=gen).tolist() for n in (300, 170, 411, 96, 250)]
-    i32 = dict(dtype=torch.int32, device=DEV)
-
-    def meta_for(idx):
-        ps = [prompts[i] for i in idx]
-        bt = torch.stack([torch.arange(i * nbp, (i + 1) * nbp, **i32) for i in idx])
-        cu = torch.tensor([0] + [sum(len(p) for p in ps[:j + 1]) for j in range(len(ps))], **i32)
-        return (torch.tensor([t for p in ps for t in p], **i32),
-                AttnMeta(decode=False, positions=torch.cat([torch.arange(len(p), **i32) for p in ps]),
-                         slots=torch.cat([bt[j, 0].long() * bs + torch.arange(len(p), device=DEV)
-                                          for j, p in enumerate(ps)]),
-                         block_tables=bt, ctx_lens=torch.tensor([len(p) for p in ps], **i32), cu_q=cu,
-                         max_q=max(len(p) for p in ps)))
-
-    kv1 = KVCache(cfg.layers, len(prompts) * nbp, cfg.kv_heads, bs, cfg.head_dim, DEV)
-    kv2 = KVCache(cfg.layers, len(prompts) * nbp, cfg.kv_heads, bs, cfg.head_dim, DEV)
-    ids, meta = meta_for(range(5))
-    h1 = model.forward(ids, meta, kv1)
-    h2 = model.forward_overlapped([meta_for(range(2)), meta_for(range(2, 5))], kv2)
-    torch.cuda.synchronize()
-    assert h2.shape == h1.shape
-    torch.testing.assert_close(h2.float(), h1.float(), rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(kv2.k.float(), kv1.k.float(), rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(kv2.v.float(), kv1.v.float(), rtol=3e-2, atol=3e-2)
-    assert hasattr(model, "_side_streams")
-
-
-def test_engine_two_stream_prefill_on_gpu():
-    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
-
-    eng = LLMEngine("tiny-llama", device=DEV, max_batch=16, block_size=64, num_blocks=128,
-                    max_prefill_tokens=4096, prefill_streams=2)
-    eng.prefill_split_min = 256
-    sp = SamplingParams(max_new_tokens=12, ignore_eos=True)
-    rids = [eng.add_request(list(range(10, 10 + 200 + 31 * i)), sp) for i in range(8)]
-    while eng.has_unfinished():
-        eng.step()
-    outs = [eng.pop_output(r) for r in rids]
-    assert hasattr(eng.model, "_side_streams")
-    assert all(len(o.token_ids) == 12 for o in outs)
-    assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
 
 
 def test_bert_encoder_bge_base_matches_hf_bertmodel(tmp_path):

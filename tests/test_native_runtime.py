@@ -121,3 +121,19 @@ def test_kv_manager_packs_blocks_low_and_caps_cached_prefixes(n):
     assert got == sorted(got) and got[0] < 400 and len(got) == 10
     # the most recently cached prefixes still hit
     assert m.add_sequence(501, [99 * 1000 + i for i in range(13)], 0) == 12
+
+
+def test_every_native_entry_point_called_from_python_is_bound(n):
+    """Each ``native().<name>`` the Python package calls exists in the built extension (a binding lost
+    in an edit otherwise only shows up on the GPU box)."""
+    import pathlib
+    import re
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    names = set()
+    for d in ("django_assistant_bot_amd", "gpu_service", "benchmarks", "tests"):
+        for f in (root / d).rglob("*.py"):
+            names |= set(re.findall(r"native\(\)\.([A-Za-z_]\w*)", f.read_text()))
+    assert len(names) > 20
+    missing = sorted(x for x in names if not hasattr(n, x))
+    assert not missing, missing
