@@ -2,7 +2,8 @@
 ai/providers/transformers.py:9-94).
 
 Same contract: prompt rendered as ``"role: content"`` lines (no chat template), sampling with
-top_k=50 / top_p=0.95, JSON mode parses the text and falls back to the raw string, usage reports
+top_k=50 / top_p=0.95, JSON mode returns the parsed object (constrained decoding: the text is
+one JSON object by construction; the raw string is kept if it still fails to parse), usage reports
 prompt/completion token counts, ``length_limited`` when the completion hit the budget.  Differences:
 requests from all concurrent callers share one continuous batch on the GPU (``LLMWorker``), and
 ``max_tokens`` bounds the completion only (the reference's ``max_length`` also counted the prompt).
@@ -44,7 +45,10 @@ class TransformersProvider(AIProvider):
 
         prompt = render_prompt(messages)
         ids = self._tokenizer.encode(prompt, add_special=True, max_len=self._worker.engine.max_model_len - 1)
-        params = SamplingParams(max_new_tokens=max_tokens, temperature=1.0, top_k=50, top_p=0.95)
+        # JSON mode constrains the sampler to one JSON object (engine/json_constraint.py): valid in
+        # one generation where the reference retries until json.loads succeeds
+        params = SamplingParams(max_new_tokens=max_tokens, temperature=1.0, top_k=50, top_p=0.95,
+                                json_mode=bool(json_format))
         out = await self._worker.generate(ids, params)
         text = out.text.strip()
         result = text

@@ -124,10 +124,12 @@ def measure_fast_steps(rag, llm, questions, info, dev, classify_tokens: int = 16
     (/root/reference/assistant/bot/services/context_service/steps/classify.py:41-45, <= 256 tokens)
     and ChooseKnownQuestionStep (.../steps/choose_known_question.py:45-50).  Both run here with the
     same prompt builders as the app layer (assistant.bot.services.context_service.steps), batched
-    over the questions of one batch on the same engine, back to back.  With random-init weights the
-    JSON answers have no natural length, so they are generated at the length of a schema-valid answer
-    ({"topic": "<title>"} ~ 16 tokens, {"question": <n>} ~ 8 tokens, ignore_eos).  Returns seconds
-    per batch (max over ranks) and the prompt sizes."""
+    over the questions of one batch on the same engine, back to back, in JSON mode (constrained
+    decoding: one generation per answer where the reference retries up to 5 times).  With
+    random-init weights the JSON answers have no natural length, so the budget is that of a
+    schema-valid answer ({"topic": "<title>"} ~ 16 tokens, {"question": <n>} ~ 8 tokens); an answer
+    ends when its object closes.  Returns seconds per batch (max over ranks), the prompt sizes and
+    the fraction of answers that parse."""
     from assistant.bot.services.context_service.steps.choose_known_question import ChooseKnownQuestionStep
     from assistant.bot.services.context_service.steps.classify import ClassifyStep
     from assistant.bot.services.context_service.utils import add_system_message
@@ -158,21 +160,29 @@ def measure_fast_steps(rag, llm, questions, info, dev, classify_tokens: int = 16
     base = [[{"role": "system", "content": SYSTEM_TEXT}, {"role": "user", "content": q}] for q in questions]
     cls_prompts = encode([render_messages(add_system_message(m, ClassifyStep.prompt(topics, examples, q)))
                           for m, q in zip(base, questions)])
-    llm.generate(cls_prompts, SamplingParams(max_new_tokens=classify_tokens, ignore_eos=True))
+    outs = llm.generate(cls_prompts, SamplingParams(max_new_tokens=classify_tokens, ignore_eos=True, json_mode=True))
     sync()
     t1 = time.perf_counter()
     related = [[int(x.split()[0][1:]) for x in dbg["related_questions"]] for _, dbg in rag.retrieve(questions, 0)]
     kq_prompts = encode([render_messages(add_system_message([], ChooseKnownQuestionStep.prompt(
         q, [row_question(r) for r in rel[:5]]))) for q, rel in zip(questions, related)])
-    llm.generate(kq_prompts, SamplingParams(max_new_tokens=known_tokens, ignore_eos=True))
+    outs += llm.generate(kq_prompts, SamplingParams(max_new_tokens=known_tokens, ignore_eos=True, json_mode=True))
     sync()
     t2 = time.perf_counter()
+
+    def parses(text):
+        try:
+            return isinstance(json.loads(text), dict)
+        except ValueError:
+            return False
     cls_s = pdist.max_over_ranks(t1 - t0, dev)
     kq_s = pdist.max_over_ranks(t2 - t1, dev)
     return {"classify_s": round(cls_s, 4), "known_question_s": round(kq_s, 4), "total_s": round(cls_s + kq_s, 4),
             "classify_prompt_tokens": int(np.mean([len(p) for p in cls_prompts])),
             "known_question_prompt_tokens": int(np.mean([len(p) for p in kq_prompts])),
-            "answer_tokens": [classify_tokens, known_tokens], "batch": len(questions)}
+            "answer_tokens": [classify_tokens, known_tokens], "batch": len(questions),
+            "json_valid": round(float(np.mean([parses(o.text) for o in outs])), 4),
+            "json_mean_tokens": round(float(np.mean([len(o.token_ids) for o in outs])), 2)}
 
 
 def _host_profiler():

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "kernels/launchers.h"
+#include "runtime/json_grammar.h"
 #include "runtime/kv_manager.h"
 #include "runtime/rag.h"
 #include "runtime/tokenizer.h"
@@ -224,6 +225,11 @@ PYBIND11_MODULE(_native, m) {
                                     ST(s)),
           "sample_tokens_2stage");
   });
+  m.def("mask_logits", [](u logits, int f32, long ld, int rows, int vocab, u mask, int words, u row_flags, u s) {
+    check(dab::mask_logits(VP(logits), f32, ld, rows, vocab, (const uint32_t*)mask, words, (const int*)row_flags,
+                           ST(s)),
+          "mask_logits");
+  });
   m.def("topk_rows_2stage", [](u scores, long ld, int rows, int n, int k, u out_vals, u out_idx, long long base,
                                u out_idx64, u ws, size_t ws_bytes, u s) {
     check(dab::topk_rows_2stage((const float*)scores, ld, rows, n, k, (float*)out_vals, (int*)out_idx, base,
@@ -264,7 +270,44 @@ PYBIND11_MODULE(_native, m) {
           },
           py::arg("texts"), py::arg("add_special") = true, py::arg("max_len") = 0, py::arg("threads") = 8)
       .def("decode", &dab::HashTokenizer::decode, py::arg("ids"), py::arg("skip_special") = true)
+      .def("token_texts",
+           [](const dab::HashTokenizer& t) {
+             py::list out;
+             for (const auto& w : t.token_texts()) out.append(py::bytes(w));
+             return out;
+           })
       .def_static("count_words", &dab::HashTokenizer::count_words);
+
+  // ---------------- JSON-constrained decoding ----------------
+  py::class_<dab::JsonVocab, std::shared_ptr<dab::JsonVocab>>(m, "JsonVocab")
+      .def(py::init([](const std::vector<py::bytes>& toks, const std::vector<int32_t>& eos) {
+             std::vector<std::string> t;
+             t.reserve(toks.size());
+             for (const auto& b : toks) t.emplace_back(b);
+             return std::make_shared<dab::JsonVocab>(t, eos);
+           }),
+           py::arg("tokens"), py::arg("eos_ids"))
+      .def("vocab_size", &dab::JsonVocab::vocab_size)
+      .def("words", &dab::JsonVocab::words)
+      .def("trie_nodes", &dab::JsonVocab::trie_nodes)
+      .def("cache_entries", &dab::JsonVocab::cache_entries);
+  py::class_<dab::JsonMatcher>(m, "JsonMatcher")
+      .def(py::init<std::shared_ptr<dab::JsonVocab>, int, int>(), py::arg("vocab"), py::arg("max_depth") = 24,
+           py::arg("max_ws") = 8)
+      .def("fill_mask",
+           [](dab::JsonMatcher& j, int remaining, u out) {
+             py::gil_scoped_release rel;
+             return j.fill_mask(remaining, (uint32_t*)out);
+           })
+      .def("advance", &dab::JsonMatcher::advance)
+      .def("done", &dab::JsonMatcher::done)
+      .def("broken", &dab::JsonMatcher::broken)
+      .def("completion", [](const dab::JsonMatcher& j) { return py::bytes(j.completion()); })
+      .def("completion_len", &dab::JsonMatcher::completion_len)
+      .def("text", [](const dab::JsonMatcher& j) { return py::bytes(j.text()); });
+  m.def("json_accepts", [](const py::bytes& b, bool complete, int max_depth, int max_ws) {
+    return dab::json_accepts(std::string(b), complete, max_depth, max_ws);
+  }, py::arg("bytes"), py::arg("complete") = true, py::arg("max_depth") = 64, py::arg("max_ws") = 255);
 
   // ---------------- KV block manager ----------------
   py::class_<dab::KVBlockManager>(m, "KVBlockManager")

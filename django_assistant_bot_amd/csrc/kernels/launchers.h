@@ -102,6 +102,10 @@ int stream_gemm_max_m(int cfg);
 int stream_gemm_shuffled(int cfg);  // 1: cfg reads weights in the ops.shuffle_weights layout
 
 // select.hip
+// Disallowed tokens of the rows with row_flags[r] != 0 (mask bit clear) -> -inf logits, in place
+// (JSON-constrained decoding); rows without the flag are untouched.
+int mask_logits(void* logits, int logits_f32, long ld, int rows, int vocab, const uint32_t* mask, int words,
+                const int* row_flags, hipStream_t s);
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
                   const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
                   float* out_logprobs, hipStream_t s);

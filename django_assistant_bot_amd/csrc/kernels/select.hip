@@ -611,6 +611,39 @@ int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float
   return hipGetLastError();
 }
 
+// One thread per 32 tokens (one mask word): the row flag and the word are read once, the logits
+// of the disallowed tokens are overwritten with -inf.  Grid (ceil(words / 256), rows); rows
+// without the flag return after one load.
+__global__ __launch_bounds__(256) void mask_logits_kernel(void* __restrict__ logits, int logits_f32, long ld,
+                                                          int vocab, const uint32_t* __restrict__ mask, int words,
+                                                          const int* __restrict__ row_flags) {
+  const int row = blockIdx.y;
+  if (row_flags[row] == 0) return;
+  const int w = blockIdx.x * 256 + threadIdx.x;
+  if (w >= words) return;
+  const uint32_t bits = mask[(size_t)row * words + w];
+  if (bits == 0xFFFFFFFFu) return;
+  const int t0 = w * 32, n = min(32, vocab - t0);
+  if (logits_f32) {
+    float* l = reinterpret_cast<float*>(logits) + (size_t)row * ld + t0;
+    for (int j = 0; j < n; ++j)
+      if (!((bits >> j) & 1u)) l[j] = -INFINITY;
+  } else {
+    bf16* l = reinterpret_cast<bf16*>(logits) + (size_t)row * ld + t0;
+    for (int j = 0; j < n; ++j)
+      if (!((bits >> j) & 1u)) l[j] = f2bf(-INFINITY);
+  }
+}
+
+int mask_logits(void* logits, int logits_f32, long ld, int rows, int vocab, const uint32_t* mask, int words,
+                const int* row_flags, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (vocab <= 0 || words * 32 < vocab) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mask_logits_kernel, dim3((words + 255) / 256, rows), dim3(256), 0, s, logits, logits_f32, ld,
+                     vocab, mask, words, row_flags);
+  return hipGetLastError();
+}
+
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
                   const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
                   float* out_logprobs, hipStream_t s) {

@@ -210,6 +210,21 @@ std::string HashTokenizer::decode(const std::vector<int32_t>& ids, bool skip_spe
   return out;
 }
 
+std::vector<std::string> HashTokenizer::token_texts() const {
+  std::vector<std::string> out(cfg_.vocab_size);
+  std::lock_guard<std::mutex> lk(mu_);
+  for (int32_t id = 0; id < cfg_.vocab_size; ++id) {
+    const bool special = id == cfg_.pad_id || id == cfg_.cls_id || id == cfg_.sep_id || id == cfg_.unk_id ||
+                         id < cfg_.first_id || id >= cfg_.last_id;
+    if (special) continue;
+    auto it = seen_.find(id);
+    const std::string w = it != seen_.end() ? it->second : pseudo_word(id);
+    const bool punct = w.size() == 1 && !((w[0] >= 'a' && w[0] <= 'z') || (w[0] >= '0' && w[0] <= '9'));
+    out[id] = punct ? w : " " + w;
+  }
+  return out;
+}
+
 int64_t HashTokenizer::count_words(const std::string& text) {
   int64_t n = 0;
   bool in = false;

@@ -42,6 +42,9 @@ class HashTokenizer {
   void encode_batch(const std::vector<std::string>& texts, bool add_special, int max_len, int threads,
                     std::vector<int32_t>& ids, std::vector<int64_t>& offsets) const;
   std::string decode(const std::vector<int32_t>& ids, bool skip_special) const;
+  // The bytes each id adds to decode() output after a first token (" word" or a lone punctuation
+  // character; "" for special ids): the vocabulary of the JSON-constrained decoder.
+  std::vector<std::string> token_texts() const;
   // Number of whitespace separated words (used by the reference's crude token estimate).
   static int64_t count_words(const std::string& text);
   const TokenizerConfig& config() const { return cfg_; }

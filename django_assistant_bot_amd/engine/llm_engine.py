@@ -49,6 +49,7 @@ class SamplingParams:
     stop_token_ids: tuple = ()
     do_sample: bool = True
     timeout_s: float | None = None  # per-request deadline from arrival: finish_reason "timeout"
+    json_mode: bool = False  # constrain the output to one JSON object (engine/json_constraint.py)
 
 
 @dataclass
@@ -77,6 +78,7 @@ class _Req:
     rng_base: int = 0
     prefill_s: float = 0.0
     preempted: int = 0
+    matcher: object = None  # native JsonMatcher of a json_mode request
 
     @property
     def seq(self):
@@ -194,6 +196,8 @@ class LLMEngine:
                        for k in ("_h_ids", "_h_pos", "_h_slots", "_h_ctx", "_h_bt", "_h_temp", "_h_topk", "_h_topp",
                                  "_h_cnt", "_h_tokens", "_h_order")}
         self._inflight = None  # launched decode step whose tokens are not consumed yet
+        self._d_mask = None  # JSON-constrained decoding buffers (allocated on first use)
+        self._masked = False
         # launched prefill chunk whose sampled first tokens are not read back yet (GPU): the next
         # chunk is launched before they are, so consecutive chunks run back to back
         self._pending_prefill = None
@@ -223,6 +227,11 @@ class LLMEngine:
             prompt = prompt[-(self.max_model_len - 1):]
         seed = params.seed if params.seed is not None else self.seed
         r = _Req(rid, prompt, params, time.perf_counter(), rng_base=((seed * 1000003 + rid) & 0xFFFFFFFF) << 20)
+        if params.json_mode:
+            from .json_constraint import matcher_for
+
+            r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids)
+            self._ensure_mask_buffers()
         self.waiting.append(r)
         return rid
 
@@ -522,8 +531,46 @@ class LLMEngine:
             key = f"gpu_{name}_ms"
             self.stats[key] = self.stats.get(key, 0.0) + ms
 
+    # ------------------------------------------------------------------ JSON-constrained rows
+    def _ensure_mask_buffers(self) -> None:
+        if getattr(self, "_d_mask", None) is not None:
+            return
+        W = -(-self.cfg.vocab_size // 32)
+        mb = self.max_batch
+        pin = self.is_gpu
+        self._h_mask = torch.zeros((mb, W), dtype=torch.int32, pin_memory=pin)
+        self._h_mflag = torch.zeros(mb, dtype=torch.int32, pin_memory=pin)
+        self._d_mask = torch.zeros((mb, W), dtype=torch.int32, device=self.device)
+        self._d_mflag = torch.zeros(mb, dtype=torch.int32, device=self.device)
+
+    def _budget(self, r: _Req) -> int:
+        """Tokens ``r`` may still generate, the one being sampled included."""
+        n, p = len(r.out), r.params
+        left = min(p.max_new_tokens - n, self.max_model_len - len(r.prompt) - n)
+        if p.max_length is not None:
+            left = min(left, p.max_length - len(r.prompt) - n)
+        return max(left, 1)
+
+    def _fill_masks(self, reqs, n_rows: int) -> bool:
+        """Host masks + row flags of the constrained rows among ``reqs`` (rows past them unflagged)
+        and their H2D copies.  -> whether any row is constrained."""
+        if not any(r.matcher is not None for r in reqs):
+            return False
+        self._h_mflag[:n_rows] = 0
+        row_bytes = self._h_mask.shape[1] * 4
+        base = self._h_mask.data_ptr()
+        for i, r in enumerate(reqs):
+            if r.matcher is not None:
+                r.matcher.fill_mask(self._budget(r), base + i * row_bytes)
+                self._h_mflag[i] = 1
+        self._d_mask[:n_rows].copy_(self._h_mask[:n_rows], non_blocking=True)
+        self._d_mflag[:n_rows].copy_(self._h_mflag[:n_rows], non_blocking=True)
+        return True
+
     def _sample(self, logits, reqs, to_host: bool = True):
         n = len(reqs)
+        if self._fill_masks(reqs, n):
+            ops.mask_logits(logits, self._d_mask[:n], self._d_mflag[:n])
         temps = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in reqs], dtype=torch.float32)
         topk = torch.tensor([r.params.top_k for r in reqs], dtype=torch.int32)
         topp = torch.tensor([r.params.top_p for r in reqs], dtype=torch.float32)
@@ -550,7 +597,15 @@ class LLMEngine:
         r.out.append(tok)
         p = r.params
         reason = ""
-        if not p.ignore_eos and (tok in self.cfg.eos_ids or tok in p.stop_token_ids):
+        json_done = False
+        if r.matcher is not None:
+            if r.matcher.advance(tok):
+                json_done = r.matcher.done()
+            else:  # only after a mask fallback (no grammar-valid token was left)
+                self.stats["json_broken"] = self.stats.get("json_broken", 0) + 1
+        if json_done:
+            reason = "stop"  # the JSON object is complete
+        elif not p.ignore_eos and (tok in self.cfg.eos_ids or tok in p.stop_token_ids):
             reason = "stop"
         elif len(r.out) >= p.max_new_tokens:
             reason = "length"
@@ -580,7 +635,9 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ pipelined decode
     def _can_pipeline(self) -> bool:
-        return bool(self.pipeline_decode and self.running and not self.waiting and not self.prefilling)
+        # constrained rows need each token on the host before the next step's mask
+        return bool(self.pipeline_decode and self.running and not self.waiting and not self.prefilling
+                    and not any(r.matcher is not None for r in self.running))
 
     def _swap_host_buffers(self) -> None:
         for k, alt in self._h_alt.items():
@@ -666,9 +723,10 @@ class LLMEngine:
                 self._d_ids[B:Bp].zero_()
         for d, h in pairs:
             d[:Bp].copy_(h[:Bp], non_blocking=True)
+        self._masked = False
         g = None
         if self.use_graphs:
-            g = self._graphs.get((Bp, self._fast))
+            g = self._graphs.get((Bp, self._fast, False))
             if g is None:
                 g = self._capture(Bp)
         with self.timer.phase("decode"):
@@ -752,10 +810,11 @@ class LLMEngine:
                      (self._d_topp, self._h_topp), (self._d_cnt, self._h_cnt), (self._d_order, self._h_order)):
             d[:Bp].copy_(h[:Bp], non_blocking=True)
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
+        self._masked = self._fill_masks(batch, Bp)
         t1 = time.perf_counter()
         g = None
         if self.use_graphs:
-            g = self._graphs.get((Bp, self._fast))
+            g = self._graphs.get((Bp, self._fast, self._masked))
             if g is None:
                 g = self._capture(Bp)
         with self.timer.phase("decode"):
@@ -798,6 +857,8 @@ class LLMEngine:
                         part_size=self._decode_part(Bp), order=self._d_order[:Bp] if self.is_gpu else None)
         h = self.model.forward(self._d_ids[:Bp], meta, self.kv)
         logits = self.model.logits(h)
+        if self._masked:
+            ops.mask_logits(logits, self._d_mask[:Bp], self._d_mflag[:Bp])
         if self.is_gpu:
             ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp], self.seed,
                               self._d_cnt[:Bp], out=self._d_tokens[:Bp], fast=self._fast,
@@ -823,7 +884,7 @@ class LLMEngine:
             with torch.cuda.graph(g, pool=self._graph_pool, stream=s):
                 self._decode_body(Bp)
             torch.cuda.synchronize(self.device)
-            self._graphs[(Bp, self._fast)] = g
+            self._graphs[(Bp, self._fast, self._masked)] = g
             return g
         except Exception as exc:  # pragma: no cover - depends on the runtime
             import logging
@@ -834,6 +895,7 @@ class LLMEngine:
 
     def capture_all(self, sizes=None):
         self._fast = True
+        self._masked = False
         for b in sizes or self._buckets:
-            if (b, True) not in self._graphs:
+            if (b, True, False) not in self._graphs:
                 self._capture(b)

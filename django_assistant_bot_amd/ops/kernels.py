@@ -692,6 +692,24 @@ def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, genera
     return out
 
 
+def mask_logits(logits, mask, row_flags):
+    """In place: logits[r, t] = -inf where bit t of ``mask[r]`` (int32 words, bit t % 32 of word
+    t // 32) is clear, for the rows whose ``row_flags[r]`` (int32) is non-zero (JSON-constrained
+    decoding).  Returns ``logits``."""
+    rows, vocab = logits.shape
+    expect(mask.dtype == torch.int32 and mask.is_contiguous() and mask.shape[0] >= rows and mask.shape[1] * 32 >= vocab,
+           "mask: int32 [rows, ceil(vocab / 32)]")
+    if not logits.is_cuda:
+        bits = (mask[:rows].view(torch.int32).unsqueeze(-1) >> torch.arange(32, dtype=torch.int32)) & 1
+        allow = bits.reshape(rows, -1)[:, :vocab].bool() | (row_flags[:rows] == 0).unsqueeze(1)
+        return logits.masked_fill_(~allow, float("-inf"))
+    expect(logits.stride(-1) == 1 and logits.dtype in (torch.float32, torch.bfloat16), "logits: fp32/bf16 rows")
+    _i32(row_flags)
+    native().mask_logits(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab, ptr(mask),
+                         mask.shape[1], ptr(row_flags), stream(logits))
+    return logits
+
+
 def topk_rows(scores, k, index_base=0, want_global=False):
     """Exact per-row top-k of fp32 scores, sorted descending.  Returns (values, idx int32) or, with
     ``want_global``, (values, idx + index_base as int64).  Long rows use the two-stage kernel."""

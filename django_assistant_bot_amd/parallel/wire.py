@@ -149,7 +149,7 @@ def add_item(model: int, rid: int, prompt, params):
     stop = [int(t) for t in (params.stop_token_ids or ())]
     words = [ADD, model, rid, len(prompt), len(stop), int(params.max_new_tokens), f2i(params.temperature),
              int(params.top_k), f2i(params.top_p), int(bool(params.ignore_eos)), opt_i(params.max_length),
-             opt_i(params.seed), int(bool(params.do_sample)), opt_f(params.timeout_s)]
+             opt_i(params.seed), int(bool(params.do_sample)), opt_f(params.timeout_s), int(bool(params.json_mode))]
     return item(words, list(prompt) + stop)
 
 
@@ -160,7 +160,7 @@ def read_add(h, p):
     sp = SamplingParams(max_new_tokens=int(h[5]), temperature=i2f(h[6]), top_k=int(h[7]), top_p=i2f(h[8]),
                         ignore_eos=bool(h[9]), max_length=i_opt(h[10]), seed=i_opt(h[11]),
                         stop_token_ids=tuple(int(t) for t in p[n_prompt:]), do_sample=bool(h[12]),
-                        timeout_s=f_opt(h[13]))
+                        timeout_s=f_opt(h[13]), json_mode=bool(h[14]))
     return int(h[1]), int(h[2]), [int(t) for t in p[:n_prompt]], sp
 
 

@@ -722,6 +722,22 @@ def test_index_recall_at_250_vs_fp32_oracle(nq):
     assert torch.all(v[:, :-1] >= v[:, 1:])
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_mask_logits(dtype):
+    """JSON-constrained decoding's mask kernel == the CPU masked_fill reference (flagged rows only,
+    vocab not a multiple of 32)."""
+    rows, V = 37, 128256 + 5
+    W = -(-V // 32)
+    logits = torch.randn(rows, V, device=DEV).to(dtype)
+    mask = torch.randint(-2**31, 2**31 - 1, (rows, W), dtype=torch.int32, device=DEV)
+    mask[3] = -1  # all allowed
+    flags = (torch.arange(rows, device=DEV) % 3 != 1).to(torch.int32)
+    exp = ops.mask_logits(logits.cpu().clone(), mask.cpu(), flags.cpu())
+    got = ops.mask_logits(logits.clone(), mask, flags)
+    assert torch.equal(got.cpu(), exp)
+    assert torch.isinf(got[0]).any() and not torch.isinf(got[1]).any() and not torch.isinf(got[3]).any()
+
+
 def test_index_threshold_search_overflow_falls_back():
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 

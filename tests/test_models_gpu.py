@@ -166,6 +166,35 @@ def test_engine_pipelined_decode_matches_synchronous_on_gpu():
     assert outs[True] == outs[False]
 
 
+def test_engine_json_mode_on_gpu_graphs():
+    """JSON-constrained rows through the HIP-graph decode (masked graph variant + mask_logits kernel)
+    beside unconstrained rows: every constrained answer parses, unconstrained ones keep their
+    length, and a later unconstrained batch returns to the pipelined unmasked graphs."""
+    import json
+
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+
+    eng = LLMEngine("tiny-llama", device=DEV, max_batch=16, block_size=64, num_blocks=128, seed=2)
+    rids = [eng.add_request(list(range(3, 40 + 5 * i)), SamplingParams(max_new_tokens=6 + 3 * i, ignore_eos=True,
+                                                                        json_mode=i % 4 != 3, seed=i))
+            for i in range(12)]
+    while eng.has_unfinished():
+        eng.step()
+    outs = [eng.pop_output(r) for r in rids]
+    for i, o in enumerate(outs):
+        if i % 4 == 3:
+            assert len(o.token_ids) == 6 + 3 * i
+        else:
+            assert isinstance(json.loads(o.text), dict), o.text
+    assert any(k[2] for k in eng._graphs) and eng.stats["graph_replays"] > 0
+    assert eng.stats.get("json_broken", 0) == 0
+    r2 = [eng.add_request(list(range(5, 30)), SamplingParams(max_new_tokens=8, ignore_eos=True)) for _ in range(4)]
+    while eng.has_unfinished():
+        eng.step()
+    assert all(len(eng.pop_output(r).token_ids) == 8 for r in r2)
+    assert any(not k[2] for k in eng._graphs)
+
+
 def test_bert_encoder_bge_base_matches_hf_bertmodel(tmp_path):
     """BertEncoder at the bge-base shape on the native kernels (bf16) vs the HF ``BertModel`` the
     reference embedder runs (/root/reference/assistant/ai/embedders/transformers.py:18-25: fp32,
