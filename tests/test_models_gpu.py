@@ -195,11 +195,131 @@ def test_engine_json_mode_on_gpu_graphs():
     assert any(not k[2] for k in eng._graphs)
 
 
-def test_bert_encoder_bge_base_matches_hf_bertmodel(tmp_path):
-    """BertEncoder at the bge-base shape on the native kernels (bf16) vs the HF ``BertModel`` the
-    reference embedder runs (/root/reference/assistant/ai/embedders/transformers.py:18-25: fp32,
-    one text at a time, mean over all tokens) and vs this repo's fp32 CPU reference path, on
-    variable-length sequences up to 512 tokens: pooled cosine >= 0.999."""
+def _ref_llama3(cfg, w, seqs):
+    """Independent fp32 Llama-3 forward (plain PyTorch, HF conventions: rotate-half RoPE with the
+    Llama-3 frequency scaling, GQA causal attention, SwiGLU over stacked [gate; up] rows) of each
+    sequence -> final hidden states [sum len, H]."""
+    H, D, Hq, Hkv = cfg.hidden, cfg.head_dim, cfg.heads, cfg.kv_heads
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, D, 2, device=DEV, dtype=torch.float64) / D))
+    sc = cfg.rope_scaling
+    if sc:
+        lo_wl = sc["original_max_position_embeddings"] / sc["low_freq_factor"]
+        hi_wl = sc["original_max_position_embeddings"] / sc["high_freq_factor"]
+        wl = 2 * torch.pi / inv
+        smooth = (sc["original_max_position_embeddings"] / wl - sc["low_freq_factor"]) / (
+            sc["high_freq_factor"] - sc["low_freq_factor"])
+        scaled = torch.where(wl > lo_wl, inv / sc["factor"], inv)
+        inv = torch.where((wl >= hi_wl) & (wl <= lo_wl), (1 - smooth) * inv / sc["factor"] + smooth * inv, scaled)
+
+    def norm(x, g):
+        return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + cfg.eps) * g
+
+    def rope(x, pos):
+        f = (pos[:, None].double() * inv[None]).float()
+        cos, sin = torch.cat([f.cos(), f.cos()], -1)[:, None], torch.cat([f.sin(), f.sin()], -1)[:, None]
+        x1, x2 = x[..., :D // 2], x[..., D // 2:]
+        return x * cos + torch.cat([-x2, x1], -1) * sin
+
+    outs = []
+    for ids in seqs:
+        S = len(ids)
+        pos = torch.arange(S, device=DEV)
+        x = w["embed"][torch.tensor(ids, device=DEV)]
+        for i in range(cfg.layers):
+            h = norm(x, w[f"l{i}.attn_norm"])
+            qkv = h @ w[f"l{i}.qkv_w"].t()
+            q = rope(qkv[:, :Hq * D].view(S, Hq, D), pos)
+            k = rope(qkv[:, Hq * D:(Hq + Hkv) * D].view(S, Hkv, D), pos)
+            v = qkv[:, (Hq + Hkv) * D:].view(S, Hkv, D)
+            k, v = k.repeat_interleave(Hq // Hkv, 1), v.repeat_interleave(Hq // Hkv, 1)
+            a = torch.nn.functional.scaled_dot_product_attention(q.transpose(0, 1), k.transpose(0, 1),
+                                                                 v.transpose(0, 1), is_causal=True)
+            x = x + a.transpose(0, 1).reshape(S, Hq * D) @ w[f"l{i}.o_w"].t()
+            h = norm(x, w[f"l{i}.mlp_norm"])
+            gu = h @ w[f"l{i}.gate_up_w"].t()
+            F_ = gu.shape[1] // 2
+            x = x + (torch.nn.functional.silu(gu[:, :F_]) * gu[:, F_:]) @ w[f"l{i}.down_w"].t()
+        outs.append(norm(x, w["final_norm"]))
+    return torch.cat(outs)
+
+
+def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32():
+    """Two decoder layers at full Llama-3-8B width (H 4096, 32 / 8 heads, D 128, F 14336, 128k
+    vocabulary, Llama-3 RoPE scaling) on the production kernels, vs an independent fp32 PyTorch
+    forward of the same bf16-rounded weights:
+      * one packed prefill of 128 sequences, 8.3k tokens (gemm256 over fragment-layout weights with
+        the residual / SwiGLU8 epilogues, RoPE-on-load flash attention, 8-row-group MLP);
+      * one decode step at B = 128 (stream_gemm split-K slabs incl. down at K = 14336, fused
+        RoPE + KV write in the paged decode attention, streamed LM head)."""
+    from django_assistant_bot_amd.models.weights import _gate_up
+
+    cfg = decoder_config("llama-3-8b", layers=2)
+    w32 = random_decoder_weights(cfg, device=DEV, dtype=torch.float32, seed=3)
+    w32 = {k: v.bfloat16().float() for k, v in w32.items()}
+    gen = torch.Generator().manual_seed(0)
+    lens = [2100] + torch.randint(20, 110, (127,), generator=gen).tolist()
+    seqs = [torch.randint(0, 128000, (n + 1,), generator=gen).tolist() for n in lens]  # +1: the decode token
+    wm = {}
+    for k, v in w32.items():
+        if k.endswith("gate_up_w"):
+            F_ = v.shape[0] // 2
+            v = _gate_up(v[:F_], v[F_:], True)
+        wm[k] = v.to(torch.bfloat16)
+    model = LlamaModel(cfg, wm, DEV, interleaved_mlp=True)
+    assert model.frag
+    del wm
+    bs = 64
+    nblk = [-(-(n + 1) // bs) for n in lens]
+    kv = KVCache(cfg.layers, sum(nblk), cfg.kv_heads, bs, cfg.head_dim, DEV)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    bt = torch.zeros((128, max(nblk)), **i32)
+    o = 0
+    for b, nb in enumerate(nblk):
+        bt[b, :nb] = torch.arange(o, o + nb, **i32)
+        o += nb
+    T = sum(lens)
+    assert T >= 8192
+    pos = torch.cat([torch.arange(n, **i32) for n in lens])
+    slots = torch.cat([(bt[b, torch.arange(n, device=DEV) // bs].long() * bs + torch.arange(n, device=DEV) % bs)
+                       for b, n in enumerate(lens)])
+    cu = torch.tensor([0] + torch.tensor(lens).cumsum(0).tolist(), **i32)
+    ids = torch.tensor([t for s_, n in zip(seqs, lens) for t in s_[:n]], **i32)
+    meta = AttnMeta(decode=False, positions=pos, slots=slots, block_tables=bt, ctx_lens=torch.tensor(lens, **i32),
+                    cu_q=cu, max_q=max(lens))
+    h_pre = model.forward(ids, meta, kv)
+    dpos = torch.tensor(lens, **i32)
+    dslots = bt[torch.arange(128, device=DEV), dpos.long() // bs].long() * bs + dpos.long() % bs
+    ws = ops.DecodeWorkspace(128, cfg.heads, cfg.head_dim, -(-max(lens) // 512) + 1, DEV)
+    dmeta = AttnMeta(decode=True, positions=dpos, slots=dslots, block_tables=bt, ctx_lens=dpos + 1, workspace=ws,
+                     part_size=2048, order=torch.argsort(-dpos).to(torch.int32))
+    h_dec = model.forward(torch.tensor([s_[-1] for s_ in seqs], **i32), dmeta, kv)
+    lg_dec = model.logits(h_dec)
+    torch.cuda.synchronize()
+    ref_h = _ref_llama3(cfg, w32, seqs)
+    last = torch.tensor(lens, device=DEV).cumsum(0) + torch.arange(128, device=DEV)  # decode rows of the ref
+    ref_lg = ref_h[last] @ w32["lm_head"].t()
+    keep = torch.ones(ref_h.shape[0], dtype=torch.bool, device=DEV)
+    keep[last] = False
+
+    def check(got, want, what, cos_min, rel_max):
+        got = got.float()
+        cos = torch.nn.functional.cosine_similarity(got, want, dim=-1)
+        rel = ((got - want).abs().max() / want.abs().max()).item()
+        print(f"{what}: min cos {cos.min().item():.5f}, max rel err {rel:.4f}")
+        assert cos.min().item() >= cos_min and rel <= rel_max, (what, cos.min().item(), rel)
+
+    check(h_pre, ref_h[keep], "prefill hidden", 0.999, 0.05)
+    check(h_dec, ref_h[last], "decode hidden", 0.999, 0.05)
+    check(lg_dec, ref_lg, "decode logits", 0.999, 0.05)
+
+
+@pytest.mark.parametrize("name,layers", [("bge-base-en", None), ("bge-large-en", 2)])
+def test_bert_encoder_matches_hf_bertmodel(tmp_path, name, layers):
+    """BertEncoder at the bge-base shape (all 12 layers) and at bge-large width (2 of 24 layers,
+    H 1024, 16 heads, F 4096) on the native kernels (bf16) vs the HF ``BertModel`` the reference
+    embedder runs (/root/reference/assistant/ai/embedders/transformers.py:18-25: fp32, one text at a
+    time, mean over all tokens) and vs this repo's fp32 CPU reference path, on variable-length
+    sequences up to 512 tokens: pooled cosine >= 0.999."""
     transformers = pytest.importorskip("transformers")
     from safetensors.torch import save_file
 
@@ -207,7 +327,7 @@ def test_bert_encoder_bge_base_matches_hf_bertmodel(tmp_path):
     from django_assistant_bot_amd.models.configs import encoder_config
     from django_assistant_bot_amd.models.weights import load_encoder_checkpoint
 
-    cfg = encoder_config("bge-base-en")
+    cfg = encoder_config(name, **({"layers": layers} if layers else {}))
     hc = transformers.BertConfig(vocab_size=cfg.vocab_size, hidden_size=cfg.hidden, num_hidden_layers=cfg.layers,
                                  num_attention_heads=cfg.heads, intermediate_size=cfg.intermediate,
                                  max_position_embeddings=cfg.max_position, type_vocab_size=cfg.type_vocab,
