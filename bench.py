@@ -21,9 +21,9 @@ Two load shapes (``--mode``):
     The index is replicated per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
   * ``batch`` (default) -- one step = a batch of C questions answered together (retrieve all,
     prefill all, decode all); the index is sharded across the ranks (queries all-gathered, partial top-k routed back with all_to_all).
-    Measured at C=128 on one MI355X: batch 32.5 q/s p50 3.9 s; serve 30.3 q/s p50 4.2 s (mixed
-    2048) -- large-M prefill GEMMs run at ~1.6 PFLOP/s, so mixing decode rows into smaller prefill
-    chunks costs more than it saves (profiles/serving_mixed_steps.md).
+    Measured at C=128 on one MI355X (round 3): batch 37.1 q/s, p50 3.44 s.  Serve mode is slower
+    (profiles/serving_mixed_steps.md): the native prefill GEMMs run at ~1.5 PFLOP/s only at large M,
+    so mixing decode rows into smaller prefill chunks costs more than it saves.
 
 Weights are random-init with the real architectures; corpus / questions are synthetic: each
 question has planted "paraphrase" rows near its embedding in 3-5 target documents so retrieval

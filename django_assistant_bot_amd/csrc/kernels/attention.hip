@@ -1208,39 +1208,27 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  // Long D=128 sequences (Llama prefill): 128-query blocks of 8 waves x 16 queries halve the K/V
-  // tile traffic per query (16x1024 causal: 298 -> 355 TFLOP/s).  DAB_FLASH_VARIANT selects for
-  // A/B runs (benchmarks/kernel_bench.py attn): w4 = 64-query blocks everywhere, qt2 = 4 waves x 2
-  // sub-tiles of 16 (halves LDS reads per MFMA; 196 TFLOP/s at 1 wave/SIMD, 340-350 since it is
-  // held to 2 waves/SIMD -- still not above the default, so LDS reads are not the bound), w8 = 8 waves
-  // also for D <= 64 (the encoder is 5 % slower that way).
-  static const int variant = [] {
-    const char* v = getenv("DAB_FLASH_VARIANT");
-    if (v == nullptr) return -1;
-    return (v[0] == 'w' && v[1] == '8') ? 1 : (v[0] == 'w' && v[1] == '4') ? 2 : (v[0] == 'q') ? 0 : -1;
-  }();
-  // Llama prefill (D = 128 over the paged cache): the 32x32 kernel; DAB_FLASH_VARIANT=w8 (or any
-  // explicit variant) keeps the 16x16 kernels for A/B runs
-  if (D == 128 && paged && variant < 0 && block_size % 64 == 0) {
+  // Llama prefill (D = 128 over the paged cache): the 32x32 kernel below
+  if (D == 128 && paged && block_size % 64 == 0) {
     dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
     if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
     else hipLaunchKernelGGL((flash_d128_kernel<false>), g32, dim3(256), 0, s, prm);
     return hipGetLastError();
   }
   if (rope_cs) return hipErrorInvalidValue;  // Q RoPE lives only in the D = 128 paged kernel above
-  const int var = variant >= 0 ? variant : (D == 128 ? 1 : 2);
-  const bool wide = max_seqlen_q > 64 && var != 2;
+  // Long D = 128 sequences: 128-query blocks of 8 waves x 16 queries halve the K/V tile traffic per
+  // query (16x1024 causal: 298 -> 355 TFLOP/s); the encoder (D <= 64) runs 64-query blocks of 4
+  // waves (8 waves measured 5 % slower there; a 4-wave x 2-sub-tile form was no faster either)
+  const bool wide = D == 128 && max_seqlen_q > 64;
   const int qb = wide ? 128 : 64;
   dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
-#define DAB_FLASH(DD, C, P)                                                                \
-  do {                                                                                    \
-    if (wide && var == 1)                                                                 \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD >= 64 ? 8 : 4), (DD >= 64 ? 1 : 2)>), grid, \
-                         dim3(DD >= 64 ? 512 : 256), 0, s, prm);                          \
-    else if (wide)                                                                        \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 2>), grid, dim3(256), 0, s, prm); \
-    else                                                                                  \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1>), grid, dim3(256), 0, s, prm); \
+#define DAB_FLASH(DD, C, P)                                                                          \
+  do {                                                                                              \
+    if (wide)                                                                                       \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD == 128 ? 8 : 4), 1>), grid,              \
+                         dim3(DD == 128 ? 512 : 256), 0, s, prm);                                   \
+    else                                                                                            \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1>), grid, dim3(256), 0, s, prm);           \
   } while (0)
 #define DAB_FLASH_D(DD)                    \
   if (paged) {                             \

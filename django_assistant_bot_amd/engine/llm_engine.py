@@ -462,7 +462,7 @@ class LLMEngine:
         P = len(chunks)
         Tp = sum(n for _, _, n in chunks)
         # pad the decode rows (slot -1, one key of block 0, output ignored) so the GEMM M is a
-        # multiple of 64: fewer distinct shapes for the vendor GEMM heuristics, full MFMA tiles
+        # multiple of 64: full MFMA tiles in the prefill GEMMs
         Bp = B + (-(Tp + B)) % 64 if self.is_gpu else B
         Bp = min(Bp, self.max_batch)
         T = Tp + Bp

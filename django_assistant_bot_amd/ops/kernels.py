@@ -8,8 +8,6 @@ from __future__ import annotations
 
 import math
 
-import os
-
 import torch
 import torch.nn.functional as F
 
@@ -232,7 +230,7 @@ def flash_attention_packed(q, k, v, cu_q, cu_k, max_seqlen_q, causal=False, scal
 
 def flash_rope_ok(D: int, block_size: int) -> bool:
     """Whether flash_attention_paged can rotate q itself (the 32x32 D = 128 kernel's Q prologue)."""
-    return D == 128 and block_size % 64 == 0 and not os.environ.get("DAB_FLASH_VARIANT")
+    return D == 128 and block_size % 64 == 0
 
 
 def flash_attention_paged(q, k_cache, v_cache, block_tables, cu_q, ctx_lens, max_seqlen_q, causal=True, scale=None,

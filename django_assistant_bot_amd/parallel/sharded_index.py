@@ -25,6 +25,8 @@ from ..engine.vector_index import VectorIndex
 
 
 class ShardedIndex:
+    SMALL_Q = 16  # queries per rank that travel in the search's first (fixed-size) all_gather
+
     def __init__(self, dim: int, device=None, group=None, capacity: int = 4096, dtype=torch.bfloat16):
         self.group = group
         self.distributed = dist.is_available() and dist.is_initialized()
@@ -160,31 +162,49 @@ class ShardedIndex:
             return self.local.search(q, k, q_groups)
         cdev = self._comm_device()
         nq = q.shape[0]
-        meta = torch.tensor([nq, int(self._wide())], dtype=torch.int64, device=cdev)
-        metas = [torch.zeros_like(meta) for _ in range(self.world)]
-        dist.all_gather(metas, meta, group=self.group)
-        counts = [int(m[0]) for m in metas]
-        wide = any(int(m[1]) for m in metas)
+        D = self.dim
+        # 1. one all_gather of a fixed-size block: a header row (query count, wide-id flag) and up to
+        #    SMALL_Q queries with their group in the last column.  Single-query searches (the app's
+        #    per-message retrieval) thus cost two collectives (this + the all_to_all), not three;
+        #    only a batch beyond SMALL_Q on some rank adds an all_gather of the remaining rows.
+        S = self.SMALL_Q
+        blk = torch.zeros((S + 1, D + 1), dtype=torch.float32, device=cdev)
+        blk[0, 0] = float(nq)
+        blk[0, 1] = float(self._wide())
+        head = min(nq, S)
+        grp = (torch.as_tensor(q_groups, dtype=torch.float32).to(cdev) if q_groups is not None
+               else torch.full((nq,), -1.0, device=cdev))
+        blk[1:1 + head, :D] = q[:head].to(cdev)
+        blk[1:1 + head, D] = grp[:head]
+        blks = [torch.empty_like(blk) for _ in range(self.world)]
+        dist.all_gather(blks, blk, group=self.group)
+        self.stats["collectives"] = 1
+        hdr = torch.stack([b[0, :2] for b in blks]).cpu()  # the one host read of the call
+        counts = [int(c) for c in hdr[:, 0].tolist()]
+        wide = bool(hdr[:, 1].max().item())
         mx = max(counts)
         if mx == 0:
             z = torch.full((0, k), -1, dtype=torch.int64, device=self.device)
             return torch.full((0, k), float("-inf"), device=self.device), z, z.clone()
-        # 1. queries (+ their group in the last column), padded to the largest batch for all_gather
-        qpad = torch.zeros((mx, self.dim + 1), dtype=torch.float32, device=cdev)
-        qpad[:nq, : self.dim] = q.to(cdev)
-        qpad[:, self.dim] = -1.0
-        if q_groups is not None:
-            qpad[:nq, self.dim] = torch.as_tensor(q_groups, dtype=torch.float32).to(cdev)
-        allq = [torch.empty_like(qpad) for _ in range(self.world)]
-        dist.all_gather(allq, qpad, group=self.group)
-        allq = torch.cat([a[:c] for a, c in zip(allq, counts)], 0).to(self.device)  # real rows only
+        parts = [b[1:1 + min(c, S)] for b, c in zip(blks, counts)]
+        if mx > S:  # rows past SMALL_Q, padded to the largest remainder
+            rest = torch.zeros((mx - S, D + 1), dtype=torch.float32, device=cdev)
+            if nq > S:
+                rest[:nq - S, :D] = q[S:].to(cdev)
+                rest[:nq - S, D] = grp[S:]
+            rests = [torch.empty_like(rest) for _ in range(self.world)]
+            dist.all_gather(rests, rest, group=self.group)
+            self.stats["collectives"] += 1
+            parts = [torch.cat([p, r[:max(c - S, 0)]], 0) for p, r, c in zip(parts, rests, counts)]
+        allq = torch.cat(parts, 0).to(self.device)  # real rows only, rank order
         # 2. local partial top-k for every query of the node
-        sims, ids, docs = self.local.search(allq[:, : self.dim], k, allq[:, self.dim].to(torch.int32))
+        sims, ids, docs = self.local.search(allq[:, :D], k, allq[:, D].to(torch.int32))
         packed = self._pack(sims, ids, docs, k, wide).to(cdev)  # [sum(counts), k, 3]
         # 3. route each rank's partials to that rank
         recv = torch.empty((self.world * nq, k, 3), dtype=packed.dtype, device=cdev)
         dist.all_to_all_single(recv, packed, output_split_sizes=[nq] * self.world, input_split_sizes=counts,
                                group=self.group)
+        self.stats["collectives"] += 1
         self.stats["merge_bytes_recv"] = recv.numel() * recv.element_size()
         # 4. merge [nq, W*k] candidates
         cand = recv.view(self.world, nq, k, 3).permute(1, 0, 2, 3).reshape(nq, self.world * k, 3)

@@ -137,6 +137,24 @@ def _index_merge_body(info, out_path):
         res["own_equal"] = bool(torch.equal(got_ids, eids) and torch.equal(got_docs, edocs))
         res["own_err"] = float((sims - es).nan_to_num(0.0).abs().max())
     res["bytes"] = idx.stats["merge_bytes_recv"]
+    res["coll_small"] = idx.stats["collectives"]
+    # a batch past SMALL_Q on one rank: the remaining rows travel in one extra all_gather
+    nq2 = 40 if info.rank == 0 else 1
+    q2 = torch.randn(nq2, dim, generator=torch.Generator().manual_seed(170 + info.rank))
+    s2, i2, d2 = idx.search(q2, k)
+    e2, ei2, ed2 = single.search(q2, k)
+    res["big_equal"] = bool(torch.equal(i2, ei2) and torch.equal(d2, ed2))
+    res["coll_big"] = idx.stats["collectives"]
+    # single-query latency (the app's per-message retrieval)
+    import time
+
+    q1 = torch.randn(1, dim, generator=torch.Generator().manual_seed(7))
+    idx.search(q1, k)
+    torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        idx.search(q1, k)
+    res["single_ms"] = (time.perf_counter() - t0) / 20 * 1e3
     # serving path: the same batch on every rank, filters resolved per shard
     qs = torch.randn(3, dim, generator=torch.Generator().manual_seed(99))
     allowed = [ids[::2].tolist(), ids[:300].tolist(), ids.tolist()]
@@ -162,6 +180,9 @@ def test_sharded_index_all_to_all_merge(tmp_path, world):
             assert res["own_equal"] and res["own_err"] < 1e-5
         # each rank receives only the partials of its own queries: W x nq x k x 12 B
         assert res["bytes"] == world * res["nq"] * k * 12
+        assert res["coll_small"] == 2 and res["coll_big"] == 3 and res["big_equal"]
+        if r == 0:
+            print(f"W={world}: single-query sharded search {res['single_ms']:.2f} ms (gloo, CPU)")
         if r == 0:
             assert res["rep_equal"] and res["rep_err"] < 1e-5
         else:
