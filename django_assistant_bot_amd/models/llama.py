@@ -73,7 +73,12 @@ class KVCache:
         return 2 * layers * kv_heads * block_size * head_dim * torch.finfo(dtype).bits // 8
 
 
-_FUSED_DECODE_ROPE = os.environ.get("DAB_DECODE_ROPE_FUSED", "1") != "0"  # profiling A/B switch
+# Decode RoPE + KV write inside the paged attention launch (``ops.paged_decode_rope``) instead of
+# its own kernel: numerically identical (tests/test_kernels_gpu.py::test_paged_decode_rope_fused)
+# and 1-6 us per layer faster under rocprof, but 0.18 ms per 32-layer step SLOWER in the un-profiled
+# bench (7.75 vs 7.56 ms, same box, profiles/round3_layout_and_parity.md): off by default, kept as
+# an A/B switch (DAB_DECODE_ROPE_FUSED=1).
+_FUSED_DECODE_ROPE = os.environ.get("DAB_DECODE_ROPE_FUSED", "0") == "1"
 
 
 class LlamaModel:
