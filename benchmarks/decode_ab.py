@@ -1,0 +1,108 @@
+"""Interleaved A/B of decode-step variants inside ONE engine (un-profiled wall time per step).
+
+rocprof serialises kernels and shifts the clock, so small decode changes can rank differently
+under it than in the bench (profiles/round3_layout_and_parity.md: a fused prologue that won under
+rocprof lost 0.18 ms per step without it).  This harness builds the bench's decode state once
+(Llama-3-8B, 128 sequences of ~1.1k-token prompts, pipelined HIP-graph decode), then times each
+arm for ``--steps`` decode steps, arms interleaved over ``--rounds`` rounds, with graphs
+re-captured per arm and every arm starting from the same contexts (prefix-cache re-admission).  An arm sets per-projection (stream_gemm cfg, K-slices) overrides and/or the
+decode attention partition.
+
+    python benchmarks/decode_ab.py --arms base,qkv21,o4 --rounds 3 --steps 40
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+ARMS = {
+    "base": {},
+    "qkv21": {"qkv": (21, 4)},
+    "qkv23": {"qkv": (23, 4)},
+    "qkv14": {"qkv": (14, 4)},
+    "qkv2": {"qkv": (10, 2)},
+    "o4": {"o": (10, 4)},
+    "o16": {"o": (10, 16)},
+    "o14": {"o": (14, 8)},
+    "down4": {"down": (10, 4)},
+    "down14": {"down": (14, 8)},
+    "down15": {"down": (15, 8)},
+    "gu22": {"gate_up": (22, 1)},
+    "gu10": {"gate_up": (10, 1)},
+    "lm29": {"lm_head": (29, 1)},
+    "lm10": {"lm_head": (10, 1)},
+    "gu14": {"gate_up": (14, 1)},
+    "gu15": {"gate_up": (15, 1)},
+    "qkv15": {"qkv": (15, 4)},
+    "o15": {"o": (15, 8)},
+    "rope": {"_rope": True},
+    "part1024": {"_part": 1024},
+    "part512": {"_part": 512},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--arms", default="base,qkv21,o4,down14")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--prompt", type=int, default=1100)
+    args = ap.parse_args()
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+    from django_assistant_bot_amd.models import llama as llama_mod
+
+    torch.manual_seed(0)
+    eng = LLMEngine("llama-3-8b", device="cuda", max_batch=args.batch, kv_cache_gb=120, max_prefill_tokens=32768)
+    g = torch.Generator().manual_seed(1)
+    sp = SamplingParams(max_new_tokens=6000, ignore_eos=True)
+    prompts = [torch.randint(0, 128000, (args.prompt + int(torch.randint(-100, 100, (1,), generator=g)),),
+                             generator=g).tolist() for _ in range(args.batch)]
+
+    def restart():
+        """Every arm decodes from the same contexts: drop the batch and re-admit the same prompts
+        (their blocks come back from the prefix cache, so only the last partial block re-runs)."""
+        eng._finish_inflight()
+        for r in [r.rid for r in list(eng.running) + list(eng.prefilling) + list(eng.waiting)]:
+            eng.abort(r)
+        eng.finished.clear()
+        for p in prompts:
+            eng.add_request(p, sp)
+        while eng.waiting or eng.prefilling or eng._pending_prefill is not None:
+            eng.step()
+
+    base_part = eng.long_part_size
+    arms = args.arms.split(",")
+    res = {a: [] for a in arms}
+    for r in range(args.rounds):
+        for a in arms:
+            spec = dict(ARMS[a])
+            restart()
+            eng.model.stream_overrides = {k: v for k, v in spec.items() if not k.startswith("_")}
+            eng.long_part_size = spec.get("_part", base_part)
+            llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
+            eng._graphs.clear()
+            for _ in range(4):
+                eng.step()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                eng.step()
+            eng._finish_inflight()
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) / args.steps * 1e3
+            res[a].append(round(ms, 4))
+            print(json.dumps({"round": r, "arm": a, "ms_per_step": round(ms, 4)}), flush=True)
+    base = sorted(res[arms[0]])[len(res[arms[0]]) // 2]
+    for a in arms:
+        med = sorted(res[a])[len(res[a]) // 2]
+        print(json.dumps({"arm": a, "median_ms": med, "vs_first": round(med / base, 4), "all": res[a]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -114,6 +114,7 @@ class LlamaModel:
             torch.cuda.empty_cache()
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
+        self.stream_overrides: dict = {}  # projection name -> (stream_gemm cfg, K-slices): tuning runs only
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -185,10 +186,13 @@ class LlamaModel:
             return ops.linear(x, w)
         if dec and self.frag:
             cfg = self._stream_cfg(name, x.shape[0], w.shape[0])
+            s = None
+            if name in self.stream_overrides:  # (cfg, splits) of a tuning run (benchmarks/decode_ab.py)
+                cfg, s = self.stream_overrides[name]
             if cfg >= 0 and w.shape[1] % 128 == 0:
                 if epilogue != ops.EPI_NONE:
                     return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg)
-                s = self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
+                s = s or self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
                 out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True)
                 return ops.slab_reduce(out) if (s > 1 and not allow_slabs) else out
         return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag)
