@@ -5,7 +5,7 @@ import logging
 from typing import List
 
 from assistant.ai.domain import AIResponse, Message
-from assistant.ai.providers.base import AIProvider
+from assistant.ai.providers.base import AIProvider, accepts_json_schema
 from assistant.ai.services.ai_service import get_ai_provider
 
 logger = logging.getLogger(__name__)
@@ -37,5 +37,7 @@ class AIDialog(AIProvider):
         return self._provider.calculate_tokens(text)
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
-        return await self._provider.get_response(messages, max_tokens, json_format)
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
+        if json_schema is None or not accepts_json_schema(self._provider.get_response):
+            return await self._provider.get_response(messages, max_tokens, json_format or json_schema is not None)
+        return await self._provider.get_response(messages, max_tokens, json_format, json_schema=json_schema)

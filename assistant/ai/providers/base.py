@@ -8,6 +8,18 @@ from assistant.ai.domain import AIResponse, Message
 from assistant.utils.debug import TimeDebugger
 
 
+def accepts_json_schema(fn) -> bool:
+    """Whether a ``get_response`` takes the ``json_schema`` keyword (custom providers written for the
+    reference's ``(messages, max_tokens, json_format)`` signature do not)."""
+    import inspect
+
+    try:
+        params = inspect.signature(fn).parameters
+    except (TypeError, ValueError):
+        return False
+    return "json_schema" in params or any(p.kind == p.VAR_KEYWORD for p in params.values())
+
+
 class AIProvider(ABC):
     #: per-call attempt counts, recorded when a debugger asks for them (None = not recording)
     calls_attempts: Optional[List[int]] = None
@@ -23,8 +35,11 @@ class AIProvider(ABC):
 
     @abstractmethod
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
-        """Chat completion for ``messages``."""
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
+        """Chat completion for ``messages``.  ``json_schema`` (an extension of the reference API):
+        a JSON Schema the answer must follow; providers that can enforce it do (the MI355X engine
+        by constrained decoding, OpenAI / Ollama by their structured-output options), the others
+        treat it as ``json_format``."""
 
     def _record_attempts(self, n: int) -> None:
         if self.calls_attempts is not None:

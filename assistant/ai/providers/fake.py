@@ -57,9 +57,10 @@ class FakeAIProvider(AIProvider):
         return len(text.split()) // 2
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         FakeAIProvider.requests.append({"messages": list(messages), "max_tokens": max_tokens,
-                                        "json_format": json_format})
+                                        "json_format": json_format, "json_schema": json_schema})
+        json_format = json_format or json_schema is not None
         if self._script:
             r = self._script.popleft()
             result = r(messages) if callable(r) else r

@@ -24,9 +24,11 @@ class GPUServiceProvider(AIProvider):
         return len(text.split()) // 2
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         payload = {"model": self._model, "messages": [dict(m) for m in messages], "max_tokens": max_tokens,
-                   "json_format": json_format}
+                   "json_format": json_format or json_schema is not None}
+        if json_schema is not None:
+            payload["json_schema"] = json_schema
         try:
             data = await post_json(f"{self._base_url}/dialog/", payload)
         except HTTPError as exc:

@@ -23,7 +23,8 @@ class GroqAIProvider(ChatGPTAIProvider):
             self.calls_attempts = []
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
+        json_format = json_format or json_schema is not None
         converted = [self.convert_message(m) for m in messages]
         if any(isinstance(m["content"], list) for m in converted):
             converted = [m for m in converted if m["role"] != "system"]  # vision models reject system turns

@@ -50,11 +50,14 @@ class OllamaAIProvider(AIProvider):
         return None
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         self._check_roles(messages)
         body = {"model": self._model, "messages": [dict(m) for m in messages], "stream": False,
                 "options": {"num_predict": max_tokens}}
-        if json_format:
+        if json_schema is not None:
+            body["format"] = json_schema  # Ollama structured outputs
+            json_format = True
+        elif json_format:
             body["format"] = "json"
         t0 = time.time()
         for attempt in range(1, 6):

@@ -26,10 +26,13 @@ class ChatGPTAIProvider(AIProvider):
     def calculate_tokens(self, text: str) -> int:
         return len(text.split()) // 2
 
-    def _payload(self, messages, max_tokens, json_format):
+    def _payload(self, messages, max_tokens, json_format, json_schema=None):
         body = {"model": self._model, "messages": [self.convert_message(m) for m in messages],
                 "max_tokens": max_tokens}
-        if json_format:
+        if json_schema is not None:
+            body["response_format"] = {"type": "json_schema",
+                                       "json_schema": {"name": "response", "schema": json_schema}}
+        elif json_format:
             body["response_format"] = {"type": "json_object"}
         return body
 
@@ -47,9 +50,10 @@ class ChatGPTAIProvider(AIProvider):
                                headers={"Authorization": f"Bearer {self._api_key}"})
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         t0 = time.time()
-        data = await self._call(self._payload(messages, max_tokens, json_format))
+        json_format = json_format or json_schema is not None
+        data = await self._call(self._payload(messages, max_tokens, json_format, json_schema))
         logger.debug("raw completion (%.2f s): %s", time.time() - t0, data)
         choice = data["choices"][0]
         content = choice["message"].get("content") or ""

@@ -40,7 +40,7 @@ class TransformersProvider(AIProvider):
         return self._tokenizer.count_tokens(text)
 
     async def get_response(self, messages: List[Message], max_tokens: int = 1024,
-                           json_format: bool = False) -> AIResponse:
+                           json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         from django_assistant_bot_amd.engine.llm_engine import SamplingParams
 
         prompt = render_prompt(messages)
@@ -48,7 +48,8 @@ class TransformersProvider(AIProvider):
         # JSON mode constrains the sampler to one JSON object (engine/json_constraint.py): valid in
         # one generation where the reference retries until json.loads succeeds
         params = SamplingParams(max_new_tokens=max_tokens, temperature=1.0, top_k=50, top_p=0.95,
-                                json_mode=bool(json_format))
+                                json_mode=bool(json_format), json_schema=json_schema)
+        json_format = json_format or json_schema is not None
         out = await self._worker.generate(ids, params)
         text = out.text.strip()
         result = text

@@ -1,6 +1,7 @@
 """Known-question matching with the fast model (reference steps/choose_known_question.py:9-61)."""
 from __future__ import annotations
 
+from assistant.ai.providers.base import accepts_json_schema
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
 from assistant.bot.services.context_service.utils import add_system_message, get_numerical_list_str
 from assistant.bot.services.schema_service import json_prompt
@@ -25,6 +26,13 @@ class ChooseKnownQuestionStep(ContextProcessingStep):
         )
 
     @staticmethod
+    def schema(n_questions: int) -> dict:
+        """The answer the condition below accepts: the number of a listed question, or null."""
+        return {"type": "object", "properties": {"question": {"anyOf": [
+            {"type": "integer", "minimum": 1, "maximum": max(1, n_questions)}, {"type": "null"}]}},
+            "required": ["question"]}
+
+    @staticmethod
     def _condition(resp) -> bool:
         return isinstance(resp.result, dict) and "question" in resp.result and (
             resp.result["question"] is None or isinstance(resp.result["question"], int))
@@ -36,8 +44,10 @@ class ChooseKnownQuestionStep(ContextProcessingStep):
             self._debug_info["the_same_question"] = None
             return
         messages = add_system_message([], self.prompt(self._state.user_question, [q.text for q in questions]))
+        kw = ({"json_schema": self.schema(len(questions))} if accepts_json_schema(self._fast_ai.get_response)
+              else {})
         response = await repeat_until(self._fast_ai.get_response, messages, json_format=True,
-                                      condition=self._condition)
+                                      condition=self._condition, **kw)
         n = response.result["question"]
         if n and 1 <= n <= len(questions):
             q = questions[n - 1]

@@ -1,6 +1,7 @@
 """Topic classification with the fast model (reference steps/classify.py:13-97)."""
 from __future__ import annotations
 
+from assistant.ai.providers.base import accepts_json_schema
 from assistant.bot.services.context_service.steps.base import ContextProcessingStep, ai_debugger
 from assistant.bot.services.context_service.utils import add_system_message, get_list_str
 from assistant.bot.services.schema_service import json_prompt
@@ -26,8 +27,11 @@ class ClassifyStep(ContextProcessingStep):
         topics = [SMALL_TALK] + [t.title for t in roots]
         examples = self._offtopic_examples + [(q, t.title) for t in roots for q in t.examples]
         messages = add_system_message(self._state.messages, self.prompt(topics, examples, self._state.user_question))
+        # providers that enforce JSON Schemas (the MI355X engine: constrained decoding) answer with
+        # one of the topic titles in one generation; the others keep the reference's retry loop
+        kw = {"json_schema": self.schema(topics)} if accepts_json_schema(self._fast_ai.get_response) else {}
         response = await repeat_until(self._fast_ai.get_response, messages, max_tokens=256, json_format=True,
-                                      condition=self._condition)
+                                      condition=self._condition, **kw)
         topic = response.result["topic"]
         self._logger.info("classified question as %s", topic)
         best = extract_bests(topic, topics, limit=1)
@@ -38,6 +42,11 @@ class ClassifyStep(ContextProcessingStep):
         chosen = roots[topics.index(best_title) - 1]
         self._debug_info["topic"] = chosen.title
         self._state.topic = chosen
+
+    @staticmethod
+    def schema(topics) -> dict:
+        return {"type": "object", "properties": {"topic": {"type": "string", "enum": list(topics)}},
+                "required": ["topic"]}
 
     @staticmethod
     def prompt(topics, examples, user_question) -> str:

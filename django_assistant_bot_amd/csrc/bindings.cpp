@@ -305,6 +305,32 @@ PYBIND11_MODULE(_native, m) {
       .def("completion", [](const dab::JsonMatcher& j) { return py::bytes(j.completion()); })
       .def("completion_len", &dab::JsonMatcher::completion_len)
       .def("text", [](const dab::JsonMatcher& j) { return py::bytes(j.text()); });
+  py::class_<dab::SchemaAutomaton, std::shared_ptr<dab::SchemaAutomaton>>(m, "SchemaAutomaton")
+      .def(py::init<std::shared_ptr<dab::JsonVocab>, int, int, const std::vector<int32_t>&,
+                    const std::vector<std::vector<int32_t>>&, const std::vector<std::vector<int32_t>>&>(),
+           py::arg("vocab"), py::arg("n_states"), py::arg("start"), py::arg("accept"), py::arg("edges"),
+           py::arg("eps"))
+      .def("dfa_states", &dab::SchemaAutomaton::dfa_states)
+      .def("accepts", [](dab::SchemaAutomaton& a, const py::bytes& b) {
+        int d = a.start();
+        for (unsigned char c : std::string(b)) {
+          d = a.step(d, c);
+          if (d < 0) return false;
+        }
+        return a.accepting(d);
+      });
+  py::class_<dab::SchemaMatcher>(m, "SchemaMatcher")
+      .def(py::init<std::shared_ptr<dab::SchemaAutomaton>>(), py::arg("automaton"))
+      .def("fill_mask",
+           [](dab::SchemaMatcher& j, int remaining, u out) {
+             py::gil_scoped_release rel;
+             return j.fill_mask(remaining, (uint32_t*)out);
+           })
+      .def("advance", &dab::SchemaMatcher::advance)
+      .def("done", &dab::SchemaMatcher::done)
+      .def("broken", &dab::SchemaMatcher::broken)
+      .def("completion_len", &dab::SchemaMatcher::completion_len)
+      .def("text", [](const dab::SchemaMatcher& j) { return py::bytes(j.text()); });
   m.def("json_accepts", [](const py::bytes& b, bool complete, int max_depth, int max_ws) {
     return dab::json_accepts(std::string(b), complete, max_depth, max_ws);
   }, py::arg("bytes"), py::arg("complete") = true, py::arg("max_depth") = 64, py::arg("max_ws") = 255);

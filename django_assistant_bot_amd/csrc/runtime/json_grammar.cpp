@@ -3,7 +3,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <deque>
 #include <limits>
+#include <stdexcept>
 
 namespace dab {
 
@@ -68,7 +70,7 @@ bool begin_value(JsonState& s, uint8_t c, int max_depth) {
   switch (c) {
     case '{': return push(s, true, max_depth);
     case '[': return push(s, false, max_depth);
-    case '"': s.mode = M_STR; s.key = 0; s.sub = 0; return true;
+    case '"': s.mode = M_STR; s.key = 0; s.sub = 0; s.lit = 0; return true;
     case '-': s.mode = M_NUM; s.sub = N_MINUS; return true;
     case '0': s.mode = M_NUM; s.sub = N_ZERO; return true;
     case 't': s.mode = M_LIT; s.lit = 0; s.sub = 1; return true;
@@ -97,6 +99,7 @@ bool json_step(JsonState& s, uint8_t c, int max_depth, int max_ws) {
         s.mode = M_STR;
         s.key = 1;
         s.sub = 0;
+        s.lit = 0;
         s.ws = 0;
         return true;
       }
@@ -138,6 +141,20 @@ bool json_step(JsonState& s, uint8_t c, int max_depth, int max_ws) {
     }
     case M_STR:
       if (s.sub == 0) {
+        // UTF-8 structure inside strings (byte-level tokens can split characters): `lit` counts
+        // the continuation bytes still owed by the last lead byte
+        if (s.lit) {
+          if (c < 0x80 || c > 0xBF) return false;
+          --s.lit;
+          return true;
+        }
+        if (c >= 0x80) {
+          if (c >= 0xC2 && c <= 0xDF) s.lit = 1;
+          else if (c >= 0xE0 && c <= 0xEF) s.lit = 2;
+          else if (c >= 0xF0 && c <= 0xF4) s.lit = 3;
+          else return false;
+          return true;
+        }
         if (c == '"') {
           if (s.key) {
             s.key = 0;
@@ -225,7 +242,7 @@ int json_completion_len(const JsonState& s) {
     case M_COLON: return 2 + d;    // :0
     case M_VALUE: return 1 + d;    // 0
     case M_STR: {
-      int n = (s.key ? 3 : 1) + d;
+      int n = (s.key ? 3 : 1) + d + s.lit;
       if (s.sub == 1) n += 1;
       else if (s.sub >= 2) n += 6 - s.sub;
       return n;
@@ -247,6 +264,7 @@ std::string json_completion(const JsonState& s) {
     case M_COLON: out = ":0"; break;
     case M_VALUE: out = "0"; break;
     case M_STR:
+      out.assign(s.lit, '\x80');
       if (s.sub == 1) out = "n";
       else if (s.sub >= 2) out.assign(6 - s.sub, '0');
       out += s.key ? "\":0" : "\"";
@@ -407,5 +425,192 @@ bool JsonMatcher::advance(int token) {
 int JsonMatcher::completion_len() const { return json_completion_len(state_); }
 
 std::string JsonMatcher::completion() const { return json_completion(state_); }
+
+// ---------------------------------------------------------------------------------------------
+SchemaAutomaton::SchemaAutomaton(std::shared_ptr<JsonVocab> vocab, int n_states, int start,
+                                 const std::vector<int32_t>& accept, const std::vector<std::vector<int32_t>>& edges,
+                                 const std::vector<std::vector<int32_t>>& eps)
+    : vocab_(std::move(vocab)), n_(n_states), tr_(n_states), eps_(n_states), nacc_(n_states, 0) {
+  for (const auto& e : edges) {
+    if (e.size() != 4 || e[0] < 0 || e[0] >= n_ || e[3] < 0 || e[3] >= n_ || e[1] < 0 || e[2] > 255 || e[1] > e[2])
+      throw std::invalid_argument("schema NFA: bad edge");
+    tr_[e[0]].emplace_back((uint32_t)e[1] | ((uint32_t)e[2] << 8), e[3]);
+  }
+  std::vector<std::vector<int32_t>> reps(n_);  // reverse epsilon edges
+  std::vector<std::vector<int32_t>> rtr(n_);   // reverse byte edges
+  for (const auto& e : eps) {
+    if (e.size() != 2 || e[0] < 0 || e[0] >= n_ || e[1] < 0 || e[1] >= n_)
+      throw std::invalid_argument("schema NFA: bad epsilon edge");
+    eps_[e[0]].push_back(e[1]);
+    reps[e[1]].push_back(e[0]);
+  }
+  for (int u = 0; u < n_; ++u)
+    for (const auto& t : tr_[u]) rtr[t.second].push_back(u);
+  // shortest accepted completion of every NFA state: 0-1 BFS backwards from the accept states
+  ndist_.assign(n_, std::numeric_limits<int32_t>::max() / 4);
+  std::deque<int32_t> q;
+  for (int32_t a : accept) {
+    if (a < 0 || a >= n_) throw std::invalid_argument("schema NFA: bad accept state");
+    nacc_[a] = 1;
+    ndist_[a] = 0;
+    q.push_back(a);
+  }
+  while (!q.empty()) {
+    const int32_t v = q.front();
+    q.pop_front();
+    for (int32_t u : reps[v])
+      if (ndist_[v] < ndist_[u]) {
+        ndist_[u] = ndist_[v];
+        q.push_front(u);
+      }
+    for (int32_t u : rtr[v])
+      if (ndist_[v] + 1 < ndist_[u]) {
+        ndist_[u] = ndist_[v] + 1;
+        q.push_back(u);
+      }
+  }
+  if (start < 0 || start >= n_) throw std::invalid_argument("schema NFA: bad start state");
+  start_ = intern({start});
+}
+
+void SchemaAutomaton::closure(std::vector<int32_t>& set) const {
+  std::vector<uint8_t> seen(n_, 0);
+  std::vector<int32_t> stack(set.begin(), set.end());
+  set.clear();
+  while (!stack.empty()) {
+    const int32_t u = stack.back();
+    stack.pop_back();
+    if (seen[u]) continue;
+    seen[u] = 1;
+    set.push_back(u);
+    for (int32_t v : eps_[u])
+      if (!seen[v]) stack.push_back(v);
+  }
+  std::sort(set.begin(), set.end());
+}
+
+int SchemaAutomaton::intern(std::vector<int32_t> set) {
+  closure(set);
+  std::string key(reinterpret_cast<const char*>(set.data()), set.size() * sizeof(int32_t));
+  auto it = ids_.find(key);
+  if (it != ids_.end()) return it->second;
+  const int32_t id = (int32_t)sets_.size();
+  uint8_t acc = 0;
+  int32_t dist = std::numeric_limits<int32_t>::max() / 4;
+  for (int32_t u : set) {
+    acc |= nacc_[u];
+    dist = std::min(dist, ndist_[u]);
+  }
+  sets_.push_back(std::move(set));
+  ids_.emplace(std::move(key), id);
+  trans_.emplace_back(256, -2);
+  acc_.push_back(acc);
+  dist_.push_back(dist);
+  exit_.push_back(-1);
+  return id;
+}
+
+int SchemaAutomaton::step_locked(int d, uint8_t c) {
+  int32_t& t = trans_[d][c];
+  if (t != -2) return t;
+  std::vector<int32_t> next;
+  for (int32_t u : sets_[d])
+    for (const auto& e : tr_[u])
+      if (c >= (e.first & 255u) && c <= (e.first >> 8)) next.push_back(e.second);
+  const int32_t r = next.empty() ? -1 : intern(std::move(next));
+  trans_[d][c] = r;  // intern may have grown trans_: index again
+  return r;
+}
+
+int SchemaAutomaton::step(int d, uint8_t c) {
+  std::lock_guard<std::mutex> lk(mu_);
+  return step_locked(d, c);
+}
+
+bool SchemaAutomaton::has_exit(int d) {
+  std::lock_guard<std::mutex> lk(mu_);
+  if (exit_[d] < 0) {
+    int8_t any = 0;
+    for (int c = 0; c < 256 && !any; ++c) any = step_locked(d, (uint8_t)c) >= 0;
+    exit_[d] = any;
+  }
+  return exit_[d] != 0;
+}
+
+int SchemaAutomaton::mask(int d, int limit, uint32_t* out) {
+  const int W = vocab_->words();
+  const uint64_t key = ((uint64_t)(uint32_t)d << 32) | (uint32_t)limit;
+  std::lock_guard<std::mutex> lk(mu_);
+  auto it = cache_.find(key);
+  if (it != cache_.end()) {
+    std::memcpy(out, it->second.data() + 1, W * sizeof(uint32_t));
+    return (int)it->second[0];
+  }
+  std::vector<uint32_t> m(W + 1, 0u);
+  int count = 0;
+  auto step = [this](int& s, uint8_t c) {
+    s = step_locked(s, c);
+    return s >= 0;
+  };
+  auto leaf = [this, limit](int s) { return dist_[s] <= limit; };
+  vocab_->walk_tokens(0, d, step, leaf, m.data() + 1, count);
+  if (acc_[d]) {
+    for (int32_t e : vocab_->eos_ids())
+      if (e >= 0 && e < vocab_->vocab_size() && !(m[1 + (e >> 5)] & (1u << (e & 31)))) {
+        m[1 + (e >> 5)] |= 1u << (e & 31);
+        ++count;
+      }
+  }
+  m[0] = (uint32_t)count;
+  std::memcpy(out, m.data() + 1, W * sizeof(uint32_t));
+  if (cache_.size() >= 1024) cache_.clear();
+  cache_.emplace(key, std::move(m));
+  return count;
+}
+
+int SchemaMatcher::fill_mask(int remaining, uint32_t* out) {
+  const JsonVocab& v = a_->vocab();
+  const int W = v.words();
+  if (!broken_) {
+    const int slack = a_->dist(d_) + 64;
+    int n = a_->mask(d_, std::min(std::max(remaining - 1, 0), slack), out);
+    if (n > 0) return n;
+    n = a_->mask(d_, std::numeric_limits<int>::max() / 8, out);
+    if (n > 0) return n;
+  }
+  std::fill(out, out + W, 0xFFFFFFFFu);
+  const int V = v.vocab_size();
+  if (V % 32) out[W - 1] = (1u << (V % 32)) - 1;
+  return V;
+}
+
+bool SchemaMatcher::advance(int token) {
+  const JsonVocab& v = a_->vocab();
+  if (broken_) return false;
+  if (token < 0 || token >= v.vocab_size()) {
+    broken_ = true;
+    return false;
+  }
+  if (v.is_eos(token)) {
+    if (a_->accepting(d_)) return true;
+    broken_ = true;
+    return false;
+  }
+  const std::string& b = v.token(token);
+  int d = d_;
+  for (unsigned char c : b) {
+    d = a_->step(d, c);
+    if (d < 0) break;
+  }
+  if (b.empty() || d < 0) {
+    broken_ = true;
+    return false;
+  }
+  d_ = d;
+  text_ += b;
+  return true;
+}
+
+bool SchemaMatcher::done() { return !broken_ && a_->accepting(d_) && !a_->has_exit(d_); }
 
 }  // namespace dab

@@ -48,6 +48,25 @@ class JsonVocab {
   // returns the number of allowed tokens.  Cached per (state, limit).
   int mask(const JsonState& s, int limit, int max_depth, int max_ws, uint32_t* out);
 
+  // Generic walk of the token trie from `node` in automaton state `s`: `step(state&, byte)` advances
+  // a copy of the state (false = dead: the subtree is pruned), `leaf(state)` decides whether a
+  // token ending in that state is allowed; allowed tokens are OR-ed into `out`.
+  template <class S, class Step, class Leaf>
+  void walk_tokens(int node, const S& s, Step& step, Leaf& leaf, uint32_t* out, int& count) const {
+    for (int32_t ch = nodes_[node].child; ch >= 0; ch = nodes_[ch].sibling) {
+      S t = s;
+      if (!step(t, nodes_[ch].byte)) continue;
+      if (nodes_[ch].tok >= 0 && leaf(t)) {
+        for (int32_t k = nodes_[ch].tok; k >= 0; k = tok_next_[k]) {
+          out[k >> 5] |= 1u << (k & 31);
+          ++count;
+        }
+      }
+      if (nodes_[ch].child >= 0) walk_tokens(ch, t, step, leaf, out, count);
+    }
+  }
+  const std::vector<int32_t>& eos_ids() const { return eos_; }
+
  private:
   struct Node {
     int32_t child = -1, sibling = -1, tok = -1;  // tok: first token ending here (chain in tok_next_)
@@ -80,6 +99,63 @@ class JsonMatcher {
   std::shared_ptr<JsonVocab> vocab_;
   JsonState state_;
   int max_depth_, max_ws_;
+  bool broken_ = false;
+  std::string text_;
+};
+
+// JSON-Schema-constrained decoding: the schema is compiled (engine/json_schema.py) into a byte NFA
+// (a regular language: fixed key order, typed / enumerated values, bounded whitespace), which is
+// determinised lazily here; masks walk the token trie through the DFA and are cached per
+// (DFA state, budget).  The budget rule is the JSON one: a token is allowed only if the shortest
+// accepted completion after it fits in the tokens left.
+class SchemaAutomaton {
+ public:
+  // edges: (from, lo, hi, to) byte-range transitions; eps: (from, to)
+  SchemaAutomaton(std::shared_ptr<JsonVocab> vocab, int n_states, int start, const std::vector<int32_t>& accept,
+                  const std::vector<std::vector<int32_t>>& edges, const std::vector<std::vector<int32_t>>& eps);
+  int start() const { return start_; }
+  int step(int d, uint8_t c);         // DFA transition (-1 = dead); builds states lazily
+  bool accepting(int d) const { return acc_[d] != 0; }
+  int dist(int d) const { return dist_[d]; }  // shortest accepted completion, bytes
+  bool has_exit(int d);               // any byte leads somewhere
+  int mask(int d, int limit, uint32_t* out);
+  int dfa_states() const { return (int)sets_.size(); }
+  const JsonVocab& vocab() const { return *vocab_; }
+
+ private:
+  std::shared_ptr<JsonVocab> vocab_;
+  int n_;
+  std::vector<std::vector<std::pair<uint32_t, int32_t>>> tr_;  // per NFA state: (lo | hi << 8, to)
+  std::vector<std::vector<int32_t>> eps_;
+  std::vector<uint8_t> nacc_;
+  std::vector<int32_t> ndist_;
+  std::vector<std::vector<int32_t>> sets_;
+  std::unordered_map<std::string, int32_t> ids_;
+  std::vector<std::vector<int32_t>> trans_;  // [dfa][256]: -2 unknown, -1 dead
+  std::vector<uint8_t> acc_;
+  std::vector<int32_t> dist_;
+  std::vector<int8_t> exit_;
+  int start_;
+  std::mutex mu_;
+  std::unordered_map<uint64_t, std::vector<uint32_t>> cache_;
+  int intern(std::vector<int32_t> set);
+  void closure(std::vector<int32_t>& set) const;
+  int step_locked(int d, uint8_t c);
+};
+
+class SchemaMatcher {
+ public:
+  explicit SchemaMatcher(std::shared_ptr<SchemaAutomaton> a) : a_(std::move(a)), d_(a_->start()) {}
+  int fill_mask(int remaining, uint32_t* out);
+  bool advance(int token);
+  bool done();
+  bool broken() const { return broken_; }
+  int completion_len() const { return a_->dist(d_); }
+  const std::string& text() const { return text_; }
+
+ private:
+  std::shared_ptr<SchemaAutomaton> a_;
+  int d_;
   bool broken_ = false;
   std::string text_;
 };

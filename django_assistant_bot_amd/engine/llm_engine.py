@@ -50,6 +50,7 @@ class SamplingParams:
     do_sample: bool = True
     timeout_s: float | None = None  # per-request deadline from arrival: finish_reason "timeout"
     json_mode: bool = False  # constrain the output to one JSON object (engine/json_constraint.py)
+    json_schema: dict | str | None = None  # ... to a JSON Schema (engine/json_schema.py; implies json_mode)
 
 
 @dataclass
@@ -227,7 +228,14 @@ class LLMEngine:
             prompt = prompt[-(self.max_model_len - 1):]
         seed = params.seed if params.seed is not None else self.seed
         r = _Req(rid, prompt, params, time.perf_counter(), rng_base=((seed * 1000003 + rid) & 0xFFFFFFFF) << 20)
-        if params.json_mode:
+        if params.json_schema is not None and self.tokenizer.byte_exact:
+            from .json_schema import matcher_for
+
+            r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids, params.json_schema)
+            self._ensure_mask_buffers()
+        elif params.json_mode or params.json_schema is not None:
+            # (the offline hash tokenizer puts a space before every word token, so exact keys /
+            # enum strings cannot be spelled: a schema degrades to plain JSON mode there)
             from .json_constraint import matcher_for
 
             r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids)

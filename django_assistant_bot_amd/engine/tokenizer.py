@@ -54,6 +54,12 @@ class Tokenizer:
         c.sep_id = -1
         return cls(n.HashTokenizer(c), "decoder", bos_id=cfg.bos_id, vocab_size=cfg.vocab_size)
 
+    @property
+    def byte_exact(self) -> bool:
+        """Whether every string can be spelled token by token (HF byte-level / SentencePiece
+        vocabularies; not the hash tokenizer, whose word tokens carry a leading space)."""
+        return self._hf is not None
+
     # ------------------------------------------------------------------ API
     def encode(self, text: str, add_special: bool = True, max_len: int = 0) -> list[int]:
         if self._hf is not None:

@@ -97,7 +97,7 @@ def unpack(meta: torch.Tensor, body: torch.Tensor) -> list:
 def payload_len(h) -> int:
     k = int(h[0])
     if k == ADD:
-        return int(h[3]) + int(h[4])
+        return int(h[3]) + int(h[4]) + int(h[15])
     if k == ABORT:
         return int(h[3])
     if k == OUT:
@@ -147,20 +147,28 @@ def bcast_batch(items, src: int, group) -> list:
 # ---------------------------------------------------------------------- requests / outputs
 def add_item(model: int, rid: int, prompt, params):
     stop = [int(t) for t in (params.stop_token_ids or ())]
+    schema = np.zeros(0, dtype=np.int64)
+    if params.json_schema is not None:
+        from ..engine.json_schema import schema_key
+
+        schema = text_words(schema_key(params.json_schema))
     words = [ADD, model, rid, len(prompt), len(stop), int(params.max_new_tokens), f2i(params.temperature),
              int(params.top_k), f2i(params.top_p), int(bool(params.ignore_eos)), opt_i(params.max_length),
-             opt_i(params.seed), int(bool(params.do_sample)), opt_f(params.timeout_s), int(bool(params.json_mode))]
-    return item(words, list(prompt) + stop)
+             opt_i(params.seed), int(bool(params.do_sample)), opt_f(params.timeout_s), int(bool(params.json_mode)),
+             len(schema)]
+    return item(words, np.concatenate([np.asarray(list(prompt) + stop, dtype=np.int64), schema]))
 
 
 def read_add(h, p):
     from ..engine.llm_engine import SamplingParams
 
-    n_prompt = int(h[3])
+    n_prompt, n_stop = int(h[3]), int(h[4])
+    n_schema = int(h[15])
+    schema = words_text(p[n_prompt + n_stop:n_prompt + n_stop + n_schema]) if n_schema else None
     sp = SamplingParams(max_new_tokens=int(h[5]), temperature=i2f(h[6]), top_k=int(h[7]), top_p=i2f(h[8]),
                         ignore_eos=bool(h[9]), max_length=i_opt(h[10]), seed=i_opt(h[11]),
-                        stop_token_ids=tuple(int(t) for t in p[n_prompt:]), do_sample=bool(h[12]),
-                        timeout_s=f_opt(h[13]), json_mode=bool(h[14]))
+                        stop_token_ids=tuple(int(t) for t in p[n_prompt:n_prompt + n_stop]), do_sample=bool(h[12]),
+                        timeout_s=f_opt(h[13]), json_mode=bool(h[14]), json_schema=schema)
     return int(h[1]), int(h[2]), [int(t) for t in p[:n_prompt]], sp
 
 

@@ -2,7 +2,7 @@
 
 Endpoints (request/response shapes of the reference where it had them):
   POST /embeddings/             {model, texts}                         -> {embeddings: [[float]]}
-  POST /dialog/                 {model, messages, max_tokens, json_format} -> {response: AIResponse}
+  POST /dialog/                 {model, messages, max_tokens, json_format[, json_schema]} -> {response: AIResponse}
   POST /index/{name}/upsert     {ids, vectors, doc_ids?, groups?}      -> {count}
   POST /index/{name}/delete     {ids}                                  -> {removed}
   POST /index/{name}/search     {queries, k, groups?, allowed?}        -> {ids, distances, doc_ids}
@@ -60,6 +60,7 @@ class DialogRequest(BaseModel):
     messages: List[Message]
     max_tokens: int = 1024
     json_format: bool = False
+    json_schema: Optional[dict] = None  # constrained decoding to a JSON Schema (engine/json_schema.py)
 
 
 class UpsertRequest(BaseModel):
@@ -132,8 +133,9 @@ async def get_response(request: DialogRequest):
     if provider is None:
         raise HTTPException(status_code=400, detail="Model is not supported")
     try:
+        kw = {"json_schema": request.json_schema} if request.json_schema is not None else {}
         resp = await provider.get_response([{"role": m.role, "content": m.content} for m in request.messages],
-                                           max_tokens=request.max_tokens, json_format=request.json_format)
+                                           max_tokens=request.max_tokens, json_format=request.json_format, **kw)
         return {"response": asdict(resp)}
     except Exception as e:
         logger.exception("dialog failed")
