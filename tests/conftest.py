@@ -1,4 +1,5 @@
 import os
+import random
 import sys
 
 import pytest
@@ -30,3 +31,29 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def bpe_dir(tmp_path_factory):
+    """A byte-level BPE tokenizer.json for tiny-llama (1000 trained tokens, <|bos|> = 1000,
+    <|eos|> = 1001): the kind of vocabulary real checkpoints ship (Llama-3 is byte-level BPE)."""
+    tokenizers = pytest.importorskip("tokenizers")
+    from tokenizers import decoders, models, pre_tokenizers, trainers
+
+    tok = tokenizers.Tokenizer(models.BPE())
+    tok.pre_tokenizer = pre_tokenizers.ByteLevel(add_prefix_space=False)
+    tok.decoder = decoders.ByteLevel()
+    rng = random.Random(0)
+    words = ["topic", "question", "billing", "access", "small", "talk", "null", "true", "false", "name", "score"]
+    corpus = [" ".join(rng.choice(words) + rng.choice(["", "s", "ing", '":', '"}', "{", ","]) for _ in range(12))
+              for _ in range(3000)] + ['{"topic": "Billing"}', '{"question": 3}', "Доступ к аккаунту"] * 50
+    trainer = trainers.BpeTrainer(vocab_size=1000, initial_alphabet=pre_tokenizers.ByteLevel.alphabet(),
+                                  show_progress=False)
+    tok.train_from_iterator(corpus, trainer)
+    n = tok.get_vocab_size()
+    tok.add_tokens([f"<pad{i}>" for i in range(1000 - n)])
+    tok.add_special_tokens(["<|bos|>", "<|eos|>"])
+    assert tok.token_to_id("<|bos|>") == 1000 and tok.token_to_id("<|eos|>") == 1001
+    d = tmp_path_factory.mktemp("bpe")
+    tok.save(str(d / "tokenizer.json"))
+    return str(d)

@@ -243,6 +243,34 @@ def _ref_llama3(cfg, w, seqs):
     return torch.cat(outs)
 
 
+def test_engine_json_schema_on_gpu_graphs(bpe_dir):
+    """JSON-Schema rows (byte-level BPE tokenizer) through the masked decode graphs: every answer
+    satisfies the reference step conditions (topic in the enum; question 1..5 or null)."""
+    import json
+
+    from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
+
+    cfg = decoder_config("tiny-llama")
+    eng = LLMEngine(cfg, device=DEV, max_batch=16, block_size=64, num_blocks=128, seed=4, checkpoint=bpe_dir,
+                    weights=random_decoder_weights(cfg, DEV, seed=4, interleave_mlp=True))
+    topics = ["Small talk", "Billing", "Доступ"]
+    cls = {"type": "object", "properties": {"topic": {"type": "string", "enum": topics}}, "required": ["topic"]}
+    known = {"type": "object", "properties": {"question": {"anyOf": [
+        {"type": "integer", "minimum": 1, "maximum": 5}, {"type": "null"}]}}, "required": ["question"]}
+    rids = [eng.add_request(list(range(3, 30 + 4 * i)), SamplingParams(max_new_tokens=24, seed=i, ignore_eos=True,
+                                                                        json_schema=cls if i % 2 else known))
+            for i in range(10)]
+    while eng.has_unfinished():
+        eng.step()
+    for i, r in enumerate(rids):
+        obj = json.loads(eng.pop_output(r).text)
+        if i % 2:
+            assert obj["topic"] in topics
+        else:
+            assert obj["question"] is None or 1 <= obj["question"] <= 5
+    assert any(k[2] for k in eng._graphs) and eng.stats.get("json_broken", 0) == 0
+
+
 def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32():
     """Two decoder layers at full Llama-3-8B width (H 4096, 32 / 8 heads, D 128, F 14336, 128k
     vocabulary, Llama-3 RoPE scaling) on the production kernels, vs an independent fp32 PyTorch
