@@ -563,7 +563,7 @@ int SchemaAutomaton::mask(int d, int limit, uint32_t* out) {
   }
   m[0] = (uint32_t)count;
   std::memcpy(out, m.data() + 1, W * sizeof(uint32_t));
-  if (cache_.size() >= 1024) cache_.clear();
+  if (cache_.size() >= 256) cache_.clear();  // per schema: <= 4 MB at a 128k vocabulary
   cache_.emplace(key, std::move(m));
   return count;
 }

@@ -223,7 +223,7 @@ def automaton_for(tokenizer, eos_ids, schema):
             cache = tokenizer._schema_automata = {}
         a = cache.get(key)
         if a is None:
-            if len(cache) >= 64:
+            if len(cache) >= 16:
                 cache.clear()
             n, s, acc, edges, eps = compile_schema(key)
             a = cache[key] = native().SchemaAutomaton(vocab, n, s, acc, edges, eps)

@@ -100,6 +100,13 @@ def _drive(node, out_path):
     res["gen_running_at_search"] = sum(not f.done() for f in futs)
     outs = [f.result(timeout=120) for f in futs]
     res["gen_tokens"] = [len(o.token_ids) for o in outs]
+    # constrained requests travel the wire too (json_mode flag / schema text in the ADD item)
+    import json
+
+    jf = [worker.submit(list(range(3, 25)), SamplingParams(max_new_tokens=12, ignore_eos=True, json_mode=True)),
+          worker.submit(list(range(4, 25)), SamplingParams(max_new_tokens=12, ignore_eos=True, json_schema={
+              "type": "object", "properties": {"q": {"type": "integer"}}}))]
+    res["json_ok"] = [isinstance(json.loads(f.result(timeout=120).text), dict) for f in jf]
     res["placed"] = worker.engine.stats_node["placed"]
     st = node.command("stats")
     res["ctrl_s"] = st[:, 0].tolist()
@@ -122,6 +129,7 @@ def test_node_control_plane_world4(tmp_path):
     assert res["gen_running_at_search"] > 0 and res["search_rows"] == [10, 10, 10]
     assert res["search_s"] < 0.25, res["search_s"]
     assert res["gen_tokens"] == [40] * 8
+    assert res["json_ok"] == [True, True]
     assert min(res["placed"]) > 0
     # per-step control cost on the replica leaders (ranks 1..3, each stepping its own replica)
     for r in range(1, W):
