@@ -41,6 +41,15 @@ ARMS = {
     "qkv15": {"qkv": (15, 4)},
     "o15": {"o": (15, 8)},
     "rope": {"_rope": True},
+    "o9_4": {"o": (9, 4)},
+    "o11_4": {"o": (11, 4)},
+    "down9_4": {"down": (9, 4)},
+    "down11_4": {"down": (11, 4)},
+    "qkv9_2": {"qkv": (9, 2)},
+    "od9_4": {"o": (9, 4), "down": (9, 4)},
+    "no_norm": {"_ablate": {"norm"}},       # upper bound of fusing the two RMSNorms away (wrong results)
+    "no_rope": {"_ablate": {"rope"}},       # upper bound of fusing the RoPE / KV write away
+    "no_norm_rope": {"_ablate": {"norm", "rope"}},
     "part1024": {"_part": 1024},
     "part512": {"_part": 512},
 }
@@ -84,6 +93,7 @@ def main():
             spec = dict(ARMS[a])
             restart()
             eng.model.stream_overrides = {k: v for k, v in spec.items() if not k.startswith("_")}
+            eng.model.ablate = set(spec.get("_ablate", ()))
             eng.long_part_size = spec.get("_part", base_part)
             llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
             eng._graphs.clear()

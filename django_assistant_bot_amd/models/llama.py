@@ -115,6 +115,9 @@ class LlamaModel:
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         self.stream_overrides: dict = {}  # projection name -> (stream_gemm cfg, K-slices): tuning runs only
+        # decode-step ablations for upper-bound timing (benchmarks/decode_ab.py; WRONG results):
+        # "norm" skips the two slab-summing RMSNorms, "rope" the RoPE / KV-write kernel
+        self.ablate: set = set()
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -229,6 +232,8 @@ class LlamaModel:
         elif residual is None:
             h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
             residual = x
+        elif sk and "norm" in self.ablate:
+            h = self._ablation_buf(x.shape[-2], x.shape[-1])
         else:
             h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
         qkv = self._proj(h, L.qkv_w, sk, name="qkv")
@@ -248,7 +253,11 @@ class LlamaModel:
                                       meta.block_tables, meta.ctx_lens, self.hq, meta.part_size, meta.workspace,
                                       order=meta.order)
             return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D)
-        q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
+        if sk and "rope" in self.ablate:
+            q = self._ablation_buf(T, self.hq * D).view(T, self.hq, D)
+        else:
+            q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv,
+                                  D)
         if meta.decode:
             a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
                                  meta.workspace, order=meta.order)
@@ -267,7 +276,10 @@ class LlamaModel:
             h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)
         else:
             o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o"))
-            h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
+            if sk and "norm" in self.ablate:
+                h = self._ablation_buf(T, cfg.hidden)
+            else:
+                h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
         # SwiGLU in the GEMM epilogue (8-row [gate | up] groups) on the GPU
         epi = ops.EPI_SWIGLU8 if (self.interleaved_mlp and h.is_cuda) else ops.EPI_NONE
         act = self._proj(h, L.gate_up_w, sk, name="gate_up", epilogue=epi)
@@ -277,6 +289,12 @@ class LlamaModel:
             return None, ops.gemm_bt(act, L.down_w, residual=residual, shuffled=self.frag)
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
         return x, residual
+
+    def _ablation_buf(self, rows: int, cols: int) -> torch.Tensor:
+        buf = getattr(self, "_abl", None)
+        if buf is None or buf.numel() < rows * cols:
+            buf = self._abl = torch.zeros(rows * cols, dtype=torch.bfloat16, device=self.device)
+        return buf[:rows * cols].view(rows, cols)
 
     @staticmethod
     def _mixed_attention(q, kv: KVCache, li: int, meta: AttnMeta) -> torch.Tensor:
