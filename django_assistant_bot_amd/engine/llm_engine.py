@@ -235,8 +235,14 @@ class LLMEngine:
             self._ensure_mask_buffers()
         elif params.json_mode or params.json_schema is not None:
             # (the offline hash tokenizer puts a space before every word token, so exact keys /
-            # enum strings cannot be spelled: a schema degrades to plain JSON mode there)
+            # enum strings cannot be spelled: a schema degrades to plain JSON mode there; it is
+            # still validated, so an unsupported schema fails the same way everywhere)
             from .json_constraint import matcher_for
+
+            if params.json_schema is not None:
+                from .json_schema import compile_schema
+
+                compile_schema(params.json_schema)
 
             r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids)
             self._ensure_mask_buffers()
@@ -546,8 +552,13 @@ class LLMEngine:
         W = -(-self.cfg.vocab_size // 32)
         mb = self.max_batch
         pin = self.is_gpu
-        self._h_mask = torch.zeros((mb, W), dtype=torch.int32, pin_memory=pin)
-        self._h_mflag = torch.zeros(mb, dtype=torch.int32, pin_memory=pin)
+        # two pinned host sets, alternated: a launched prefill chunk's mask copy may still be queued
+        # behind its forward when the next chunk fills masks (each set is reused only after the copy
+        # issued from it two calls ago has run)
+        self._h_masks = [(torch.zeros((mb, W), dtype=torch.int32, pin_memory=pin),
+                          torch.zeros(mb, dtype=torch.int32, pin_memory=pin)) for _ in range(2)]
+        self._mask_events = [None, None]
+        self._mask_turn = 0
         self._d_mask = torch.zeros((mb, W), dtype=torch.int32, device=self.device)
         self._d_mflag = torch.zeros(mb, dtype=torch.int32, device=self.device)
 
@@ -564,15 +575,24 @@ class LLMEngine:
         and their H2D copies.  -> whether any row is constrained."""
         if not any(r.matcher is not None for r in reqs):
             return False
-        self._h_mflag[:n_rows] = 0
-        row_bytes = self._h_mask.shape[1] * 4
-        base = self._h_mask.data_ptr()
+        t = self._mask_turn
+        self._mask_turn ^= 1
+        if self._mask_events[t] is not None:
+            self._mask_events[t].synchronize()
+        h_mask, h_flag = self._h_masks[t]
+        h_flag[:n_rows] = 0
+        row_bytes = h_mask.shape[1] * 4
+        base = h_mask.data_ptr()
         for i, r in enumerate(reqs):
             if r.matcher is not None:
                 r.matcher.fill_mask(self._budget(r), base + i * row_bytes)
-                self._h_mflag[i] = 1
-        self._d_mask[:n_rows].copy_(self._h_mask[:n_rows], non_blocking=True)
-        self._d_mflag[:n_rows].copy_(self._h_mflag[:n_rows], non_blocking=True)
+                h_flag[i] = 1
+        self._d_mask[:n_rows].copy_(h_mask[:n_rows], non_blocking=True)
+        self._d_mflag[:n_rows].copy_(h_flag[:n_rows], non_blocking=True)
+        if self.is_gpu:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._mask_events[t] = ev
         return True
 
     def _sample(self, logits, reqs, to_host: bool = True):

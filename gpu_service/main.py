@@ -137,6 +137,8 @@ async def get_response(request: DialogRequest):
         resp = await provider.get_response([{"role": m.role, "content": m.content} for m in request.messages],
                                            max_tokens=request.max_tokens, json_format=request.json_format, **kw)
         return {"response": asdict(resp)}
+    except ValueError as e:  # e.g. a JSON Schema the constrained decoder cannot compile
+        raise HTTPException(status_code=400, detail=str(e))
     except Exception as e:
         logger.exception("dialog failed")
         raise HTTPException(status_code=500, detail=str(e))

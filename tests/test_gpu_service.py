@@ -39,6 +39,18 @@ def test_dialog(client):
     assert client.post("/dialog/", json={"model": "x", "messages": []}).status_code == 400
 
 
+def test_dialog_json_schema(client):
+    """/dialog/ with a JSON Schema (an extension of the reference schema): the answer is an object;
+    a schema the constrained decoder cannot compile is a 400, not a 500."""
+    msg = [{"role": "user", "content": "json please"}]
+    schema = {"type": "object", "properties": {"question": {"type": ["integer", "null"]}}}
+    r = client.post("/dialog/", json={"model": "tiny-llama", "messages": msg, "max_tokens": 16,
+                                      "json_format": True, "json_schema": schema})
+    assert r.status_code == 200 and isinstance(r.json()["response"]["result"], dict)
+    bad = client.post("/dialog/", json={"model": "tiny-llama", "messages": msg, "json_schema": {"type": "string"}})
+    assert bad.status_code == 400
+
+
 def test_index_roundtrip(client):
     vecs = [[1.0, 0.0, 0.0, 0.0], [0.0, 1.0, 0.0, 0.0], [0.7, 0.7, 0.0, 0.0]]
     r = client.post("/index/q/upsert", json={"ids": [10, 11, 12], "vectors": vecs, "doc_ids": [1, 2, 3]})
