@@ -109,6 +109,7 @@ class LLMEngine:
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
         self.is_gpu = self.device.type == "cuda"
         self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank
+        own_weights = weights is None  # a dict built here may be consumed while it is converted
         if weights is None:
             if checkpoint:
                 from ..models import load_decoder_checkpoint
@@ -119,8 +120,13 @@ class LLMEngine:
                 weights = random_decoder_weights(cfg, self.device, seed=seed, tp_rank=tp_rank, tp_size=tp_size,
                                                  interleave_mlp=interleaved_mlp)
         self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
-                                interleaved_mlp=interleaved_mlp)
+                                interleaved_mlp=interleaved_mlp, consume=own_weights)
         del weights
+        if self.is_gpu:
+            # the caller's weight dict held the row-major originals while the model converted them
+            # to the fragment layout: return those blocks to the device before the KV pool is sized
+            # from the free memory (cached blocks are not "free")
+            torch.cuda.empty_cache()
         if tp_size > 1 and self.is_gpu:
             from ..parallel.custom_allreduce import maybe_create
 

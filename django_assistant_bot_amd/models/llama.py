@@ -83,34 +83,41 @@ _FUSED_DECODE_ROPE = os.environ.get("DAB_DECODE_ROPE_FUSED", "0") == "1"
 
 class LlamaModel:
     def __init__(self, cfg: DecoderConfig, weights: dict, device, tp_group=None, tp_size: int = 1,
-                 interleaved_mlp: bool = False, fragment_layout: bool = True):
+                 interleaved_mlp: bool = False, fragment_layout: bool = True, consume: bool = False):
+        """``consume``: the entries of ``weights`` are popped as the model takes them over, so each
+        original is freed as soon as its fragment-layout copy exists (peak HBM = model + one
+        tensor: 70B at TP 1 needs it, 2 x 140 GB would not fit in 288 GB)."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.tp_group, self.tp_size = tp_group, tp_size
         self.hq = cfg.heads // tp_size
         self.hkv = cfg.kv_heads // tp_size
         self.interleaved_mlp = interleaved_mlp  # gate_up rows in 8-row [gate | up] groups (EPI_SWIGLU8)
-        w = {k: v.to(self.device) for k, v in weights.items()}
-        self.embed = w.pop("embed")
-        self.final_norm = w.pop("final_norm")
-        self.lm_head = w.pop("lm_head", self.embed)
-        self.layers = [
-            DecoderLayer(*(w.pop(f"l{i}.{n}") for n in ("attn_norm", "qkv_w", "o_w", "mlp_norm", "gate_up_w", "down_w")))
-            for i in range(cfg.layers)
-        ]
-        del w
         # One copy of every projection, in the fragment layout both GEMM families read (VERDICT r2
         # "stop paying HBM twice": the decode-only shuffled copies were +15 GB for Llama-3-8B and
         # disabled the streaming decode for 70B at TP 1).  The LM head too; a tied embedding table
         # keeps its row-major copy for the gather.
         # (``fragment_layout=False``: row-major weights on the GPU too, every projection on the
         # 128x128 / 8-phase GEMMs -- the comparison path of tests/test_models_gpu.py)
-        self.frag = fragment_layout and self.device.type == "cuda" and self._fragment_ok()
-        if self.frag:
-            for L in self.layers:
-                for n in ("qkv_w", "o_w", "gate_up_w", "down_w"):
-                    setattr(L, n, ops.shuffle_weights(getattr(L, n)))
-            self.lm_head = ops.shuffle_weights(self.lm_head)
+        self.frag = fragment_layout and self.device.type == "cuda" and self._fragment_ok(weights)
+        take = weights.pop if consume else weights.__getitem__
+
+        def proj(key):
+            t = take(key).to(self.device)
+            return ops.shuffle_weights(t) if self.frag else t
+
+        self.embed = take("embed").to(self.device)
+        self.final_norm = take("final_norm").to(self.device)
+        if "lm_head" in weights:
+            self.lm_head = proj("lm_head")
+        else:
+            self.lm_head = ops.shuffle_weights(self.embed) if self.frag else self.embed
+        self.layers = [
+            DecoderLayer(take(f"l{i}.attn_norm").to(self.device), proj(f"l{i}.qkv_w"), proj(f"l{i}.o_w"),
+                         take(f"l{i}.mlp_norm").to(self.device), proj(f"l{i}.gate_up_w"), proj(f"l{i}.down_w"))
+            for i in range(cfg.layers)
+        ]
+        if self.frag and consume:
             torch.cuda.empty_cache()
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
@@ -121,9 +128,11 @@ class LlamaModel:
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
-    def _fragment_ok(self) -> bool:
-        mats = [self.lm_head] + [getattr(L, n) for L in self.layers for n in ("qkv_w", "o_w", "gate_up_w", "down_w")]
-        return all(m.shape[0] % 16 == 0 and m.shape[1] % 64 == 0 for m in mats) and self.interleaved_mlp
+    def _fragment_ok(self, weights: dict) -> bool:
+        keys = ["lm_head" if "lm_head" in weights else "embed"] + [
+            f"l{i}.{n}" for i in range(self.cfg.layers) for n in ("qkv_w", "o_w", "gate_up_w", "down_w")]
+        return self.interleaved_mlp and all(weights[k].shape[0] % 16 == 0 and weights[k].shape[1] % 64 == 0
+                                            for k in keys)
 
     @property
     def dtype(self):
