@@ -184,7 +184,7 @@ PYBIND11_MODULE(_native, m) {
     int rc = hipErrorInvalidValue;
     if (M <= 16 && K % 256 == 0 && K <= 1024)
       rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
-    else if (M <= 128)
+    else if (M < 128)  // 128+ queries fill the persistent 256x256 kernel's tiles (gemm256 G_CAND)
       rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
     else
       rc = dab::gemm_score_candidates(CVP(A), lda, CVP(Wshuf), K, M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s), b_rows);

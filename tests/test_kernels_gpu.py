@@ -577,10 +577,11 @@ def test_score_candidates_exact_set(M):
         torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 17, 37, 64, 65, 128])
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 37, 64, 65, 127, 128, 300])
 def test_score_candidates_shuffled_exact_set(M):
     """The scans over a shuffle_weights copy of the rows (1..16 queries: index_scan.hip SHUF;
-    17..64: the streaming kernel's cfg 12; 65..128: cfg 10) append exactly the filtered scores >=
+    17..64: the streaming kernel's cfg 12; 65..127: cfg 10; 128+: gemm256 G_CAND reading the fragment
+    layout) append exactly the filtered scores >=
     thr[m] (N not a multiple of 128: the copy is zero-padded)."""
     N, K = 100_004, 768
     A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
