@@ -38,6 +38,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -215,7 +216,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--mode", choices=("serve", "batch"), default="batch")
+    ap.add_argument("--mode", choices=("serve", "batch", "overlap"), default="batch",
+                    help="overlap: two engines sharing the weights on two streams, batches alternating "
+                         "so one's prefill overlaps the other's decode (throughput setting)")
     ap.add_argument("--batch", type=int, default=128,
                     help="questions in flight per GPU (serve) / per batch (batch); one step = this many answers")
     ap.add_argument("--admit-group", type=int, default=16, help="serve: questions retrieved + queued together")
@@ -260,6 +263,9 @@ def main():
     n_steps = args.warmup + args.steps
 
     serve = args.mode == "serve"
+    overlap = args.mode == "overlap"
+    if overlap and (args.warmup < 2 or args.tp > 1):
+        raise SystemExit("--mode overlap needs --warmup >= 2 (one batch per engine) and --tp 1")
     G = max(1, min(args.admit_group, B))
     if serve:
         # questions answered in the timed window + the ones still in flight at both ends
@@ -269,15 +275,21 @@ def main():
 
     t_setup = time.perf_counter()
     embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
+    kv_gb = args.kv_gb if (args.kv_gb or not overlap) else 48.0  # two pools in overlap mode
     llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
-                    use_graphs=not args.no_graphs, kv_cache_gb=args.kv_gb, max_prefill_tokens=args.prefill_tokens,
+                    use_graphs=not args.no_graphs, kv_cache_gb=kv_gb, max_prefill_tokens=args.prefill_tokens,
                     mixed_prefill_tokens=args.mixed_tokens if serve else 0, tp_group=tp_group, tp_size=args.tp,
                     tp_rank=tp_rank)
+    llm2 = None
+    if overlap:
+        llm2 = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
+                         use_graphs=not args.no_graphs, kv_cache_gb=kv_gb, max_prefill_tokens=args.prefill_tokens,
+                         shared_model=llm.model)
     # ---- synthetic corpus: index rows (questions) grouped into documents
     n_rows = args.index_rows
     n_docs = max(1, n_rows // args.rows_per_doc)
     docs = SyntheticDocuments(n_docs, args.seed).materialize()
-    if serve:  # replicated: every rank holds all rows (identical generator), no collective per search
+    if serve or overlap:  # replicated: every rank holds all rows (identical generator), no collective per search
         index = VectorIndex(embedder.dim, dev)
         gen = torch.Generator(device=dev).manual_seed(args.seed * 31)
         my_ids = np.arange(n_rows, dtype=np.int64)
@@ -321,7 +333,12 @@ def main():
     index.add(np.concatenate(plant_ids), torch.cat(plant_vecs), doc_ids=np.concatenate(plant_docs),
               groups=np.zeros(sum(len(x) for x in plant_ids), dtype=np.int32))
     del q_emb, q_own
-    rag = RAGPipeline(embedder, index, llm, docs, system_text=SYSTEM_TEXT)
+    rag_lock = threading.Lock() if overlap else None
+    rag = RAGPipeline(embedder, index, llm, docs, system_text=SYSTEM_TEXT, retrieve_lock=rag_lock)
+    rag2 = RAGPipeline(embedder, index, llm2, docs, system_text=SYSTEM_TEXT, retrieve_lock=rag_lock) if overlap else None
+    if overlap and llm.use_graphs:  # no capture may run while the other engine's thread launches work
+        llm.capture_all()
+        llm2.capture_all()
     params = SamplingParams(max_new_tokens=args.max_new_tokens, ignore_eos=True, temperature=1.0, top_k=50,
                             top_p=0.95)
     if dev.type == "cuda":
@@ -376,6 +393,62 @@ def main():
                     stats0, t0 = sync_start()
                 if done == total_n:
                     break
+    elif overlap:
+        # warm-up batches alternate between the engines on the main thread; then one thread per
+        # engine, each on its own stream, works through its half of the timed batches; engine 1
+        # starts once engine 0's first timed batch is decoding, so their phases interleave
+        pipes = (rag, rag2)
+        for step in range(args.warmup):
+            pipes[step % 2].answer(my_q[step * B:(step + 1) * B], params, bot_group=0)
+        stats0, t0 = sync_start()
+        go = threading.Event()
+        results = ([], [])
+        errors = []
+
+        def run(w):
+            import contextlib
+
+            try:
+                gpu = dev.type == "cuda"
+                if gpu:
+                    torch.cuda.set_device(dev)
+                pipe = pipes[w]
+                if w == 1:
+                    go.wait(timeout=600)
+                with torch.cuda.stream(torch.cuda.Stream(dev)) if gpu else contextlib.nullcontext():
+                    for step in range(args.warmup + w, n_steps, 2):
+                        qs = my_q[step * B:(step + 1) * B]
+                        rids = pipe.submit(qs, params, bot_group=0)
+                        pending, got = set(rids), {}
+                        while pending:
+                            for rid, r in pipe.poll():
+                                got[rid] = r
+                                pending.discard(rid)
+                            if w == 0 and not go.is_set() and pipe.llm.running and not (
+                                    pipe.llm.waiting or pipe.llm.prefilling):
+                                go.set()
+                        results[w].append([got[r] for r in rids])
+                        go.set()
+                    if gpu:
+                        torch.cuda.current_stream(dev).synchronize()
+            except BaseException as exc:  # surfaced on the main thread
+                errors.append(exc)
+                go.set()
+
+        threads = [threading.Thread(target=run, args=(w,)) for w in (0, 1)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        if errors:
+            raise errors[0]
+        for res in results[0] + results[1]:
+            latencies += [r.latency_s for r in res]
+            prompt_lens += [r.usage["prompt_tokens"] for r in res]
+            n_docs_used += [len(r.documents) for r in res]
+            phases["retrieve_s"].append(res[0].debug_info["took"])
+            phases["prompt_s"].append(res[0].debug_info["prompt"]["took"])
+            phases["generate_s"].append(max(r.debug_info["final"]["took"] for r in res))
     else:
         for step in range(n_steps):
             if step == args.warmup:
@@ -401,7 +474,7 @@ def main():
     # ---- reported separately: the two fast JSON generations per query, after the
     # timed region so the headline is unchanged
     fast = None
-    if not args.no_fast_steps and not serve:
+    if not args.no_fast_steps and not serve and not overlap:
         fast = measure_fast_steps(rag, llm, my_q[:B], info, dev)
     p50 = float(np.median(latencies)) if latencies else float("nan")
     p50 = pdist.max_over_ranks(p50, dev)
@@ -436,12 +509,13 @@ def main():
             "seq_len": int(np.mean(prompt_lens)) if prompt_lens else 0,
             "max_new_tokens": args.max_new_tokens,
             "parallelism": f"dp{n_rep}" + (f"xtp{args.tp}" if args.tp > 1 else ""),
-            "mode": ("batch" if not serve else
+            "mode": ("overlap (2 engines x batch {}, one weight copy, phases interleaved)".format(B) if overlap else
+                     "batch" if not serve else
                      f"serve (open loop, {args.qps} q/s per replica offered, max batch {B}, mixed {args.mixed_tokens})"
                      if args.qps > 0 else
                      f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"),
             "index_rows": n_rows,
-            "index": "replicated per GPU" if serve else "sharded (all_to_all merge)",
+            "index": "replicated per GPU" if (serve or overlap) else "sharded (all_to_all merge)",
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
             "graphs": llm.use_graphs,

@@ -103,14 +103,19 @@ class LLMEngine:
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, prefix_cache: bool = True,
                  tp_group=None, tp_size: int = 1, tp_rank: int = 0, interleaved_mlp: bool = True,
                  part_size: int = 512, kv_memory_fraction: float = 0.85, mixed_prefill_tokens: int = 0,
-                 pipeline_decode: bool = True):
+                 pipeline_decode: bool = True, shared_model: LlamaModel | None = None):
+        """``shared_model``: serve with another engine's ``LlamaModel`` (one copy of the weights, a
+        KV pool / scheduler / HIP graphs of this engine's own; e.g. two engines on two streams whose
+        prefill and decode phases overlap: bench.py --mode overlap)."""
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
         self.is_gpu = self.device.type == "cuda"
         self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank
         own_weights = weights is None  # a dict built here may be consumed while it is converted
-        if weights is None:
+        if shared_model is not None:
+            weights = {}
+        elif weights is None:
             if checkpoint:
                 from ..models import load_decoder_checkpoint
 
@@ -119,15 +124,18 @@ class LLMEngine:
             else:
                 weights = random_decoder_weights(cfg, self.device, seed=seed, tp_rank=tp_rank, tp_size=tp_size,
                                                  interleave_mlp=interleaved_mlp)
-        self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
-                                interleaved_mlp=interleaved_mlp, consume=own_weights)
+        if shared_model is not None:
+            self.model = shared_model
+        else:
+            self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
+                                    interleaved_mlp=interleaved_mlp, consume=own_weights)
         del weights
-        if self.is_gpu:
+        if self.is_gpu and shared_model is None:
             # the caller's weight dict held the row-major originals while the model converted them
             # to the fragment layout: return those blocks to the device before the KV pool is sized
             # from the free memory (cached blocks are not "free")
             torch.cuda.empty_cache()
-        if tp_size > 1 and self.is_gpu:
+        if tp_size > 1 and self.is_gpu and shared_model is None:
             from ..parallel.custom_allreduce import maybe_create
 
             self.model.custom_ar = maybe_create(tp_group, self.device, tp_size)

@@ -101,8 +101,12 @@ def fill_info(docs: list[StoredDocument], context_size: int = 8000, max_tokens_s
 class RAGPipeline:
     def __init__(self, embedder, index, llm: LLMEngine, documents: dict, system_text: str = "",
                  context_size: int = 8000, max_scores_n: int = 5, top_n: int = 5, related_n: int = 5,
-                 same_question_distance: float = 0.05, max_documents: int = 3, max_tokens_share: float = 0.15):
+                 same_question_distance: float = 0.05, max_documents: int = 3, max_tokens_share: float = 0.15,
+                 retrieve_lock=None):
+        """``retrieve_lock``: held around retrieval + prompt building when several pipelines (each
+        with its own LLMEngine) share one embedder / index from different threads."""
         self.embedder, self.index, self.llm = embedder, index, llm
+        self._retrieve_lock = retrieve_lock
         self.documents = documents
         self.system_text = system_text
         self.context_size = context_size
@@ -177,9 +181,15 @@ class RAGPipeline:
         prompt chunks into the running decode steps)."""
         params = params or SamplingParams(max_new_tokens=1024)
         t0 = time.perf_counter()
-        retrieved = self.retrieve(questions, bot_group)
-        t_ret = time.perf_counter()
-        token_lists, used_docs = self.build_prompts(questions, retrieved, now)
+        if self._retrieve_lock is not None:
+            with self._retrieve_lock:
+                retrieved = self.retrieve(questions, bot_group)
+                t_ret = time.perf_counter()
+                token_lists, used_docs = self.build_prompts(questions, retrieved, now)
+        else:
+            retrieved = self.retrieve(questions, bot_group)
+            t_ret = time.perf_counter()
+            token_lists, used_docs = self.build_prompts(questions, retrieved, now)
         t_prompt = time.perf_counter()
         rids = []
         for q, toks, ret, used in zip(questions, token_lists, retrieved, used_docs):

@@ -56,3 +56,14 @@ def test_bench_two_gloo_ranks():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + TINY
     _check(_run(cmd), 2)
+
+
+def test_bench_overlap_mode_single_process():
+    """--mode overlap: two engines sharing one weight copy, each on its own thread / stream, batches
+    alternating; the timed region answers every question once (2 timed batches of 4)."""
+    args = [a for a in TINY]
+    args[args.index("--steps") + 1] = "2"
+    args[args.index("--warmup") + 1] = "2"
+    d = _run([sys.executable, "bench.py", "--gpus", "1", "--mode", "overlap", *args])
+    assert d["steps"] == 2 and d["value"] > 0 and d["config"]["mode"].startswith("overlap")
+    assert d["value"] == pytest.approx(8 / (2 * d["ms_per_step"] / 1000.0), rel=0.02)
