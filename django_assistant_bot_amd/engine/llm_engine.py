@@ -417,7 +417,6 @@ class LLMEngine:
 
     def _run_prefill(self, chunks):
         t0 = time.perf_counter()
-        dev = self.device
         B = len(chunks)
         T = sum(n for _, _, n in chunks)
         ids = np.empty(T, dtype=np.int32)
@@ -436,7 +435,7 @@ class LLMEngine:
             ctx[i] = s + n
         bt = torch.zeros((B, self.max_blocks_per_seq), dtype=torch.int32)
         self._build_block_tables([r.seq for r, _, _ in chunks], bt)
-        to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
+        to = self._h2d
         meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
                         cu_q=to(cu), max_q=max(n for _, _, n in chunks))
         with self.timer.phase("prefill"):
@@ -446,7 +445,7 @@ class LLMEngine:
         self.stats["prefill_steps"] += 1
         reqs, toks = [], []
         if last_rows:
-            sel = torch.as_tensor([int(cu[i + 1]) - 1 for i in last_rows], dtype=torch.long).to(dev)
+            sel = self._h2d(torch.as_tensor([int(cu[i + 1]) - 1 for i in last_rows], dtype=torch.long))
             logits = self.model.logits(hidden.index_select(0, sel))
             reqs = [chunks[i][0] for i in last_rows]
             toks = self._sample(logits, reqs, to_host=not self.is_gpu)
@@ -481,6 +480,15 @@ class LLMEngine:
                 r.preempted = 0
                 self.running.append(r)
                 self._accept_token(r, int(t), now)
+
+    def _h2d(self, a):
+        """Host array -> device tensor on the current stream, from pinned memory on the GPU so the
+        copy is asynchronous (a pageable copy blocks the host until the stream reaches it, so the
+        next prefill chunk could not be enqueued behind the running one)."""
+        t = torch.as_tensor(a)
+        if not self.is_gpu:
+            return t
+        return t.pin_memory().to(self.device, non_blocking=True)
 
     def _run_mixed(self, batch: list, chunks):
         """Prefill chunks + one decode token per running sequence in one forward (see ``step``)."""
@@ -618,10 +626,10 @@ class LLMEngine:
         topp = torch.tensor([r.params.top_p for r in reqs], dtype=torch.float32)
         cnt = torch.tensor([r.rng_base + len(r.out) for r in reqs], dtype=torch.int64)
         if self.is_gpu:
-            d = self.device
             fast = all((0 < r.params.top_k <= ops.kernels.SAMPLE_FAST_MAX_K) or not r.params.do_sample
                        or r.params.temperature <= 0 for r in reqs)
-            toks = ops.sample_tokens(logits, temps.to(d), topk.to(d), topp.to(d), self.seed, cnt.to(d), fast=fast)
+            h = self._h2d
+            toks = ops.sample_tokens(logits, h(temps), h(topk), h(topp), self.seed, h(cnt), fast=fast)
             toks = self._tp_sync_tokens(toks)
             return toks.cpu().tolist() if to_host else toks
         g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
