@@ -17,7 +17,6 @@ import json
 import os
 import sys
 import time
-import types
 
 import numpy as np
 import torch

@@ -11,7 +11,6 @@ import random
 
 import numpy as np
 import pytest
-import torch
 
 from django_assistant_bot_amd.ops import native
 
