@@ -10,6 +10,8 @@ host-side control plane.  The layout comes from the settings (``assistant.conf``
   searches scan all shards and gather the partial top-k to rank 0 (12 B per hit).
 * ``EMBED_DP`` = D     -- ranks 0..D-1 hold an encoder replica; a large ``/embeddings/`` batch (ingest)
   is split D ways (each rank receives only its texts) and the vectors are gathered to rank 0.
+  Document ingest (``/index/{name}/ingest``) is rank-local instead: each text goes to the encoder
+  rank that owns its row's shard, which embeds it and writes its shard from HBM.
 * ``GEN_TP`` = T       -- W / T generator replicas; replica g is the TP group of ranks gT..gT+T-1.
 
 (0 for S or D means "every rank".)  Rank 0 serves HTTP.  Two independent control channels:
@@ -97,7 +99,8 @@ def _subgroup(n: int, world: int):
 
 
 # command op codes (header word 0 of the control broadcast)
-_OPS = ("stop", "name", "index_upsert", "index_delete", "index_search", "index_sizes", "embed", "fault", "stats")
+_OPS = ("stop", "name", "index_upsert", "index_delete", "index_search", "index_sizes", "embed", "fault", "stats",
+        "index_ingest")
 _CODE = {op: i for i, op in enumerate(_OPS)}
 _NORM = {None: -1, False: 0, True: 1}
 
@@ -168,7 +171,8 @@ class Node:
         self.commands = 0
         self.healthy = True
         self.last_error = ""
-        self.stats = {"upsert_bytes_recv": 0, "embed_bytes_recv": 0, "ctrl_s": 0.0, "llm_steps": 0,
+        self.stats = {"upsert_bytes_recv": 0, "embed_bytes_recv": 0, "ingest_bytes_recv": 0,
+                      "ingest_vec_bytes_recv": 0, "ctrl_s": 0.0, "llm_steps": 0,
                       "link_bytes_sent": 0}
         self._side = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
         self._llm_thread: threading.Thread | None = None
@@ -202,7 +206,8 @@ class Node:
             if not self.healthy:
                 raise NodeFault(f"node group is broken ({self.last_error}); waiting for the restart")
             try:
-                if op in ("index_upsert", "index_delete", "index_search") and payload[0] not in self.names:
+                if op in ("index_upsert", "index_delete", "index_search", "index_ingest") and \
+                        payload[0] not in self.names:
                     self._run("name", payload[0])
                 return self._run(op, payload)
             except Exception as exc:
@@ -470,10 +475,127 @@ class Node:
     def embed_ctrl_group(self):
         return self.ctrl
 
+    # ------------------------------------------------------------------ rank-local ingest
+    def _ingest_plan(self, ids) -> np.ndarray:
+        """Encoder rank of each row: the shard owner itself when it holds an encoder (the default
+        layout, S = D = W), else owner % D (the vectors of those rows then move to their owner)."""
+        owner = np.asarray(ids, dtype=np.int64) % self.plan.index_shards
+        return np.where(owner < self.plan.embed_dp, owner, owner % self.plan.embed_dp)
+
+    def _hdr_index_ingest(self, p):
+        name, model, ids, texts, docs, groups, normalize, ret = p
+        dim = self.embeds[model].dim
+        return [self.names.index(name), self.embed_names.index(model), len(ids), int(docs is not None),
+                int(groups is not None), _NORM[normalize], int(ret), dim]
+
+    def _op_index_ingest(self, h, p):
+        """Embed + index write where the row lives: rank 0 routes each text (not a vector) to the
+        encoder rank that owns the row's shard (``id % S``); that rank embeds its texts and adds
+        the vectors to its own shard from HBM.  With the default layout no vector crosses a link;
+        only the per-(encoder, owner) counts are broadcast and the new index size is reduced.
+        ``ret`` gathers the vectors to rank 0 as well (for callers that store them in the DB, as
+        the reference's embedding step does: assistant/processing/documents/steps/embeddings.py)."""
+        name, model, n, has_docs, has_groups = self.names[h[1]], self.embed_names[h[2]], h[3], h[4], h[5]
+        norm, ret, dim = {-1: None, 0: False, 1: True}[h[6]], h[7], h[8]
+        S, D = self.plan.index_shards, self.plan.embed_dp
+        cnt = torch.zeros((D, S), dtype=torch.int64)
+        if self.rank == 0:
+            _, _, ids, texts, docs, groups, _, _ = p
+            enc = self._ingest_plan(ids)
+            owner = ids % S
+            # rows grouped by (encoder, owner): each encoder's share is contiguous per owner
+            order = np.lexsort((owner, enc))
+            np.add.at(cnt.numpy(), (enc, owner), 1)
+        self._bcast(cnt)
+        c = cnt.numpy()
+        g = self.embed_ctrl_group()
+        mine_ints = mine_texts = None
+        if self.rank == 0:
+            start = np.concatenate([[0], np.cumsum(c.sum(1))])
+            for e in range(D):
+                rows = order[start[e]:start[e + 1]]
+                ints = np.stack([ids[rows], docs[rows] if has_docs else np.zeros(len(rows), np.int64),
+                                 groups[rows].astype(np.int64) if has_groups else np.zeros(len(rows), np.int64)])
+                tx = [texts[i] for i in rows]
+                if e == 0:
+                    mine_ints, mine_texts = ints, tx
+                    continue
+                if not len(rows):
+                    continue
+                offs, flat = _texts_words(tx)
+                dist.send(_i64(ints), dst=e, group=g)
+                dist.send(_i64(offs), dst=e, group=g)
+                dist.send(_i64([len(flat)]), dst=e, group=g)
+                if len(flat):
+                    dist.send(_i64(flat), dst=e, group=g)
+        elif self.in_embed and c[self.rank].sum():
+            m = int(c[self.rank].sum())
+            ints, offs, ln = torch.zeros((3, m), dtype=torch.int64), torch.zeros(m + 1, dtype=torch.int64), \
+                torch.zeros(1, dtype=torch.int64)
+            dist.recv(ints, src=0, group=g)
+            dist.recv(offs, src=0, group=g)
+            dist.recv(ln, src=0, group=g)
+            flat = torch.zeros(int(ln), dtype=torch.int64)
+            if int(ln):
+                dist.recv(flat, src=0, group=g)
+            self.stats["ingest_bytes_recv"] += 8 * (ints.numel() + offs.numel() + 1 + flat.numel())
+            mine_ints, mine_texts = ints.numpy(), _words_texts(offs.numpy(), flat.numpy())
+        vecs = None
+        if self.in_embed and mine_texts:
+            vecs = self.embeds[model].embed(mine_texts, normalize=norm, out_dtype=torch.float32)
+        # index writes: own rows from HBM; rows of encoder-less shards (owner >= D) travel once
+        if self.in_index:
+            idx = self._index(name, dim)
+            if self.rank < D and vecs is not None:
+                lo = int(c[self.rank, :self.rank].sum())
+                k = int(c[self.rank, self.rank])
+                if k:
+                    a = mine_ints[:, lo:lo + k]
+                    idx.add(a[0], vecs[lo:lo + k], a[1] if has_docs else None,
+                            a[2].astype(np.int32) if has_groups else None)
+        for owner in range(D, S):
+            src = owner % D
+            k = int(c[src, owner])
+            if not k:
+                continue
+            if self.rank == src:
+                lo = int(c[src, :owner].sum())
+                dist.send(_i64(mine_ints[:, lo:lo + k]), dst=owner, group=g)
+                dist.send(vecs[lo:lo + k].cpu().contiguous(), dst=owner, group=g)
+            elif self.rank == owner:
+                ints, v = torch.zeros((3, k), dtype=torch.int64), torch.zeros((k, dim), dtype=torch.float32)
+                dist.recv(ints, src=src, group=g)
+                dist.recv(v, src=src, group=g)
+                self.stats["ingest_vec_bytes_recv"] += v.numel() * 4
+                a = ints.numpy()
+                self._index(name, dim).add(a[0], v, a[1] if has_docs else None,
+                                           a[2].astype(np.int32) if has_groups else None)
+        total = self._index_total(len(self._index(name, dim).local)) if self.in_index else None
+        if not ret:
+            return total
+        # optional: vectors back to rank 0, in request order
+        if self.rank == 0:
+            out = torch.empty((n, dim), dtype=torch.float32)
+            start = np.concatenate([[0], np.cumsum(c.sum(1))])
+            if vecs is not None:
+                out[torch.from_numpy(order[start[0]:start[1]])] = vecs.cpu()
+            for e in range(1, D):
+                m = int(c[e].sum())
+                if m:
+                    v = torch.zeros((m, dim), dtype=torch.float32)
+                    dist.recv(v, src=e, group=g)
+                    out[torch.from_numpy(order[start[e]:start[e + 1]])] = v
+            return total, out
+        if self.in_embed and vecs is not None:
+            dist.send(vecs.cpu().contiguous(), dst=0, group=g)
+        return None
+
     def _op_stats(self, h, p):
-        """Per-rank control-plane counters gathered to rank 0: [ctrl_s, llm_steps, upsert bytes, embed bytes]."""
+        """Per-rank control-plane counters gathered to rank 0: [ctrl_s, llm_steps, upsert bytes, embed bytes,
+        ingest text bytes, ingest vector bytes] (bytes received by that rank)."""
         t = torch.tensor([self.stats["ctrl_s"], self.stats["llm_steps"], self.stats["upsert_bytes_recv"],
-                          self.stats["embed_bytes_recv"]], dtype=torch.float64)
+                          self.stats["embed_bytes_recv"], self.stats["ingest_bytes_recv"],
+                          self.stats["ingest_vec_bytes_recv"]], dtype=torch.float64)
         if self.world == 1:
             return t[None]
         parts = [torch.zeros_like(t) for _ in range(self.world)] if self.rank == 0 else None
@@ -841,6 +963,42 @@ class NodeIndexes:
                                                None if grp is None else grp.astype(np.int32)))
         self._counts[name] = n
         return n
+
+    def ingest(self, name, model, ids, texts, doc_ids=None, groups=None, normalize=None,
+               return_vectors=False):
+        """Embed ``texts`` with ``model`` and upsert them as rows ``ids``, rank-locally (see
+        ``Node._op_index_ingest``).  Returns the index size, or (size, [n, dim] vectors)."""
+        model = str(model).lower()
+        if model not in self.node.embed_names:
+            raise ValueError(f"embedder {model} is not served")
+        ids = np.asarray(ids)
+        if ids.ndim != 1 or (len(ids) and not np.issubdtype(ids.dtype, np.integer)):
+            raise ValueError("ids must be a list of integers")
+        ids = ids.astype(np.int64)
+        if (ids < 0).any():
+            raise ValueError("ids must be >= 0")
+        if len(texts) != len(ids) or not all(isinstance(t, str) for t in texts):
+            raise ValueError("texts must hold one string per id")
+        dim = self.node.embeds[model].dim
+        if self._dims.get(name, dim) != dim:
+            raise ValueError(f"index {name} has dim {self._dims[name]}, embedder {model} gives {dim}")
+        docs = None if doc_ids is None else np.asarray(doc_ids)
+        if docs is not None and (docs.shape != ids.shape or (len(docs) and not np.issubdtype(docs.dtype, np.integer))):
+            raise ValueError("doc_ids must be one integer per id")
+        grp = None if groups is None else np.asarray(groups)
+        if grp is not None and (grp.shape != ids.shape or (len(grp) and not np.issubdtype(grp.dtype, np.integer))
+                                or (grp < 0).any() or (grp >= 2 ** 31).any()):
+            raise ValueError("groups must be one integer in [0, 2^31) per id")
+        if len(ids) == 0:
+            n = self._counts.get(name, 0)
+            return (n, torch.zeros((0, dim))) if return_vectors else n
+        self._dims.setdefault(name, dim)
+        out = self.node.command("index_ingest", (name, model, ids, list(texts),
+                                                 None if docs is None else docs.astype(np.int64),
+                                                 None if grp is None else grp.astype(np.int32), normalize,
+                                                 bool(return_vectors)))
+        self._counts[name] = out[0] if return_vectors else out
+        return out
 
     def delete(self, name, ids) -> int:
         if name not in self._dims:

@@ -6,6 +6,8 @@ Endpoints (request/response shapes of the reference where it had them):
   POST /index/{name}/upsert     {ids, vectors, doc_ids?, groups?}      -> {count}
   POST /index/{name}/delete     {ids}                                  -> {removed}
   POST /index/{name}/search     {queries, k, groups?, allowed?}        -> {ids, distances, doc_ids}
+  POST /index/{name}/ingest     {model, ids, texts, doc_ids?, groups?, return_vectors?}
+                                -> {count[, embeddings]}  (embed + upsert; rank-local in node mode)
   GET  /health                  loaded models, device
   GET  /metrics                 Prometheus text (engine counters, queue depths, HBM use)
 
@@ -68,6 +70,15 @@ class UpsertRequest(BaseModel):
     vectors: List[List[float]]
     doc_ids: Optional[List[int]] = None
     groups: Optional[List[int]] = None
+
+
+class IngestRequest(BaseModel):
+    model: str
+    ids: List[int]
+    texts: List[str]
+    doc_ids: Optional[List[int]] = None
+    groups: Optional[List[int]] = None
+    return_vectors: bool = False
 
 
 class DeleteRequest(BaseModel):
@@ -237,6 +248,33 @@ async def index_upsert(name: str, request: UpsertRequest):
         raise HTTPException(status_code=400, detail=f"index {name} has dim {dim}")
     n = await _call_index(index_backend.upsert, name, request.ids, request.vectors, request.doc_ids, request.groups)
     return {"count": n}
+
+
+@app.post("/index/{name}/ingest")
+async def index_ingest(name: str, request: IngestRequest):
+    """Document ingest in one call: embed the texts and write them into the index.  Node mode runs
+    it where the rows live (each text goes to the rank owning its shard, which embeds it and writes
+    its own shard from HBM: no vector crosses a link); one process embeds then upserts."""
+    _index_guard()
+    if len(request.ids) != len(request.texts):
+        raise HTTPException(status_code=400, detail="ids and texts differ in length")
+    if hasattr(index_backend, "ingest"):
+        out = await _call_index(index_backend.ingest, name, request.model, request.ids, request.texts,
+                                request.doc_ids, request.groups, None, request.return_vectors)
+        if request.return_vectors:
+            return {"count": out[0], "embeddings": out[1].tolist()}
+        return {"count": out}
+    embedder = embedders.get(request.model.lower())
+    if embedder is None:
+        raise HTTPException(status_code=400, detail="Model is not supported")
+    if not request.ids:
+        return {"count": index_backend.size(name), **({"embeddings": []} if request.return_vectors else {})}
+    vecs = await embedder.embeddings(request.texts)
+    dim = index_backend.dim(name)
+    if dim is not None and len(vecs[0]) != dim:
+        raise HTTPException(status_code=400, detail=f"index {name} has dim {dim}")
+    n = await _call_index(index_backend.upsert, name, request.ids, vecs, request.doc_ids, request.groups)
+    return {"count": n, **({"embeddings": vecs} if request.return_vectors else {})}
 
 
 @app.post("/index/{name}/delete")

@@ -66,6 +66,18 @@ def test_index_roundtrip(client):
     assert client.post("/index/none/search", json={"queries": [[1, 0, 0, 0]], "k": 3}).json()["ids"] == [[]]
 
 
+def test_index_ingest_single_process(client):
+    texts = ["alpha beta", "gamma delta", "epsilon zeta"]
+    r = client.post("/index/docs/ingest", json={"model": "TINY-BERT", "ids": [5, 6, 7], "texts": texts,
+                                                "doc_ids": [1, 1, 2], "return_vectors": True}).json()
+    assert r["count"] == 3 and len(r["embeddings"]) == 3
+    q = client.post("/embeddings/", json={"model": "tiny-bert", "texts": [texts[1]]}).json()["embeddings"]
+    hit = client.post("/index/docs/search", json={"queries": q, "k": 1}).json()
+    assert hit["ids"] == [[6]] and hit["doc_ids"] == [[1]]
+    assert client.post("/index/docs/ingest", json={"model": "x", "ids": [1], "texts": ["a"]}).status_code == 400
+    assert client.post("/index/docs/ingest", json={"model": "tiny-bert", "ids": [1], "texts": []}).status_code == 400
+
+
 def test_health_and_metrics(client):
     h = client.get("/health").json()
     assert h["status"] == "ok" and "tiny-bert" in h["embedders"] and "tiny-llama" in h["providers"]
