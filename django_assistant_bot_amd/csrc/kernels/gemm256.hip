@@ -454,20 +454,26 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       if constexpr (RES) {
         rR = make_rsrc(p.residual + (size_t)m0 * p.ldr, (unsigned)(c_rows * p.ldr * 2));
       }
+      // RES: all 16 residual vectors of the wave are requested before the first store (64 VGPRs,
+      // the dead fragment registers), so one vmcnt(0) per tile instead of one per 128-row half
+      // (the second also waited for the first half's stores: gfx9 counts stores in vmcnt).  Within
+      // noise of the per-half form (profiles/gemm_epilogue_probe.md): what the residual costs at
+      // short K (+25-35 % at K = 768) is the chip-wide burst of residual reads when every CU reaches
+      // its epilogue at the same time, not the round trips.
+      u32x4 rvv[2][4][2];
+      if constexpr (RES) {
 #pragma unroll
-      for (int ih = 0; ih < 2; ++ih) {
-        // RES: the half-tile's 8 residual vectors are requested together (one round trip per
-        // 128 rows instead of one per 16-B store: the stores in between keep loads from passing)
-        u32x4 rvv[4][2];
-        if constexpr (RES) {
+        for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int jh = 0; jh < 2; ++jh)
-              rvv[i][jh] = __builtin_amdgcn_raw_buffer_load_b128(
+              rvv[ih][i][jh] = __builtin_amdgcn_raw_buffer_load_b128(
                   rR, (unsigned)(((128 * ih + 64 * wr + 16 * i + e_li) * p.ldr + n0 + 128 * jh + 32 * e_wc + cq) * 2), 0,
                   0);
-        }
+      }
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int mr = 128 * ih + 64 * wr + 16 * i + e_li;
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
               for (int r = 0; r < 8; ++r) o[r] = gelu_erf(o[r]);
             }
             if constexpr (RES) {
-              const u32x4 rv = rvv[i][jh];
+              const u32x4 rv = rvv[ih][i][jh];
 #pragma unroll
               for (int q = 0; q < 4; ++q) {  // round like a bf16 GEMM output, then the bf16 add (HF)
                 o[2 * q] = bf2f(f2bf(o[2 * q])) + __uint_as_float(rv[q] << 16);
@@ -502,7 +508,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
             if constexpr (BIAS || RES) {
-              if (i == 0 && jh == 0 && (RES || ih == 0)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              if (i == 0 && jh == 0 && ih == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
           }
