@@ -62,12 +62,14 @@ def main():
     ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--prompt", type=int, default=1100)
+    ap.add_argument("--block-size", type=int, default=64, help="paged-KV block (tokens): one engine per value")
     args = ap.parse_args()
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
     from django_assistant_bot_amd.models import llama as llama_mod
 
     torch.manual_seed(0)
-    eng = LLMEngine("llama-3-8b", device="cuda", max_batch=args.batch, kv_cache_gb=120, max_prefill_tokens=32768)
+    eng = LLMEngine("llama-3-8b", device="cuda", max_batch=args.batch, kv_cache_gb=120, max_prefill_tokens=32768,
+                    block_size=args.block_size)
     g = torch.Generator().manual_seed(1)
     sp = SamplingParams(max_new_tokens=6000, ignore_eos=True)
     prompts = [torch.randint(0, 128000, (args.prompt + int(torch.randint(-100, 100, (1,), generator=g)),),
