@@ -29,15 +29,17 @@ def _free_port():
     return p
 
 
-def _entry(rank, world, port, embed_dp, out_path):
+def _entry(rank, world, port, embed_dp, out_path, device="cpu"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port), GPU_SERVICE_DEVICE="cpu")
+                      MASTER_PORT=str(port), GPU_SERVICE_DEVICE=device)
     torch.set_num_threads(1)
     from django_assistant_bot_amd.parallel.node import NodePlan
     from gpu_service import node_main
 
+    # device "cuda": every rank on the one GPU of the box (gloo control plane): the encoder runs
+    # the native kernels and the shard is written from HBM
     node = node_main.setup(embedders=["tiny-bert"], providers=[], plan=NodePlan(world, embed_dp=embed_dp),
-                           backend="gloo", device_type="cpu")
+                           backend="gloo", device_type=device)
     try:
         if rank == 0:
             _drive(node, out_path)
@@ -69,10 +71,10 @@ def _drive(node, out_path):
     body = r.json()
     res["count2"] = body["count"]
     got = torch.tensor(body["embeddings"])
-    ref = node.embeds["tiny-bert"].embed(texts[half:], out_dtype=torch.float32)
+    ref = node.embeds["tiny-bert"].embed(texts[half:], out_dtype=torch.float32).cpu()
     res["vec_err"] = float((got - ref).abs().max())
     # every row is found by its own embedding, with its doc id
-    q = node.embeds["tiny-bert"].embed(texts[::10], out_dtype=torch.float32)
+    q = node.embeds["tiny-bert"].embed(texts[::10], out_dtype=torch.float32).cpu()
     s = c.post("/index/docs/search", json={"queries": q.tolist(), "k": 1}).json()
     res["top1"] = [x[0] for x in s["ids"]]
     res["top1_doc"] = [x[0] for x in s["doc_ids"]]
@@ -93,11 +95,25 @@ def _drive(node, out_path):
     torch.save(res, out_path)
 
 
+def _run(tmp_path, embed_dp, device="cpu"):
+    out = str(tmp_path / "ingest.pt")
+    mp.spawn(_entry, args=(W, _free_port(), embed_dp, out, device), nprocs=W, join=True)
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.gpu
+def test_rank_local_ingest_on_gpu(tmp_path):
+    """Three ranks on the one GPU: native encoder, shards in HBM; the same checks as on CPU."""
+    res = _run(tmp_path, 2, "cuda")
+    assert res["count1"] == N // 2 and res["count2"] == N
+    assert res["vec_err"] < 1e-3
+    assert res["top1"] == res["want"]
+    assert res["ingest_vec_bytes"][1] == 0 and res["ingest_vec_bytes"][2] == res["owned"][2] * res["dim"] * 4
+
+
 @pytest.mark.parametrize("embed_dp", [0, 2])
 def test_rank_local_ingest(tmp_path, embed_dp):
-    out = str(tmp_path / "ingest.pt")
-    mp.spawn(_entry, args=(W, _free_port(), embed_dp, out), nprocs=W, join=True)
-    res = torch.load(out, weights_only=True)
+    res = _run(tmp_path, embed_dp)
     print({k: res[k] for k in ("ingest_text_bytes", "ingest_vec_bytes", "vec_err")})
     assert res["count1"] == N // 2 and res["count2"] == N
     assert res["vec_err"] < 1e-4
