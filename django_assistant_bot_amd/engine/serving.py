@@ -250,10 +250,6 @@ def health() -> dict:
     return {"healthy": not bad, "unhealthy_workers": bad}
 
 
-def loaded_models() -> dict:
-    return {"embedders": sorted(_emb), "providers": sorted(_llm)}
-
-
 def engine_metrics() -> dict:
     import torch
 

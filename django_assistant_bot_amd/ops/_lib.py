@@ -54,10 +54,6 @@ def stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def on_gpu(t: torch.Tensor) -> bool:
-    return t.is_cuda
-
-
 def expect(cond: bool, msg: str) -> None:
     if not cond:
         raise ValueError(msg)
