@@ -1,8 +1,8 @@
-"""Tensor-parallel generation on the GPU path: W = 2 / 4 ranks of ``LLMEngine``
+"""Tensor-parallel generation on the GPU path: W = 2 / 4 / 8 ranks of ``LLMEngine``
 share the box's one GPU (gloo default group; one-shot IPC all-reduce for the TP partial sums,
 captured inside the HIP-graph decode; split-K decode GEMMs with bf16 partial sums; sampled tokens
 broadcast from TP rank 0), at the Llama-3-70B head layout (64 query / 8 KV heads: at TP 4 each rank
-holds 16 query and 2 KV heads).
+holds 16 query and 2 KV heads, at TP 8 -- the degree BASELINE config 5 names -- 8 and 1).
 
 Parity with TP = 1: the TP ranks' greedy tokens are checked against a TP = 1 model of the full
 weights with teacher forcing (every generated position scored on the TP-generated prefix): the
@@ -75,7 +75,7 @@ def _body(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_tp_engine_on_gpu_matches_tp1(tmp_path, world):
     from django_assistant_bot_amd.models.llama import AttnMeta, KVCache, LlamaModel
     from django_assistant_bot_amd.models.weights import _gate_up, random_decoder_weights
