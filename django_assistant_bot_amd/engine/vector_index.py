@@ -245,7 +245,7 @@ class VectorIndex:
         if queries.ndim == 1:
             queries = queries[None]
         nq = queries.shape[0]
-        if self.n == 0 or k <= 0:
+        if self.n == 0 or k <= 0 or nq == 0:
             z = torch.full((nq, max(k, 0)), -1, dtype=torch.int64, device=self.device)
             return torch.full((nq, max(k, 0)), float("-inf"), device=self.device), z, z.clone()
         got = None

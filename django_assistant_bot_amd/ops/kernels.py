@@ -713,6 +713,9 @@ def topk_rows(scores, k, index_base=0, want_global=False):
     ``want_global``, (values, idx + index_base as int64).  Long rows use the two-stage kernel."""
     rows, n = scores.shape
     expect(1 <= k <= min(n, 1024), "1 <= k <= min(n, 1024)")
+    if rows == 0:  # e.g. a rank with no queries in a sharded search (an empty view's strides are arbitrary)
+        return (torch.empty((0, k), dtype=torch.float32, device=scores.device),
+                torch.empty((0, k), dtype=torch.int64 if want_global else torch.int32, device=scores.device))
     if not scores.is_cuda:
         v, i = ref.topk_rows(scores, k)
         return (v, i.long() + index_base) if want_global else (v, i)
