@@ -1,4 +1,4 @@
-"""gpu_service node mode on the GPU path: two ranks share the box's one MI355X (gloo control and data
+"""gpu_service node mode on the GPU path: two (or four) ranks share the box's one MI355X (gloo control and data
 plane; RCCL needs a device per rank), each with a tiny-llama generator replica (HIP-graph decode) and
 a tiny-bert encoder replica, the index sharded over both.  Over HTTP (FastAPI TestClient on rank 0):
 a DP-split /embeddings/ batch equals one encoder's vectors, /dialog/ answers from both replicas
@@ -17,9 +17,6 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 pytest.importorskip("fastapi")
 
-W = 2
-
-
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -28,7 +25,7 @@ def _free_port():
     return p
 
 
-def _entry(rank, world, port, out_path):
+def _entry(rank, world, port, out_path, gen_tp=1):
     import traceback
 
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -36,7 +33,7 @@ def _entry(rank, world, port, out_path):
     from django_assistant_bot_amd.parallel.node import NodePlan
     from gpu_service import node_main
 
-    node = node_main.setup(embedders=["tiny-bert"], providers=["tiny-llama"], plan=NodePlan(world),
+    node = node_main.setup(embedders=["tiny-bert"], providers=["tiny-llama"], plan=NodePlan(world, gen_tp=gen_tp),
                            backend="gloo", device_type="cuda", max_batch=8)
     try:
         if rank == 0:
@@ -100,12 +97,15 @@ def _drive(node, out_path):
     torch.save(res, out_path)
 
 
-def test_node_service_on_gpu(tmp_path):
+@pytest.mark.parametrize("world,gen_tp", [(2, 1), (4, 2)])
+def test_node_service_on_gpu(tmp_path, world, gen_tp):
+    """(4, 2): two TP-2 generator replicas (leader-driven lock step inside each, IPC all-reduce in the
+    decode graphs), four encoder replicas and four index shards."""
     out = str(tmp_path / "node.pt")
     try:
-        mp.spawn(_entry, args=(W, _free_port(), out), nprocs=W, join=True)
+        mp.spawn(_entry, args=(world, _free_port(), out, gen_tp), nprocs=world, join=True)
     except Exception:
-        for r in range(W):
+        for r in range(world):
             if os.path.exists(out + f".err{r}"):
                 print(f"rank {r}:\n" + open(out + f".err{r}").read())
         raise
