@@ -136,3 +136,33 @@ def test_dp_corpus_embedding_on_gpu(tmp_path):
     assert r0["total"] == r1["total"] == 301
     assert r0["local"] == r0["own"] and r1["local"] == r1["own"] and r0["own"] + r1["own"] == 301
     assert r0["err"] < 1e-3
+
+
+def _snap_entry(rank, world, port, directory):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from django_assistant_bot_amd.parallel import dist as pdist
+    from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
+
+    pdist.init(backend="gloo", device_type="cuda")
+    try:
+        g = torch.Generator().manual_seed(3)
+        n, dim = 5000, 256
+        vecs = torch.randn(n, dim, generator=g)
+        ids = np.arange(n, dtype=np.int64) * 7 + 1
+        idx = ShardedIndex(dim, "cuda")
+        idx.add(ids, vecs, doc_ids=ids // 10, groups=np.zeros(n, dtype=np.int32))
+        idx.remove(ids[:5])
+        idx.save(directory)
+        torch.distributed.barrier()
+        back = ShardedIndex.load(directory, "cuda")
+        q = torch.randn(4, dim, generator=g)
+        for x, y in zip(idx.search(q, 20), back.search(q, 20)):
+            assert torch.equal(x.cpu(), y.cpu())
+    finally:
+        pdist.shutdown()
+
+
+def test_sharded_index_snapshot_on_gpu(tmp_path):
+    """Per-rank safetensors shards written from HBM (fragment layout -> row-major) and read back."""
+    mp.spawn(_snap_entry, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
