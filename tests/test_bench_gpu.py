@@ -1,0 +1,51 @@
+"""bench.py on the GPU path with the tiny presets: batch, serve and overlap modes in one process
+(HIP-graph decode, native kernels), and the 2-rank launch shape of ``torch.distributed.run`` with both
+ranks on the one GPU (gloo: RCCL needs a device per rank).  Each run prints exactly one JSON line
+with the driver's keys and a positive whole-job value."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TINY = ["--embed-model", "tiny-bert", "--llm-model", "tiny-llama", "--index-rows", "20000", "--batch", "8",
+        "--max-new-tokens", "8", "--steps", "1", "--warmup", "1"]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(cmd, **env):
+    p = subprocess.run(cmd, cwd=ROOT, env=dict(os.environ, **env), capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["dtype"] == "bf16"
+    return d
+
+
+@pytest.mark.parametrize("mode", ["batch", "serve", "overlap"])
+def test_bench_modes_on_gpu(mode):
+    args = list(TINY)
+    if mode == "overlap":
+        args[args.index("--steps") + 1] = "2"
+        args[args.index("--warmup") + 1] = "2"
+    d = _run([sys.executable, "bench.py", "--mode", mode, *args])
+    assert d["config"]["mode"].startswith(mode) and d["config"]["graphs"] is True
+    assert d["n_gpus"] == 1
+
+
+def test_bench_two_ranks_on_one_gpu():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + TINY
+    d = _run(cmd, DAB_DIST_BACKEND="gloo")
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
