@@ -33,9 +33,11 @@ def _run(cmd, **env):
     return d
 
 
-@pytest.mark.parametrize("mode", ["batch", "serve", "overlap"])
+@pytest.mark.parametrize("mode", ["batch", "serve", "overlap", "qps"])
 def test_bench_modes_on_gpu(mode):
     args = list(TINY)
+    if mode == "qps":  # open loop: a fixed arrival schedule (profiles/fixed_qps.md)
+        mode, args = "serve", args + ["--qps", "20"]
     if mode == "overlap":
         args[args.index("--steps") + 1] = "2"
         args[args.index("--warmup") + 1] = "2"
@@ -44,8 +46,15 @@ def test_bench_modes_on_gpu(mode):
     assert d["n_gpus"] == 1
 
 
-def test_bench_two_ranks_on_one_gpu():
+@pytest.mark.parametrize("tp", [1, 2])
+def test_bench_two_ranks_on_one_gpu(tp):
+    """tp 1: two DP replicas with the index sharded over them; tp 2: one TP-2 generator (IPC
+    all-reduce inside the decode graphs) -- config 5's launch shape at toy size."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2"] + TINY
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2", "--tp", str(tp)] + TINY
     d = _run(cmd, DAB_DIST_BACKEND="gloo")
-    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
+    assert d["n_gpus"] == 2
+    if tp == 1:
+        assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
+    else:
+        assert "tp2" in d["config"]["parallelism"]
