@@ -194,3 +194,42 @@ def test_prefix_blocks_are_shared_from_the_launch_of_their_chunk():
         cold.step()
     assert eng.pop_output(r2).token_ids == cold.pop_output(c2).token_ids
     assert len(eng.pop_output(r1).token_ids) == 6
+
+
+def _preempt_run(eng, prompts, abort_idx=None, steps_before_abort=6):
+    greedy = SamplingParams(max_new_tokens=40, do_sample=False, temperature=0.0, ignore_eos=True)
+    rids = [eng.add_request(p, greedy) for p in prompts]
+    for _ in range(steps_before_abort):
+        eng.step()
+    if abort_idx is not None:
+        assert eng.abort(rids[abort_idx])
+    while eng.has_unfinished():
+        eng.step()
+    return [eng.pop_output(r) for r in rids]
+
+
+def test_preemption_recompute_matches_an_unconstrained_pool():
+    """A KV pool too small for the batch: the youngest sequences are preempted (blocks freed,
+    re-queued, prompt + generated tokens recomputed) and still produce the tokens of a run that never
+    ran dry; an abort in the middle frees its blocks; prompts sharing a 32-token prefix reuse blocks.
+    Every block is free at the end."""
+    w = _weights()
+    shared = list(range(500, 532))
+    prompts = [shared + list(range(10 * i, 10 * i + 8 + 5 * i)) for i in range(6)]
+
+    def engine(blocks):
+        return LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(w), max_batch=8, block_size=16,
+                         num_blocks=blocks, max_prefill_tokens=512, use_graphs=False)
+
+    ref = [o.token_ids for o in _preempt_run(engine(256), prompts)]
+    small = engine(18)  # 6 sequences need up to 6 x 7 blocks
+    outs = _preempt_run(small, prompts)
+    assert small.stats["preemptions"] > 0
+    assert [o.token_ids for o in outs] == ref
+    assert small.blocks.num_free_blocks() == small.blocks.num_blocks()
+    # with an abort: the aborted request ends early, the others are unchanged
+    small = engine(18)
+    outs = _preempt_run(small, prompts, abort_idx=2)
+    assert outs[2].finish_reason == "abort" and len(outs[2].token_ids) < 40
+    assert [o.token_ids for i, o in enumerate(outs) if i != 2] == [t for i, t in enumerate(ref) if i != 2]
+    assert small.blocks.num_free_blocks() == small.blocks.num_blocks()
