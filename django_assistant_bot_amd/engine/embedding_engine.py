@@ -21,6 +21,10 @@ class EmbeddingEngine:
                  checkpoint: str | None = None, seed: int = 0, max_batch_tokens: int = 65536,
                  normalize: bool | None = None):
         self.cfg = encoder_config(model) if isinstance(model, str) else model
+        if checkpoint is None and weights is None:
+            from ..models.configs import checkpoint_dir
+
+            checkpoint = checkpoint_dir(model)  # a local HF directory given as the model name
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
         if weights is None:
             if checkpoint:

@@ -109,6 +109,10 @@ class LLMEngine:
         prefill and decode phases overlap: bench.py --mode overlap)."""
         self.cfg = decoder_config(model) if isinstance(model, str) else model
         cfg = self.cfg
+        if checkpoint is None and weights is None and shared_model is None:
+            from ..models.configs import checkpoint_dir
+
+            checkpoint = checkpoint_dir(model)  # a local HF directory given as the model name
         self.device = torch.device(device if device is not None else ("cuda" if torch.cuda.is_available() else "cpu"))
         self.is_gpu = self.device.type == "cuda"
         self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank

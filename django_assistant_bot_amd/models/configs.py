@@ -7,6 +7,8 @@ directory is given.
 """
 from __future__ import annotations
 
+import json
+import os
 from dataclasses import asdict, dataclass, field, replace
 
 
@@ -109,23 +111,98 @@ def _key(name: str) -> str:
     return _ALIASES.get(k, k)
 
 
+# ------------------------------------------------------------------ local HF checkpoint directories
+# A model name may also be a local HF directory (config.json + *.safetensors [+ tokenizer.json]), as
+# the reference's TransformersEmbedder / TransformersProvider accept (ai/embedders/transformers.py:13,
+# ai/providers/transformers.py:18-20: ``from_pretrained(model_name)``).  The architecture comes from
+# config.json; only the families the native kernels implement are accepted.
+
+def checkpoint_dir(name) -> str | None:
+    """``name`` if it is a local directory with a config.json, else None."""
+    if isinstance(name, str) and os.path.isfile(os.path.join(name, "config.json")):
+        return name
+    return None
+
+
+def _hf(path: str) -> dict:
+    with open(os.path.join(path, "config.json")) as f:
+        return json.load(f)
+
+
+def _label(path: str) -> str:
+    return os.path.basename(os.path.normpath(path)).lower()
+
+
+def encoder_config_from_hf(path: str) -> EncoderConfig:
+    c = _hf(path)
+    if c.get("model_type") != "bert":
+        raise ValueError(f"{path}: model_type {c.get('model_type')!r} is not a BERT encoder")
+    if c.get("hidden_act", "gelu") != "gelu" or c.get("position_embedding_type", "absolute") != "absolute":
+        raise ValueError(f"{path}: only erf-GELU BERT encoders with absolute positions are supported")
+    return EncoderConfig(_label(path), vocab_size=c["vocab_size"], hidden=c["hidden_size"],
+                         layers=c["num_hidden_layers"], heads=c["num_attention_heads"],
+                         intermediate=c["intermediate_size"], max_position=c.get("max_position_embeddings", 512),
+                         type_vocab=c.get("type_vocab_size", 2), eps=c.get("layer_norm_eps", 1e-12))
+
+
+def decoder_config_from_hf(path: str) -> DecoderConfig:
+    c = _hf(path)
+    if c.get("model_type") != "llama":
+        raise ValueError(f"{path}: model_type {c.get('model_type')!r} is not a Llama decoder")
+    if c.get("hidden_act", "silu") != "silu" or c.get("attention_bias") or c.get("mlp_bias"):
+        raise ValueError(f"{path}: only bias-free SiLU Llama decoders are supported")
+    heads = c["num_attention_heads"]
+    if c.get("head_dim", c["hidden_size"] // heads) * heads != c["hidden_size"]:
+        raise ValueError(f"{path}: head_dim x heads must equal hidden_size")
+    # transformers 4.x: rope_theta + rope_scaling; 5.x: rope_parameters (theta and scaling together)
+    rp = c.get("rope_parameters") or {}
+    theta = c.get("rope_theta", rp.get("rope_theta", 10000.0))
+    rs = c.get("rope_scaling") or (rp if rp.get("rope_type") not in (None, "default") else None)
+    if rs is not None:
+        kind = rs.get("rope_type", rs.get("type"))
+        if kind == "default":
+            rs = None
+        elif kind != "llama3":
+            raise ValueError(f"{path}: rope_scaling type {kind!r} is not supported (llama3 or none)")
+        else:
+            rs = {k: float(rs[k]) if k != "original_max_position_embeddings" else int(rs[k])
+                  for k in ("factor", "low_freq_factor", "high_freq_factor", "original_max_position_embeddings")}
+    eos = c.get("eos_token_id")
+    eos = tuple(eos) if isinstance(eos, (list, tuple)) else ((eos,) if eos is not None else ())
+    return DecoderConfig(_label(path), vocab_size=c["vocab_size"], hidden=c["hidden_size"],
+                         layers=c["num_hidden_layers"], heads=heads,
+                         kv_heads=c.get("num_key_value_heads") or heads, intermediate=c["intermediate_size"],
+                         rope_theta=float(theta), rope_scaling=rs,
+                         eps=float(c.get("rms_norm_eps", 1e-6)), max_position=c.get("max_position_embeddings", 8192),
+                         bos_id=c.get("bos_token_id", 1) if c.get("bos_token_id") is not None else 1,
+                         eos_ids=eos or (2,), tie_embeddings=bool(c.get("tie_word_embeddings", False)))
+
+
 def encoder_config(name: str, **overrides) -> EncoderConfig:
+    if checkpoint_dir(name):
+        cfg = encoder_config_from_hf(name)
+        return replace(cfg, **overrides) if overrides else cfg
     k = _key(name)
     if k not in ENCODERS:
-        raise KeyError(f"unknown encoder model '{name}' (known: {sorted(ENCODERS)})")
+        raise KeyError(f"unknown encoder model '{name}' (known: {sorted(ENCODERS)}, or a local HF directory)")
     return replace(ENCODERS[k], **overrides) if overrides else ENCODERS[k]
 
 
 def decoder_config(name: str, **overrides) -> DecoderConfig:
+    if checkpoint_dir(name):
+        cfg = decoder_config_from_hf(name)
+        return replace(cfg, **overrides) if overrides else cfg
     k = _key(name)
     if k not in DECODERS:
-        raise KeyError(f"unknown decoder model '{name}' (known: {sorted(DECODERS)})")
+        raise KeyError(f"unknown decoder model '{name}' (known: {sorted(DECODERS)}, or a local HF directory)")
     return replace(DECODERS[k], **overrides) if overrides else DECODERS[k]
 
 
 def is_encoder(name: str) -> bool:
-    return _key(name) in ENCODERS
+    d = checkpoint_dir(name)
+    return _hf(d).get("model_type") == "bert" if d else _key(name) in ENCODERS
 
 
 def is_decoder(name: str) -> bool:
-    return _key(name) in DECODERS
+    d = checkpoint_dir(name)
+    return _hf(d).get("model_type") == "llama" if d else _key(name) in DECODERS
