@@ -13,11 +13,11 @@ import torch
 transformers = pytest.importorskip("transformers")
 
 
-def _llama_dir(tmp, bpe_dir, rope_scaling=None, hidden=256, heads=4, kv_heads=2):
+def _llama_dir(tmp, bpe_dir, rope_scaling=None, hidden=256, heads=4, kv_heads=2, tie=False):
     torch.manual_seed(0)
     hc = transformers.LlamaConfig(vocab_size=1024, hidden_size=hidden, num_hidden_layers=2, num_attention_heads=heads,
                                   num_key_value_heads=kv_heads, intermediate_size=512, rms_norm_eps=1e-5,
-                                  rope_theta=500000.0, max_position_embeddings=2048, tie_word_embeddings=False,
+                                  rope_theta=500000.0, max_position_embeddings=2048, tie_word_embeddings=tie,
                                   bos_token_id=1000, eos_token_id=1001, rope_scaling=rope_scaling,
                                   attn_implementation="eager")
     hf = transformers.LlamaForCausalLM(hc).eval()
@@ -74,10 +74,15 @@ def teacher_forced_agreement(hf, prompts, outs):
     return exact / total
 
 
-def test_llm_engine_runs_a_saved_hf_llama(tmp_path, bpe_dir):
+@pytest.mark.parametrize("tie", [False, True])
+def test_llm_engine_runs_a_saved_hf_llama(tmp_path, bpe_dir, tie):
+    """tie: Llama-3.2-style tied input / output embeddings (no lm_head tensor in the checkpoint)."""
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
 
-    hf, d = _llama_dir(str(tmp_path), bpe_dir, rope_scaling=LLAMA3_SCALING)
+    hf, d = _llama_dir(str(tmp_path), bpe_dir, rope_scaling=LLAMA3_SCALING, tie=tie)
+    from django_assistant_bot_amd.models.configs import decoder_config
+
+    assert decoder_config(d).tie_embeddings == tie
     eng = LLMEngine(d, device="cpu", max_batch=4, block_size=16, num_blocks=64, use_graphs=False)
     assert eng.tokenizer.byte_exact  # the directory's tokenizer.json, not the hash fallback
     prompts = [eng.tokenizer.encode(t) for t in ("the quick brown fox", "jumps over the lazy dog again")]
