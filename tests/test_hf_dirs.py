@@ -118,12 +118,13 @@ def test_embedding_engine_runs_a_saved_hf_bert(tmp_path):
 
 
 @pytest.mark.gpu
-def test_llm_engine_runs_a_saved_hf_llama_on_gpu(tmp_path, bpe_dir):
+@pytest.mark.parametrize("tie", [False, True])
+def test_llm_engine_runs_a_saved_hf_llama_on_gpu(tmp_path, bpe_dir, tie):
     """The GPU path at D = 128 (flash_d128 prefill with RoPE on load, the paged decode attention,
     fragment-layout stream GEMMs, HIP-graph decode) against HF fp32 with Llama-3 RoPE scaling."""
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
 
-    hf, d = _llama_dir(str(tmp_path), bpe_dir, rope_scaling=LLAMA3_SCALING, hidden=512, heads=4, kv_heads=2)
+    hf, d = _llama_dir(str(tmp_path), bpe_dir, rope_scaling=LLAMA3_SCALING, hidden=512, heads=4, kv_heads=2, tie=tie)
     eng = LLMEngine(d, device="cuda", max_batch=8, block_size=64, num_blocks=64)
     assert eng.cfg.head_dim == 128 and eng.model.frag
     texts = ["the quick brown fox", "jumps over the lazy dog again and again", "a" * 300]
