@@ -1,7 +1,8 @@
 """In-process generator on the MI355X engine (replaces the reference's HF ``TransformersProvider``,
 ai/providers/transformers.py:9-94).
 
-Same contract: prompt rendered as ``"role: content"`` lines (no chat template), sampling with
+Same contract: prompt rendered as ``"role: content"`` lines (no chat template; the setting
+``ENGINE_CHAT_TEMPLATE`` opts into the checkpoint's own template when it has one), sampling with
 top_k=50 / top_p=0.95, JSON mode returns the parsed object (constrained decoding: the text is
 one JSON object by construction; the raw string is kept if it still fails to parse), usage reports
 prompt/completion token counts, ``length_limited`` when the completion hit the budget.  Differences:
@@ -43,8 +44,17 @@ class TransformersProvider(AIProvider):
                            json_format: bool = False, json_schema: dict | None = None) -> AIResponse:
         from django_assistant_bot_amd.engine.llm_engine import SamplingParams
 
-        prompt = render_prompt(messages)
-        ids = self._tokenizer.encode(prompt, add_special=True, max_len=self._worker.engine.max_model_len - 1)
+        from assistant.conf import settings
+
+        flag = settings.get("ENGINE_CHAT_TEMPLATE", False)
+        flag = flag if isinstance(flag, bool) else str(flag).strip().lower() in ("1", "true", "yes", "on")
+        if flag and getattr(self._tokenizer, "has_chat_template", False):
+            # the template writes BOS and the role headers itself
+            prompt = self._tokenizer.render_chat([{"role": m["role"], "content": m["content"]} for m in messages])
+            ids = self._tokenizer.encode(prompt, add_special=False, max_len=self._worker.engine.max_model_len - 1)
+        else:
+            prompt = render_prompt(messages)
+            ids = self._tokenizer.encode(prompt, add_special=True, max_len=self._worker.engine.max_model_len - 1)
         # JSON mode constrains the sampler to one JSON object (engine/json_constraint.py): valid in
         # one generation where the reference retries until json.loads succeeds
         params = SamplingParams(max_new_tokens=max_tokens, temperature=1.0, top_k=50, top_p=0.95,

@@ -37,6 +37,9 @@ DEFAULTS: dict[str, Any] = {
     "INDEX_SHARDS": 0,
     "INDEX_DTYPE": "bfloat16",
     "ENGINE_RANDOM_WEIGHTS": True,
+    # engine: apply a checkpoint's chat template (tokenizer_config.json) instead of the reference's
+    # "role: content" prompt lines
+    "ENGINE_CHAT_TEMPLATE": False,
 }
 
 _overrides: dict[str, Any] = {}

@@ -4,6 +4,12 @@ The reference uses ``AutoTokenizer.from_pretrained(local_files_only=True)`` (ai/
 ai/providers/transformers.py:18).  Here, a directory with ``tokenizer.json`` is loaded through the
 ``tokenizers`` library (no hub access); otherwise the native C++ ``HashTokenizer`` (csrc/runtime/tokenizer.cpp)
 provides the same contract with the model's vocabulary size and special ids.
+
+Chat templates: the reference renders messages as ``"role: content"`` lines (no template;
+ai/providers/transformers.py:48).  A checkpoint directory's ``tokenizer_config.json`` template is
+available through ``render_chat`` for deployments that opt in (setting ``ENGINE_CHAT_TEMPLATE``):
+real instruct checkpoints answer in their trained format.  The Jinja template comes from the local
+checkpoint and is rendered in a sandboxed environment (no attribute access to Python internals).
 """
 from __future__ import annotations
 
@@ -16,12 +22,37 @@ from ..ops._lib import native
 
 
 class Tokenizer:
-    def __init__(self, impl, kind: str, hf=None, cls_id=None, sep_id=None, bos_id=None, vocab_size=0):
+    def __init__(self, impl, kind: str, hf=None, cls_id=None, sep_id=None, bos_id=None, vocab_size=0,
+                 chat_template: dict | None = None):
         self._impl = impl
         self._hf = hf
         self.kind = kind
         self.cls_id, self.sep_id, self.bos_id = cls_id, sep_id, bos_id
         self.vocab_size = vocab_size
+        self._chat = chat_template  # {"template", "bos_token", "eos_token"} from tokenizer_config.json
+        self._chat_fn = None
+
+    @property
+    def has_chat_template(self) -> bool:
+        return self._chat is not None
+
+    def render_chat(self, messages: list[dict], add_generation_prompt: bool = True) -> str:
+        """The checkpoint's chat template applied to ``messages`` (text; BOS as the template writes it)."""
+        if self._chat is None:
+            raise ValueError("this tokenizer has no chat template")
+        if self._chat_fn is None:
+            from jinja2.sandbox import ImmutableSandboxedEnvironment
+
+            env = ImmutableSandboxedEnvironment(trim_blocks=True, lstrip_blocks=True)
+
+            def raise_exception(msg):
+                raise ValueError(msg)
+
+            env.globals["raise_exception"] = raise_exception
+            self._chat_fn = env.from_string(self._chat["template"])
+        return self._chat_fn.render(messages=list(messages), add_generation_prompt=add_generation_prompt,
+                                    bos_token=self._chat.get("bos_token") or "",
+                                    eos_token=self._chat.get("eos_token") or "")
 
     # ------------------------------------------------------------------ construction
     @classmethod
@@ -41,7 +72,8 @@ class Tokenizer:
     def for_decoder(cls, cfg: DecoderConfig, path: str | None = None) -> "Tokenizer":
         hf = _maybe_hf(path)
         if hf is not None:
-            return cls(None, "decoder", hf=hf, bos_id=cfg.bos_id, vocab_size=cfg.vocab_size)
+            return cls(None, "decoder", hf=hf, bos_id=cfg.bos_id, vocab_size=cfg.vocab_size,
+                       chat_template=_chat_template(path))
         n = native()
         c = n.TokenizerConfig()
         c.vocab_size = cfg.vocab_size
@@ -87,6 +119,28 @@ class Tokenizer:
 
     def count_tokens(self, text: str) -> int:
         return len(self.encode(text, add_special=False))
+
+
+def _chat_template(path) -> dict | None:
+    """``chat_template`` (and the BOS / EOS token strings it references) of a checkpoint directory's
+    tokenizer_config.json; a named-template list takes the "default" entry."""
+    import json
+
+    f = os.path.join(path, "tokenizer_config.json") if path and os.path.isdir(path) else None
+    if not f or not os.path.exists(f):
+        return None
+    with open(f) as fh:
+        c = json.load(fh)
+    t = c.get("chat_template")
+    if isinstance(t, list):
+        t = next((x.get("template") for x in t if x.get("name") == "default"), None)
+    if not t:
+        return None
+
+    def tok(v):
+        return v.get("content") if isinstance(v, dict) else v
+
+    return {"template": t, "bos_token": tok(c.get("bos_token")), "eos_token": tok(c.get("eos_token"))}
 
 
 def _maybe_hf(path):
