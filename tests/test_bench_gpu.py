@@ -58,3 +58,11 @@ def test_bench_two_ranks_on_one_gpu(tp):
         assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 16
     else:
         assert "tp2" in d["config"]["parallelism"]
+
+
+def test_bench_four_ranks_on_one_gpu():
+    """The multi-GPU launch shape at 4 ranks (index sharded 4 ways, all_to_all merge), on one card."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4"] + TINY
+    d = _run(cmd, DAB_DIST_BACKEND="gloo")
+    assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["config"]["global_batch"] == 32
