@@ -51,6 +51,10 @@ ARMS = {
     "no_rope": {"_ablate": {"rope"}},       # upper bound of fusing the RoPE / KV write away
     "no_norm_rope": {"_ablate": {"norm", "rope"}},
     "part1024": {"_part": 1024},
+    "nofuse": {"_nofuse": True},            # RMSNorms as their own kernels (base fuses them when run with DAB_DECODE_NORM_FUSED=1)
+    "fn_o10": {"o": (10, 8)},               # fused-norm producers on 128-row tiles x 8 slices
+    "fn_d10": {"down": (10, 8)},
+    "fn_od10": {"o": (10, 8), "down": (10, 8)},
     "part512": {"_part": 512},
 }
 
@@ -96,6 +100,7 @@ def main():
             restart()
             eng.model.stream_overrides = {k: v for k, v in spec.items() if not k.startswith("_")}
             eng.model.ablate = set(spec.get("_ablate", ()))
+            eng.model.decode_norm_fusion = not spec.get("_nofuse", False)
             eng.long_part_size = spec.get("_part", base_part)
             llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
             eng._graphs.clear()

@@ -198,6 +198,13 @@ PYBIND11_MODULE(_native, m) {
                            cfg),
           "stream_gemm");
   });
+  m.def("stream_gemm_norm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N,
+                               int K, int S, int epilogue, u s, int nt, int cfg, u h_out, u ss_out, u counters, u ss_in,
+                               int ss_tiles, float eps) {
+    check(dab::stream_gemm_norm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s),
+                                nt, cfg, VP(h_out), (float*)ss_out, (int*)counters, (const float*)ss_in, ss_tiles, eps),
+          "stream_gemm_norm");
+  });
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
   m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);

@@ -80,6 +80,11 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
+// ... with the decode RMSNorm fused across a projection pair (StreamParams in stream_gemm.hip):
+// producer h_out / ss_out / counters, consumer ss_in / ss_tiles / eps
+int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual,
+                     long ldr, int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg,
+                     void* h_out, float* ss_out, int* counters, const float* ss_in, int ss_tiles, float eps);
 int stream_gemm_bn(int cfg);
 // fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
 int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
