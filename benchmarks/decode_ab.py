@@ -56,6 +56,8 @@ ARMS = {
     "fn_d10": {"down": (10, 8)},
     "fn_od10": {"o": (10, 8), "down": (10, 8)},
     "part512": {"_part": 512},
+    "part640": {"_part": 640},              # ~2 equal partitions of a ~1.2k context
+    "part768": {"_part": 768},
 }
 
 
