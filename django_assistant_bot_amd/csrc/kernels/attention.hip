@@ -715,7 +715,15 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
   // the grid-stride loop; with part fastest, a power-of-two max_parts pinned all live work onto the
   // few workgroups with blockIdx % max_parts == live part (measured 3-10x slower).
   const int BH = total_items / p.max_parts;
-  for (int item = blockIdx.x; item < total_items; item += gridDim.x) {
+  // partitions past the longest context are empty: with a longest-first order (order[0] holds the
+  // longest context, the paged_decode contract) the walk stops there instead of visiting every
+  // partition the workspace could hold (max_parts covers max_model_len at the finest partition)
+  int live_items = total_items;
+  if (p.order) {
+    const int maxc = p.ctx_lens[p.order[0]];
+    live_items = min(p.max_parts, (maxc + p.part_size - 1) / p.part_size) * BH;
+  }
+  for (int item = blockIdx.x; item < live_items; item += gridDim.x) {
     const int part = item / BH;
     const int bh = item - part * BH;
     const int hk = bh % p.Hkv, b = p.order ? p.order[bh / p.Hkv] : bh / p.Hkv;

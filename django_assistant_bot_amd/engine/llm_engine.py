@@ -535,10 +535,15 @@ class LLMEngine:
         to = lambda a: torch.as_tensor(a).to(dev, non_blocking=True)  # noqa: E731
         self._d_ctx[:Bp].copy_(self._h_ctx[:Bp], non_blocking=True)
         self._d_bt[:Bp].copy_(self._h_bt[:Bp], non_blocking=True)
+        order = None
+        if self.is_gpu:  # longest first: the decode attention stops at the longest context's partitions
+            self._fill_order(Bp)
+            self._d_order[:Bp].copy_(self._h_order[:Bp], non_blocking=True)
+            order = self._d_order[:Bp]
         meta = AttnMeta(decode=False, positions=to(pos), slots=to(slots), block_tables=to(bt), ctx_lens=to(ctx),
                         cu_q=to(cu), max_q=max(n for _, _, n in chunks), workspace=self._workspace,
                         part_size=self._decode_part(Bp), n_decode=Bp, dec_block_tables=self._d_bt[:Bp],
-                        dec_ctx_lens=self._d_ctx[:Bp])
+                        dec_ctx_lens=self._d_ctx[:Bp], order=order)
         with self.timer.phase("mixed"):
             hidden = self.model.forward(to(ids), meta, self.kv)
         last_rows = [i for i, (r, s, n) in enumerate(chunks) if s + n == len(r.full_prompt())]
@@ -901,7 +906,9 @@ class LLMEngine:
 
     def _decode_part(self, Bp: int) -> int:
         """Decode attention key partition for a step of Bp sequences: long partitions once the
-        (sequence, kv head) pairs alone cover every CU twice over (512 pairs on 256 CUs)."""
+        (sequence, kv head) pairs alone cover every CU twice over (512 pairs on 256 CUs).  (At batch
+        1 the attention is a chain of dependent round trips: 16.4 us per layer with 512- and with
+        128-key partitions alike, profiles/low_load_latency.md.)"""
         hkv = self.cfg.kv_heads // self.tp_size
         return self.long_part_size if Bp * hkv >= 512 else self.part_size
 

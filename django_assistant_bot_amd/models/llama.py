@@ -57,7 +57,8 @@ class AttnMeta:
     n_decode: int = 0
     dec_block_tables: torch.Tensor | None = None
     dec_ctx_lens: torch.Tensor | None = None
-    order: torch.Tensor | None = None  # int32 [B] decode attention dispatch order (longest context first)
+    order: torch.Tensor | None = None  # int32 [B] decode attention dispatch order (longest context first;
+    # of the decode rows in a mixed step)
 
 
 class KVCache:
@@ -401,7 +402,7 @@ class LlamaModel:
             ops.flash_attention_paged(q[:Tp], kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                       meta.max_q, causal=True, out=a[:Tp])
         ops.paged_decode(q[Tp:], kv.k[li], kv.v[li], meta.dec_block_tables, meta.dec_ctx_lens, meta.part_size,
-                         meta.workspace, out=a[Tp:])
+                         meta.workspace, out=a[Tp:], order=meta.order)
         return a
 
     def logits(self, h: torch.Tensor) -> torch.Tensor:
