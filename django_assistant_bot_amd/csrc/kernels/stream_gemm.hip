@@ -69,6 +69,7 @@ struct StreamParams {
   float eps;
 };
 constexpr int ST_SS_MAX = 64;  // producer tiles a consumer can sum (BN 64 x 64 = 4096 columns)
+constexpr int ST_PROD_IT = 4;  // fused-norm producer: 8-column items per thread it holds in flight
 
 constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2, ST_EPI_SWIGLU8 = 4, ST_EPI_CAND = 8;
 
@@ -317,6 +318,9 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, (m * p.N + c4) * 4, 0, 16);
       }
     }
+    if constexpr ((MP * (BN / 8) + NT - 1) / NT > ST_PROD_IT) {
+      return;  // no fused-norm producer in this configuration (the host rejects h_out for it)
+    } else {
     if (!p.h_out) return;
     // ---- fused norm producer: the last slice of this tile to arrive finishes it.  No fences
     // (cdna_hip_programming.md Guideline 16, R1, as the decode attention's partition combine): the
@@ -393,6 +397,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
       }
     }
     return;
+    }
   }
   if (p.epi == ST_EPI_CAND) {
     for (int e = tid; e < MP * (BN / 4); e += NT) {
@@ -557,6 +562,9 @@ int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out
     // producer: slabs (ldo == N) + residual -> h, per-tile sums of squares; no other epilogue
     if (epilogue != ST_EPI_NONE || !residual || !ss_out || !counters || ldo != N || ldr % 8) return hipErrorInvalidValue;
     if ((long)S * M * N * 4 >= (1L << 31)) return hipErrorInvalidValue;  // slab buffer descriptor range
+    const StreamCfg& c = kStreamCfgs[cfg];
+    const int nt = 64 * (c.nwc + c.nl), items = 16 * c.mt * (bn / 8);
+    if ((items + nt - 1) / nt > ST_PROD_IT) return hipErrorInvalidValue;  // compiled out there
   } else if (S > 1 && (epilogue != ST_EPI_NONE || residual)) {
     return hipErrorInvalidValue;
   }
