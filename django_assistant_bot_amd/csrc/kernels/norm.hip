@@ -242,6 +242,91 @@ __global__ __launch_bounds__(NT) void layernorm_kernel(bf16* __restrict__ out, c
   }
 }
 
+// Same LayerNorm, one WAVE per row for encoder widths (cols = 256 CPL: bge-base 768, bge-large
+// 1024): every lane holds CPL 4-element chunks (lane-strided, so each load instruction is one
+// coalesced 512-B run), the two row sums are wave shuffles (no LDS, no barrier), a wave takes RPW
+// rows with all their loads in flight at once and a 256-thread workgroup 4 RPW rows.  Per 64k x 768
+// LN in the bge encoder (rocprof, profiles/embed_study.md): row-per-workgroup kernel 45.2 us, RPW 1
+// 41.0, RPW 2 34.1 (5.9 TB/s), RPW 4 34.0.  The row-per-workgroup kernel above left a quarter of its 128 lanes
+// idle at 768 columns and waited on two workgroup barriers per row.
+template <int CPL, int RPW>
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(bf16* __restrict__ out, const bf16* __restrict__ x,
+                                                            const bf16* __restrict__ res_in,
+                                                            const bf16* __restrict__ gamma,
+                                                            const bf16* __restrict__ beta, int rows, float eps) {
+  constexpr int cols = 256 * CPL;
+  const int lane = threadIdx.x & 63;
+  const size_t row0 = ((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  if (row0 >= (size_t)rows) return;  // whole wave
+  // every row's loads are issued before the first reduction (RPW rows of one wave in flight)
+  u32x2 xv[RPW][CPL], rv[RPW][CPL];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    const size_t row = min(row0 + r, (size_t)rows - 1);
+    const u32x2* xr = reinterpret_cast<const u32x2*>(x + row * cols);
+    const u32x2* rr = reinterpret_cast<const u32x2*>(res_in + row * cols);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      xv[r][c] = xr[c * 64 + lane];
+      if (res_in) rv[r][c] = rr[c * 64 + lane];
+    }
+  }
+  const u32x2* gr = reinterpret_cast<const u32x2*>(gamma);
+  const u32x2* br = reinterpret_cast<const u32x2*>(beta);
+  u32x2 gv[CPL], bv[CPL];
+#pragma unroll
+  for (int c = 0; c < CPL; ++c) {
+    gv[c] = gr[c * 64 + lane];
+    bv[c] = br[c * 64 + lane];
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) {
+    if (row0 + r >= (size_t)rows) break;  // wave-uniform
+    float v[CPL][4];
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        v[c][2 * j] = __uint_as_float(xv[r][c][j] << 16);
+        v[c][2 * j + 1] = __uint_as_float(xv[r][c][j] & 0xffff0000u);
+        if (res_in) {
+          v[c][2 * j] += __uint_as_float(rv[r][c][j] << 16);
+          v[c][2 * j + 1] += __uint_as_float(rv[r][c][j] & 0xffff0000u);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) s += v[c][j];
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) s += __shfl_xor(s, d, 64);
+    const float mean = s / (float)cols;
+    float sq = 0.f;
+#pragma unroll
+    for (int c = 0; c < CPL; ++c)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float d = v[c][j] - mean;
+        sq += d * d;
+      }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sq += __shfl_xor(sq, d, 64);
+    const float inv = rsqrtf(sq / (float)cols + eps);
+    u32x2* orow = reinterpret_cast<u32x2*>(out + (row0 + r) * cols);
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        o[2 * j] = (v[c][2 * j] - mean) * inv * __uint_as_float(gv[c][j] << 16) + __uint_as_float(bv[c][j] << 16);
+        o[2 * j + 1] = (v[c][2 * j + 1] - mean) * inv * __uint_as_float(gv[c][j] & 0xffff0000u) +
+                       __uint_as_float(bv[c][j] & 0xffff0000u);
+      }
+      orow[c * 64 + lane] = u32x2{pack2bf(o[0], o[1]), pack2bf(o[2], o[3])};
+    }
+  }
+}
+
 // BERT embeddings: LN(word[id] + pos[pos_id] + type[type_id]) fused; type ids default to 0.
 template <int NT, int VPT>
 __global__ __launch_bounds__(NT) void bert_embed_kernel(bf16* __restrict__ out, const int* __restrict__ ids,
@@ -416,6 +501,19 @@ int layernorm(void* out, const void* x, const void* res_in, const void* gamma, c
               float eps, hipStream_t s) {
   if (rows <= 0) return 0;
   if (cols % 8 || cols > 16384) return hipErrorInvalidValue;
+  // encoder widths: one wave per LN_RPW rows, 4 waves per workgroup
+  constexpr int LN_RPW = 2;  // 4 measured the same (34.0 us)
+  const dim3 g4((rows + 4 * LN_RPW - 1) / (4 * LN_RPW));
+  if (cols == 768) {
+    hipLaunchKernelGGL((layernorm_rows_kernel<3, LN_RPW>), g4, dim3(256), 0, s, (bf16*)out, (const bf16*)x,
+                       (const bf16*)res_in, (const bf16*)gamma, (const bf16*)beta, rows, eps);
+    return hipGetLastError();
+  }
+  if (cols == 1024) {
+    hipLaunchKernelGGL((layernorm_rows_kernel<4, LN_RPW>), g4, dim3(256), 0, s, (bf16*)out, (const bf16*)x,
+                       (const bf16*)res_in, (const bf16*)gamma, (const bf16*)beta, rows, eps);
+    return hipGetLastError();
+  }
   DAB_ROW_DISPATCH(layernorm_kernel, rows, cols, s, (bf16*)out, (const bf16*)x, (const bf16*)res_in,
                    (const bf16*)gamma, (const bf16*)beta, cols, eps);
   return hipGetLastError();

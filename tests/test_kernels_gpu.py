@@ -59,9 +59,11 @@ def test_rmsnorm(cols, with_res):
         assert torch.equal(res, er)
 
 
-@pytest.mark.parametrize("cols", [384, 768, 1024])
-def test_layernorm(cols):
-    x, r, g, b = bf(29, cols), bf(29, cols), bf(cols), bf(cols)
+@pytest.mark.parametrize("cols,rows", [(384, 29), (768, 29), (1024, 29), (768, 4099), (1024, 4096)])
+def test_layernorm(cols, rows):
+    """Row-per-workgroup kernel (384) and the wave-per-row kernel of the encoder widths (768 / 1024;
+    4 rows per workgroup, row counts that do and do not fill the last one)."""
+    x, r, g, b = bf(rows, cols), bf(rows, cols), bf(cols), bf(cols)
     close(ops.layernorm(x, g, b, 1e-12, residual=r), ref.layernorm(x, g, b, 1e-12, residual=r))
     close(ops.layernorm(x, g, b, 1e-12), ref.layernorm(x, g, b, 1e-12))
 
