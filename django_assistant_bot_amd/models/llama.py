@@ -83,7 +83,8 @@ _FUSED_DECODE_ROPE = os.environ.get("DAB_DECODE_ROPE_FUSED", "0") == "1"
 
 # Decode RMSNorms inside the GEMMs (``NormPending``: the o / down producers finish their split-K
 # tiles in-launch and leave per-tile sums of squares, qkv / gate_up scale their rows by the norm;
-# gains folded into the weights).  Bitwise-equivalent arithmetic and tested, but 2.3 % per decode
+# gains folded into the weights).  The norm kernel's arithmetic (the gain rounded into the weight
+# instead of the activation) and tested against fp32, but 2.3 % per decode
 # step SLOWER un-profiled (7.65 vs 7.47 ms, profiles/decode_norm_fusion.md): the in-launch tile
 # finish costs three dependent memory round trips (store drain, arrival ticket, slab read), ~6 us,
 # more than the 5 us norm launch it replaces.  Off by default; DAB_DECODE_NORM_FUSED=1 is the A/B
@@ -272,7 +273,8 @@ class LlamaModel:
                 s = s or self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
                 out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True, ss=ss, eps=eps)
                 return ops.slab_reduce(out) if (s > 1 and not allow_slabs) else out
-        assert ss is None, "fused norm needs the streaming GEMM"
+        if ss is not None:
+            raise RuntimeError("the fused decode norm needs the streaming GEMM path")
         return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag)
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: KVCache) -> torch.Tensor:
