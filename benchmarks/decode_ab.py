@@ -56,6 +56,8 @@ ARMS = {
     "fn_d10": {"down": (10, 8)},
     "fn_od10": {"o": (10, 8), "down": (10, 8)},
     "part512": {"_part": 512},
+    "spart256": {"_spart": 256},            # small-batch partition (engine.part_size; ctx <= 16 x part)
+    "spart128": {"_spart": 128},
     "part640": {"_part": 640},              # ~2 equal partitions of a ~1.2k context
     "part768": {"_part": 768},
 }
@@ -93,7 +95,7 @@ def main():
         while eng.waiting or eng.prefilling or eng._pending_prefill is not None:
             eng.step()
 
-    base_part = eng.long_part_size
+    base_part, base_spart = eng.long_part_size, eng.part_size
     arms = args.arms.split(",")
     res = {a: [] for a in arms}
     for r in range(args.rounds):
@@ -104,6 +106,7 @@ def main():
             eng.model.ablate = set(spec.get("_ablate", ()))
             eng.model.decode_norm_fusion = not spec.get("_nofuse", False)
             eng.long_part_size = spec.get("_part", base_part)
+            eng.part_size = spec.get("_spart", base_spart)
             llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
             eng._graphs.clear()
             for _ in range(4):

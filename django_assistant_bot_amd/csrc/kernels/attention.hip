@@ -687,8 +687,15 @@ struct DecodeParams {
 // partition: it stores them to the cache for the next steps (no wait) and writes the same bf16
 // rows over that sub-tile's LDS image once the copy has landed, so nothing in this launch reads
 // the fresh cache row back.
-template <int D, bool KV_NT, bool DMA = false, bool ROPE = false>
-__global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, int total_items) {
+//
+// NSLOT 2 (small batches, DMA without ROPE): two LDS slots per wave, so sub-tile i + 1's copy is in
+// flight while sub-tile i computes, and the wave's block ids are fetched once, one per lane, before
+// the first copy.  At batch 1 - 8 a workgroup's waves walk their sub-tiles back to back with the
+// whole GPU otherwise idle: one copy round trip per sub-tile was the critical path.  128 KB of LDS:
+// one workgroup per CU, which small batches never fill anyway.
+template <int D, bool KV_NT, bool DMA = false, bool ROPE = false, int NSLOT = 1>
+__global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(DecodeParams p, int total_items) {
+  static_assert(NSLOT == 1 || (NSLOT == 2 && DMA && !ROPE), "two slots: DMA staging without RoPE only");
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
@@ -696,7 +703,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
   constexpr int SUB_BYTES = KT * D * 2;
   constexpr int CH = KT * CPR / 64;  // 16-B chunks per lane per sub-tile (K and V each)
   constexpr int RED_BYTES = 4 * 16 * D * 4 + 2 * 4 * 16 * 4;
-  constexpr int STAGE_BYTES = 4 * 2 * SUB_BYTES;
+  constexpr int STAGE_BYTES = 4 * 2 * SUB_BYTES * NSLOT;
   // one LDS array (a second __shared__ object can cost vmcnt(0) waits); the last-arriver flag
   // lives right after the reduction area
   constexpr int AREA_BYTES = STAGE_BYTES > RED_BYTES + 16 ? STAGE_BYTES : RED_BYTES + 16;
@@ -707,7 +714,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
   const int G = p.Hq / p.Hkv;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* ks = smem + w * 2 * SUB_BYTES;
+  char* ks = smem + w * 2 * SUB_BYTES * NSLOT;
   char* vs = ks + SUB_BYTES;
 
   // persistent walk over (key partition, sequence, kv head) items.  The partition is the SLOWEST
@@ -1058,6 +1065,28 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
                                                    0, 0, KV_NT ? 2 : 0);
         }
       };
+      if constexpr (NSLOT == 2) {
+        char* const slot0 = smem + w * 2 * SUB_BYTES * NSLOT;
+        const int n_sub = kw < k_end ? (k_end - kw + 4 * KT - 1) / (4 * KT) : 0;  // <= 64 (launcher)
+        const int myblk = lane < n_sub ? blk_at(kw + lane * 4 * KT) : 0;  // lane i: sub-tile i's block
+        auto issue = [&](int i) {
+          ks = slot0 + (i & 1) * 2 * SUB_BYTES;
+          vs = ks + SUB_BYTES;
+          dma(kw + i * 4 * KT, __builtin_amdgcn_readlane(myblk, i));
+        };
+        if (n_sub > 0) issue(0);
+        for (int i = 0; i < n_sub; ++i) {
+          if (i + 1 < n_sub) {
+            issue(i + 1);  // into the slot sub-tile i - 1 was read from (its MFMAs consumed it)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");  // sub-tile i's 16 pieces landed
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+          ks = slot0 + (i & 1) * 2 * SUB_BYTES;
+          vs = ks + SUB_BYTES;
+          compute(kw + i * 4 * KT);
+        }
+      } else {
       int blk = __builtin_amdgcn_readfirstlane(blk_at(kw));
       if constexpr (ROPE) {  // q's loads ahead of the first copy: both latencies overlap
         pro_load();
@@ -1082,6 +1111,7 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(DecodeParams p, in
         blk = __builtin_amdgcn_readfirstlane(blk);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
       if constexpr (ROPE) pro_load();
       load_sub(kA, vA, kw);
@@ -1314,6 +1344,8 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   // section); D = 64 (small test models) keeps the register path.
   if (D == 128) {
     if (rope) hipLaunchKernelGGL((paged_decode_kernel<128, true, true, true>), grid, dim3(256), 0, s, prm, total_items);
+    else if (batch * Hkv <= 64 && part_size <= 64 * 4 * 32)  // small batches: two LDS slots per wave
+      hipLaunchKernelGGL((paged_decode_kernel<128, true, true, false, 2>), grid, dim3(256), 0, s, prm, total_items);
     else hipLaunchKernelGGL((paged_decode_kernel<128, true, true>), grid, dim3(256), 0, s, prm, total_items);
   } else if (D == 64) {
     if (rope) hipLaunchKernelGGL((paged_decode_kernel<64, true, false, true>), grid, dim3(256), 0, s, prm, total_items);
