@@ -509,6 +509,9 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // weight byte (LM head: 128256 = 668 x 192)
     {8, 2, 1, 4, 3, 2, true, 0, 6},  // 28: 6 + 2 waves
     {8, 2, 1, 4, 2, 2, true, 0, 6},  // 29: = 28 with a 2-stage weight ring
+    // M <= 16 (interactive decode, batch 1-16): one 16-row X tile per stage, a quarter of cfg 13's X
+    // staging and MFMAs
+    {1, 2, 1, 4, 4, 2, true},  // 30: BN 128, 2 loaders
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
