@@ -57,6 +57,7 @@ ARMS = {
     "fn_od10": {"o": (10, 8), "down": (10, 8)},
     "part512": {"_part": 512},
     "m16via13": {"_m16": 13},                # batches <= 16 on the M <= 64 configuration (cfg 13)
+    "m32via13": {"_m32": 13},                # batches 17..32 on cfg 13
     "spart256": {"_spart": 256},            # small-batch partition (engine.part_size; ctx <= 16 x part)
     "spart128": {"_spart": 128},
     "part640": {"_part": 640},              # ~2 equal partitions of a ~1.2k context
@@ -109,6 +110,7 @@ def main():
             eng.long_part_size = spec.get("_part", base_part)
             eng.part_size = spec.get("_spart", base_spart)
             eng.model.STREAM_CFG_M16 = spec.get("_m16", type(eng.model).STREAM_CFG_M16)
+            eng.model.STREAM_CFG_M32 = spec.get("_m32", type(eng.model).STREAM_CFG_M32)
             llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
             eng._graphs.clear()
             for _ in range(4):

@@ -512,6 +512,7 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // M <= 16 (interactive decode, batch 1-16): one 16-row X tile per stage, a quarter of cfg 13's X
     // staging and MFMAs
     {1, 2, 1, 4, 4, 2, true},  // 30: BN 128, 2 loaders
+    {2, 2, 1, 4, 4, 2, true},  // 31: M <= 32, BN 128, 2 loaders
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 

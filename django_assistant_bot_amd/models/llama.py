@@ -193,7 +193,7 @@ class LlamaModel:
     # Decode batches of 129..256 rows: 64-row tiles, 2 k-groups x 4 row groups (cfg 27; M = 256:
     # qkv 27.4 / o 18.6 / gate_up 98.7 / down 49.2 us against 32.4 / 25.8 / 104 / 55 for two
     # M = 128 passes, profiles/decode_round2.md).
-    STREAM_CFG_M16, STREAM_CFG_M64, STREAM_CFG_M128, STREAM_CFG_M256 = 30, 13, 10, 27
+    STREAM_CFG_M16, STREAM_CFG_M32, STREAM_CFG_M64, STREAM_CFG_M128, STREAM_CFG_M256 = 30, 31, 13, 10, 27
     STREAM_WIDE = {"gate_up": 20, "lm_head": 28}
     STREAM_MAX_M = ops.STREAM_MAX_M
 
@@ -203,6 +203,8 @@ class LlamaModel:
             cfg = self.STREAM_CFG_M256
         elif M <= 16 and N % nat.stream_gemm_bn(self.STREAM_CFG_M16) == 0:
             cfg = self.STREAM_CFG_M16
+        elif M <= 32 and N % nat.stream_gemm_bn(self.STREAM_CFG_M32) == 0:
+            cfg = self.STREAM_CFG_M32
         elif M <= 64:
             cfg = self.STREAM_CFG_M64
         else:

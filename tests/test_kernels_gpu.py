@@ -399,7 +399,7 @@ def test_gemm_swiglu():
 
 
 @pytest.mark.parametrize("cfg,M,N,K,S", _stream_cases(
-    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30], [1, 16, 37, 64, 100, 128, 200, 256],
+    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30, 31], [1, 16, 30, 37, 64, 100, 128, 200, 256],
     [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1), (672, 512, 1),
      (1344, 1024, 4), (2688, 1792, 7)]))
 def test_stream_gemm(cfg, M, N, K, S):
@@ -469,7 +469,7 @@ def test_stream_swiglu_and_strided_x(cfg, M):
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([10, 13, 20, 21, 22, 23, 30], [5, 64, 128])])
+@pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([10, 13, 20, 21, 22, 23, 30, 31], [5, 30, 64, 128])])
 def test_stream_swiglu8(cfg, M):
     """8-row [gate | up] groups (EPI_SWIGLU8, the decode copy of gate_up): BN 96 / 112 / 128 tiles."""
     F, K = 1344, 1024
