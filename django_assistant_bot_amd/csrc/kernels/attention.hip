@@ -16,8 +16,6 @@
 //
 // Reference behaviour replaced: HF BertSelfAttention (ai/embedders/transformers.py:18-22) and the
 // HF Llama attention inside model.generate (ai/providers/transformers.py:57-66).
-#include <cstdlib>
-
 #include "common.h"
 #include "launchers.h"
 
@@ -1344,7 +1342,9 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   // section); D = 64 (small test models) keeps the register path.
   if (D == 128) {
     if (rope) hipLaunchKernelGGL((paged_decode_kernel<128, true, true, true>), grid, dim3(256), 0, s, prm, total_items);
-    else if (batch * Hkv <= 64 && part_size <= 64 * 4 * 32)  // small batches: two LDS slots per wave
+    // small batches: two LDS slots per wave (at batch 128 the one-slot kernel's two workgroups per CU
+    // are 2.8 % faster per step: 7.44 vs 7.65 ms, profiles/low_load_latency.md)
+    else if (batch * Hkv <= 64 && part_size <= 64 * 4 * 32)
       hipLaunchKernelGGL((paged_decode_kernel<128, true, true, false, 2>), grid, dim3(256), 0, s, prm, total_items);
     else hipLaunchKernelGGL((paged_decode_kernel<128, true, true>), grid, dim3(256), 0, s, prm, total_items);
   } else if (D == 64) {
