@@ -16,6 +16,8 @@
 //
 // Reference behaviour replaced: HF BertSelfAttention (ai/embedders/transformers.py:18-22) and the
 // HF Llama attention inside model.generate (ai/providers/transformers.py:57-66).
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
