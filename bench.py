@@ -13,24 +13,34 @@ the batched mirror of the reference's ContextService -> ChatCompletion chain):
 
 Two load shapes (``--mode``):
 
+  * ``batch`` (default) -- one step = a batch of C (= ``--batch``) questions answered together
+    (retrieve all, prefill all, decode all); the index is sharded across the ranks (queries
+    all-gathered, partial top-k routed back with all_to_all).  Driver record of round 3 at C=128 on
+    one MI355X: 38.45 q/s, p50 3.33 s (BENCH_r03.json).
   * ``serve`` -- a bot's real traffic: questions keep arriving.  Closed loop at a fixed
-    concurrency C (= ``--batch``) per GPU: whenever ``--admit-group`` slots are free, that many new
-    questions are retrieved and queued; their prompt chunks ride along inside the running decode
-    steps (``LLMEngine`` mixed steps).  Arrivals are staggered over the first generation length so
-    the load is in steady state; one "step" = C completed questions (warmup steps are not timed).
-    The index is replicated per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
-  * ``batch`` (default) -- one step = a batch of C questions answered together (retrieve all,
-    prefill all, decode all); the index is sharded across the ranks (queries all-gathered, partial top-k routed back with all_to_all).
-    Measured at C=128 on one MI355X (round 3): batch 37.1 q/s, p50 3.44 s.  Serve mode is slower
-    (profiles/serving_mixed_steps.md): the native prefill GEMMs run at ~1.5 PFLOP/s only at large M,
-    so mixing decode rows into smaller prefill chunks costs more than it saves.
+    concurrency C per replica (whenever ``--admit-group`` slots are free, that many new questions
+    are retrieved and queued), or open loop at ``--qps`` arrivals per second per replica (latency
+    from the scheduled arrival, queueing included).  Admitted prompts are prefilled in their own
+    steps by default (``--mixed-tokens 0``; mixing prompt chunks into decode steps measured slower,
+    profiles/serving_mixed_steps.md).  One "step" = C completed questions.  The index is replicated
+    per GPU (1.5 GB of 288 GB), so retrieval never waits on another rank.
+  * ``overlap`` -- two engines sharing one weight copy on two streams (throughput setting).
+
+Configs (``--config``, BASELINE.json): 4 (default) is the headline above; 5 is bge-large +
+Llama-3-70B with TP = --gpus in serve mode at a fixed QPS.
 
 Weights are random-init with the real architectures; corpus / questions are synthetic: each
 question has planted "paraphrase" rows near its embedding in 3-5 target documents so retrieval
 returns real documents and prompts have realistic length (~1k tokens).  Every rank runs TP=1 by
 default (DP replicas; "scaling": weak -- per-GPU load fixed).
 
-    python bench.py --gpus N --steps K --warmup W      (N > 1 under torch.distributed.run)
+    python bench.py --gpus N --steps K --warmup W
+
+With N > 1 and no torch.distributed.run around it, bench.py starts the N ranks itself
+(``parallel/launch.py``: torch.distributed.run as a child process, rendezvous on 127.0.0.1) and
+forwards rank 0's JSON line; under torch.distributed.run it is one rank.  ``n_gpus`` is the world
+that formed; a mismatch with --gpus is an error.  ``DAB_DIST_BACKEND=gloo`` rehearses N ranks on one
+GPU (RCCL needs one device per rank).
 """
 from __future__ import annotations
 
@@ -53,6 +63,7 @@ METRIC = "RAG queries/sec + p50 end-to-end latency, bge-base + Llama-3-8B, 1/2/4
 # reference algorithm (benchmarks/reference_rerun.py, profiles/reference_rerun.md): 0.277 q/s per
 # gunicorn worker on one MI355X, x2 for its default of 2 workers (upper bound) -> per GPU.
 BASELINE_QPS_PER_GPU = 0.554
+METRIC_CONFIG5 = "RAG queries/sec + p50 end-to-end latency at fixed QPS, bge-large + Llama-3-70B TP=8 (config 5)"
 
 _WORDS = ("account access admin answer api archive backup billing bot calendar campaign channel client cloud "
           "config contact contract dashboard data deadline delivery deploy dialog document domain email error "
@@ -211,6 +222,22 @@ def _dump_host_profile(prof):
         f.write(buf.getvalue())
 
 
+def _apply_config(args, ap) -> None:
+    """BASELINE.json config presets.  Config 5 (Llama-3-70B TP=8 + bge-large at a fixed QPS) takes
+    its TP degree from --gpus; flags given explicitly on the command line keep their value (a
+    rehearsal swaps in a tiny-depth 70B layout with --llm-model)."""
+    if args.config != 5:
+        return
+    given = {a.split("=")[0] for a in sys.argv[1:] if a.startswith("--")}
+    preset = {"llm_model": "llama-3-70b", "embed_model": "bge-large-en", "mode": "serve", "qps": 4.0,
+              "batch": 64, "tp": args.gpus}
+    for k, v in preset.items():
+        if "--" + k.replace("_", "-") not in given:
+            setattr(args, k, v)
+    if args.mode != "serve" or args.qps <= 0:
+        ap.error("--config 5 is an open-loop serve run: --mode serve with --qps > 0")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,7 +268,17 @@ def main():
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel size (groups of consecutive ranks)")
     ap.add_argument("--no-fast-steps", action="store_true",
                     help="skip the separately reported classify / known-question generations")
+    ap.add_argument("--config", type=int, choices=(4, 5), default=4,
+                    help="BASELINE config: 4 = bge-base + Llama-3-8B, TP=1 per GPU, batch mode (the headline); "
+                         "5 = bge-large + Llama-3-70B, TP = --gpus, serve mode at a fixed QPS (--qps, default 4)")
     args = ap.parse_args()
+    _apply_config(args, ap)
+
+    # --gpus N from a plain process: start the N ranks here (children of this process, which has
+    # not touched the GPU) and exit with the job's code; under torch.distributed.run this is a rank
+    from django_assistant_bot_amd.parallel.launch import check_world, maybe_spawn
+
+    maybe_spawn(args.gpus, __file__)
 
     from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
@@ -257,8 +294,9 @@ def main():
     if args.tp > 1:
         rep = R // args.tp  # DP replica index (consecutive ranks form a TP group)
     n_rep = W // max(1, args.tp)
-    if W != args.gpus and R == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={W}", file=sys.stderr)
+    check_world(args.gpus, W)
+    if W % max(1, args.tp):
+        raise SystemExit(f"--tp {args.tp} does not divide the world of {W} ranks")
     torch.manual_seed(args.seed + R)
     B = args.batch
     n_steps = args.warmup + args.steps
@@ -468,7 +506,9 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     pdist.barrier(info)
-    elapsed = pdist.max_over_ranks(time.perf_counter() - t0, dev)
+    my_elapsed = time.perf_counter() - t0
+    elapsed = pdist.max_over_ranks(my_elapsed, dev)
+    rank_qps = [round(x, 3) for x in pdist.gather_floats(B * args.steps / my_elapsed, dev)]
     # engine counters of the timed region only (before the separately reported fast steps run)
     eng = {k: round(v - stats0.get(k, 0), 3) if isinstance(v, float) else v - stats0.get(k, 0)
            for k, v in llm.stats.items()}
@@ -488,17 +528,19 @@ def main():
         full = {"fast_steps_s": fast["total_s"],
                 "full_pipeline_qps": round(n_rep * B / (batch_s + fast["total_s"]), 3),
                 "full_pipeline_p50_latency_ms": round(1000 * (p50 + fast["total_s"]), 1)}
+    cfg5 = args.config == 5
     out = {
-        "metric": METRIC,
+        "metric": METRIC_CONFIG5 if cfg5 else METRIC,
         "value": round(qps, 3),
         "unit": "queries/s",
         "n_gpus": W,
+        "backend": info.backend,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * elapsed / args.steps, 2),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": round(qps / (BASELINE_QPS_PER_GPU * W), 2),
+        "vs_baseline": None if cfg5 else round(qps / (BASELINE_QPS_PER_GPU * W), 2),
         "dtype": "bf16",
         "data": "synthetic (random-init weights; synthetic corpus/questions)",
         "p50_latency_ms": round(1000 * p50, 1),
@@ -522,6 +564,7 @@ def main():
             "graphs": llm.use_graphs,
             "setup_s": round(setup_s, 1),
             "generated_tokens_per_s": round(total_q * args.max_new_tokens / elapsed, 1),
+            "per_rank_qps": rank_qps,
             "engine_rank0": eng,
             **({"fast_steps": fast} if fast else {}),
             "phases_rank0_s": {k: round(float(np.mean(v)), 4) for k, v in phases.items() if v},

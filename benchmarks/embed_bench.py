@@ -3,7 +3,7 @@ process per GPU (data parallel, ``torch.distributed.run --nproc-per-node N``), v
 rank's shard of the HBM index as they are produced (parallel.dp_embed).
 
     python benchmarks/embed_bench.py --chunks 1000000 [--words 48]
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/embed_bench.py
+    python benchmarks/embed_bench.py --gpus 8 ...     (starts its 8 ranks itself; or one rank under torchrun)
 
 Prints one JSON line (rank 0): chunks/s and tokens/s for the whole job, time measured between barriers.
 """
@@ -27,7 +27,13 @@ def main():
     ap.add_argument("--model", default="bge-base-en")
     ap.add_argument("--max-batch-tokens", type=int, default=65536)
     ap.add_argument("--warmup-chunks", type=int, default=20000)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
+                    help="ranks; from a plain process the script starts them itself (parallel/launch.py)")
     args = ap.parse_args()
+
+    from django_assistant_bot_amd.parallel.launch import check_world, maybe_spawn
+
+    maybe_spawn(args.gpus, __file__)
 
     from bench import _WORDS
     from django_assistant_bot_amd.engine.embedding_engine import EmbeddingEngine
@@ -36,6 +42,7 @@ def main():
     from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
 
     info = pdist.init()
+    check_world(args.gpus, info.world_size)
     eng = EmbeddingEngine(args.model, info.device, seed=0, max_batch_tokens=args.max_batch_tokens)
     words = np.array(_WORDS)
 

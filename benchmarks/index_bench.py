@@ -12,7 +12,7 @@ query batch:
 ``ShardedIndex.search`` is the same path ``bench.py`` and the RAG pipeline use.
 
     python benchmarks/index_bench.py --rows 10000000 --batch 1 64 512
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 benchmarks/index_bench.py ...
+    python benchmarks/index_bench.py --gpus 8 ...     (starts its 8 ranks itself; or one rank under torchrun)
 
 Reported per query batch size: latency per search call (max over ranks), queries/s over the whole
 job, and the effective scan rate (index bytes read per second, summed over ranks).
@@ -40,12 +40,19 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 64, 512], help="queries per rank per call")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
+                    help="ranks; from a plain process the script starts them itself (parallel/launch.py)")
     args = ap.parse_args()
+
+    from django_assistant_bot_amd.parallel.launch import check_world, maybe_spawn
+
+    maybe_spawn(args.gpus, __file__)
 
     from django_assistant_bot_amd.parallel import dist as pdist
     from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
 
     info = pdist.init()
+    check_world(args.gpus, info.world_size)
     dev, W, R = info.device, info.world_size, info.rank
     index = ShardedIndex(args.dim, dev, capacity=args.rows // W + 1024)
     g = torch.Generator(device=dev).manual_seed(7 + R)

@@ -91,6 +91,12 @@ DECODERS = {
     "tiny-llama-70b-layout": DecoderConfig("tiny-llama-70b-layout", vocab_size=1024, hidden=1024, layers=2, heads=64,
                                            kv_heads=8, intermediate=1024, max_position=2048, bos_id=1000,
                                            eos_ids=(1001,), rope_scaling=None, rope_theta=10000.0),
+    # Llama-3-70B's real attention layout (hidden 8192, 64 / 8 heads of D = 128) at 2 layers with a
+    # toy vocabulary and MLP: TP=8 ranks run the D = 128 prefill / decode attention kernels with 8
+    # query heads over 1 KV head and all-reduce 70B-sized rows (B x 8192)
+    "tiny-llama-70b-d128": DecoderConfig("tiny-llama-70b-d128", vocab_size=1024, hidden=8192, layers=2, heads=64,
+                                         kv_heads=8, intermediate=2048, max_position=2048, bos_id=1000,
+                                         eos_ids=(1001,), rope_scaling=None, rope_theta=10000.0),
 }
 
 _ALIASES = {

@@ -100,6 +100,16 @@ def max_over_ranks(value: float, device) -> float:
     return float(t.item())
 
 
+def gather_floats(value: float, device) -> list[float]:
+    """Every rank's ``value``, in rank order, on every rank (one all_gather; [value] without a group)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return [value]
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 def shutdown() -> None:
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

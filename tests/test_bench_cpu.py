@@ -58,6 +58,34 @@ def test_bench_two_gloo_ranks():
     _check(_run(cmd), 2)
 
 
+def test_bench_self_launches_its_ranks():
+    """``python bench.py --gpus 2`` as ONE plain command (the driver's form): the script starts the
+    two ranks itself and the JSON reports the world that formed, its backend and per-rank rates."""
+    d = _run([sys.executable, "bench.py", "--gpus", "2"] + TINY)
+    _check(d, 2)
+    assert d["backend"] == "gloo" and len(d["config"]["per_rank_qps"]) == 2
+
+
+def test_bench_world_mismatch_is_an_error():
+    """A torchrun world that is not the --gpus asked for fails instead of reporting a mislabelled number."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4"] + TINY
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "formed a world of 2" in p.stderr
+
+
+def test_bench_config5_preset_self_launch():
+    """--config 5 (Llama-3-70B layout TP = --gpus + bge-large, open-loop serve at a fixed QPS) at
+    toy depth: 2 ranks form one TP-2 replica."""
+    args = list(TINY)
+    args[args.index("--llm-model") + 1] = "tiny-llama-70b-layout"
+    d = _run([sys.executable, "bench.py", "--config", "5", "--gpus", "2", "--qps", "40", *args])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp1xtp2"
+    assert d["config"]["mode"].startswith("serve (open loop") and d["vs_baseline"] is None
+    assert "70B" in d["metric"] and d["value"] > 0
+
+
 def test_bench_overlap_mode_single_process():
     """--mode overlap: two engines sharing one weight copy, each on its own thread / stream, batches
     alternating; the timed region answers every question once (2 timed batches of 4)."""
