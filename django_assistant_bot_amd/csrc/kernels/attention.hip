@@ -722,14 +722,16 @@ __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(D
   // the grid-stride loop; with part fastest, a power-of-two max_parts pinned all live work onto the
   // few workgroups with blockIdx % max_parts == live part (measured 3-10x slower).
   const int BH = total_items / p.max_parts;
-  // partitions past the longest context are empty: with a longest-first order (order[0] holds the
-  // longest context, the paged_decode contract) the walk stops there instead of visiting every
-  // partition the workspace could hold (max_parts covers max_model_len at the finest partition)
-  int live_items = total_items;
-  if (p.order) {
-    const int maxc = p.ctx_lens[p.order[0]];
-    live_items = min(p.max_parts, (maxc + p.part_size - 1) / p.part_size) * BH;
-  }
+  // partitions past the longest context are empty: the walk stops there instead of visiting every
+  // partition the workspace could hold (max_parts covers max_model_len at the finest partition).
+  // The longest context is a wave max over ctx_lens (B <= a few hundred ints, L2-resident), so the
+  // bound holds for any visit order; the longest-first order is only a load-balancing hint.
+  int maxc = 0;
+  for (int i = lane; i < BH / p.Hkv; i += 64) maxc = max(maxc, p.ctx_lens[i]);
+#pragma unroll
+  for (int off = 32; off; off >>= 1) maxc = max(maxc, __shfl_xor(maxc, off));
+  maxc = __builtin_amdgcn_readfirstlane(maxc);
+  const int live_items = min(p.max_parts, (maxc + p.part_size - 1) / p.part_size) * BH;
   for (int item = blockIdx.x; item < live_items; item += gridDim.x) {
     const int part = item / BH;
     const int bh = item - part * BH;

@@ -115,11 +115,22 @@ class SchemaAutomaton {
                   const std::vector<std::vector<int32_t>>& edges, const std::vector<std::vector<int32_t>>& eps);
   int start() const { return start_; }
   int step(int d, uint8_t c);         // DFA transition (-1 = dead); builds states lazily
-  bool accepting(int d) const { return acc_[d] != 0; }
-  int dist(int d) const { return dist_[d]; }  // shortest accepted completion, bytes
+  // (intern() under mu_ in another thread's step / mask may reallocate acc_ / dist_ / sets_: read
+  // them under the same lock -- automata are shared per tokenizer across engines and threads)
+  bool accepting(int d) const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return acc_[d] != 0;
+  }
+  int dist(int d) const {  // shortest accepted completion, bytes
+    std::lock_guard<std::mutex> lk(mu_);
+    return dist_[d];
+  }
   bool has_exit(int d);               // any byte leads somewhere
   int mask(int d, int limit, uint32_t* out);
-  int dfa_states() const { return (int)sets_.size(); }
+  int dfa_states() const {
+    std::lock_guard<std::mutex> lk(mu_);
+    return (int)sets_.size();
+  }
   const JsonVocab& vocab() const { return *vocab_; }
 
  private:
@@ -136,7 +147,7 @@ class SchemaAutomaton {
   std::vector<int32_t> dist_;
   std::vector<int8_t> exit_;
   int start_;
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::unordered_map<uint64_t, std::vector<uint32_t>> cache_;
   int intern(std::vector<int32_t> set);
   void closure(std::vector<int32_t>& set) const;

@@ -24,6 +24,10 @@ import threading
 
 from ..ops._lib import native
 
+class SchemaError(ValueError):
+    """A JSON Schema the constrained decoder cannot compile (a client error: /dialog/ answers 400)."""
+
+
 _WS = [(0x09, 0x0A), (0x0D, 0x0D), (0x20, 0x20)]
 _DIGIT = [(0x30, 0x39)]
 _HEX = [(0x30, 0x39), (0x41, 0x46), (0x61, 0x66)]
@@ -39,7 +43,7 @@ class _Nfa:
     def state(self) -> int:
         self.n += 1
         if self.n > 200_000:
-            raise ValueError("schema too large for the constrained decoder")
+            raise SchemaError("schema too large for the constrained decoder")
         return self.n - 1
 
     # every builder returns a fragment (start, end)
@@ -130,9 +134,9 @@ class _Compiler:
     def value(self, sch):
         a = self.a
         if sch is True or sch == {}:
-            raise ValueError("unconstrained sub-schemas are not supported (give a type)")
+            raise SchemaError("unconstrained sub-schemas are not supported (give a type)")
         if "$ref" in sch:
-            raise ValueError("recursive schemas ($ref) are not supported")
+            raise SchemaError("recursive schemas ($ref) are not supported")
         if "enum" in sch:
             return self.literals(sch["enum"])
         if "const" in sch:
@@ -157,7 +161,7 @@ class _Compiler:
         if t == "array":
             items = sch.get("items")
             if not isinstance(items, dict):
-                raise ValueError("arrays need an 'items' schema")
+                raise SchemaError("arrays need an 'items' schema")
             lo = int(sch.get("minItems", 0))
             hi = sch.get("maxItems")
             sep = lambda: a.seq(self.ws(), a.lit(b","), self.ws(), self.value(items))  # noqa: E731
@@ -186,19 +190,27 @@ class _Compiler:
                           self.value(props[k])]
             parts += [self.ws(), a.lit(b"}")]
             return a.seq(*parts)
-        raise ValueError(f"unsupported schema: {sch!r}")
+        raise SchemaError(f"unsupported schema: {sch!r}")
 
 
 def compile_schema(schema, max_ws: int = 4):
     """-> (n_states, start, accept, edges, eps) of the schema's byte NFA (leading whitespace
-    allowed, nothing after the closing bracket)."""
-    if isinstance(schema, (str, bytes)):
-        schema = json.loads(schema)
-    t = schema.get("type")
-    if t not in ("object", "array") and "properties" not in schema:
-        raise ValueError("the top level of a decoding schema must be an object or an array")
-    c = _Compiler(max_ws)
-    s, e = c.a.seq(c.ws(), c.value(schema))
+    allowed, nothing after the closing bracket).  Every malformed or unsupported schema raises
+    ``SchemaError``."""
+    try:
+        if isinstance(schema, (str, bytes)):
+            schema = json.loads(schema)
+        if not isinstance(schema, dict):
+            raise SchemaError("a decoding schema must be a JSON object")
+        t = schema.get("type")
+        if t not in ("object", "array") and "properties" not in schema:
+            raise SchemaError("the top level of a decoding schema must be an object or an array")
+        c = _Compiler(max_ws)
+        s, e = c.a.seq(c.ws(), c.value(schema))
+    except SchemaError:
+        raise
+    except (ValueError, TypeError, AttributeError, KeyError) as exc:  # malformed JSON / schema values
+        raise SchemaError(f"invalid JSON schema: {exc}") from exc
     return c.a.n, s, [e], c.a.edges, c.a.eps
 
 

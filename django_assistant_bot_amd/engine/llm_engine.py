@@ -246,12 +246,25 @@ class LLMEngine:
             prompt = prompt[-(self.max_model_len - 1):]
         seed = params.seed if params.seed is not None else self.seed
         r = _Req(rid, prompt, params, time.perf_counter(), rng_base=((seed * 1000003 + rid) & 0xFFFFFFFF) << 20)
-        if params.json_schema is not None and self.tokenizer.byte_exact:
-            from .json_schema import matcher_for
-
-            r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids, params.json_schema)
+        r.matcher = self.check_params(params, matcher=True)
+        if r.matcher is not None:
             self._ensure_mask_buffers()
-        elif params.json_mode or params.json_schema is not None:
+        self.waiting.append(r)
+        return rid
+
+    def check_params(self, params: SamplingParams, matcher: bool = False):
+        """Validates a request's decoding constraint (raises ``SchemaError`` for a schema the
+        constrained decoder cannot compile) and, with ``matcher``, returns the request's native
+        matcher (None when unconstrained).  Callers that queue requests for another rank's engine
+        (``NodeLLM``) call it first, so a bad schema fails its caller, never the remote step."""
+        if params.json_schema is not None and self.tokenizer.byte_exact:
+            from .json_schema import automaton_for, matcher_for
+
+            if not matcher:
+                automaton_for(self.tokenizer, self.cfg.eos_ids, params.json_schema)  # cached per schema
+                return None
+            return matcher_for(self.tokenizer, self.cfg.eos_ids, params.json_schema)
+        if params.json_mode or params.json_schema is not None:
             # (the offline hash tokenizer puts a space before every word token, so exact keys /
             # enum strings cannot be spelled: a schema degrades to plain JSON mode there; it is
             # still validated, so an unsupported schema fails the same way everywhere)
@@ -261,11 +274,18 @@ class LLMEngine:
                 from .json_schema import compile_schema
 
                 compile_schema(params.json_schema)
+            return matcher_for(self.tokenizer, self.cfg.eos_ids) if matcher else None
+        return None
 
-            r.matcher = matcher_for(self.tokenizer, self.cfg.eos_ids)
-            self._ensure_mask_buffers()
-        self.waiting.append(r)
-        return rid
+    def rejected_output(self, rid: int, prompt_ids, reason: str) -> GenerationOutput:
+        """The output of a request that could not be admitted (no tokens, ``finish_reason`` =
+        ``"error: ..."``): answers its caller instead of failing the step it arrived in."""
+        return GenerationOutput(request_id=rid, prompt_ids=list(prompt_ids), token_ids=[], text="",
+                                finish_reason=f"error: {reason}",
+                                usage={"prompt_tokens": len(prompt_ids), "completion_tokens": 0,
+                                       "total_tokens": len(prompt_ids)},
+                                timings={"queue_s": 0.0, "ttft_s": 0.0, "total_s": 0.0, "decode_s": 0.0,
+                                         "prefill_s": 0.0})
 
     def has_unfinished(self) -> bool:
         return bool(self.waiting or self.prefilling or self.running)

@@ -102,7 +102,11 @@ class LLMWorker:
             for rid in finished:
                 fut = self._futures.pop(rid, None)
                 out = self.engine.pop_output(rid)
-                if fut is not None and not fut.done():
+                if fut is None or fut.done():
+                    continue
+                if out is not None and out.finish_reason.startswith("error:"):  # refused by a replica
+                    fut.set_exception(RuntimeError(f"request refused by the engine ({out.finish_reason})"))
+                else:
                     fut.set_result(out)
 
     def stop(self):

@@ -292,9 +292,9 @@ class DecodeWorkspace:
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
                  scale=None, out=None, order=None):
     """q [B, Hq, D] (one new token per sequence) over the paged caches.  ``order`` (int32 [B], a
-    permutation of the batch, LONGEST CONTEXT FIRST: the kernel stops at the partitions of
-    ctx_lens[order[0]]) is the order the (sequence, kv head) items are dispatched in: longest
-    context first balances the two rounds of workgroups every CU runs at RAG batch sizes."""
+    permutation of the batch) is the order the (sequence, kv head) items are dispatched in: longest
+    context first balances the two rounds of workgroups every CU runs at RAG batch sizes.  Any
+    permutation is correct: the kernel bounds its partition walk by its own max over ctx_lens."""
     B, Hq, D = q.shape
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if not q.is_cuda:

@@ -641,7 +641,12 @@ class Node:
             k = int(h[0])
             if k == wire.ADD:
                 m, rid, prompt, sp = wire.read_add(h, p)
-                engines[m].add_request(prompt, sp, request_id=rid)
+                try:
+                    engines[m].add_request(prompt, sp, request_id=rid)
+                except Exception as exc:  # a request the engine refuses fails alone, on every TP rank alike
+                    logger.warning("rank %d: request %d refused: %s", self.rank, rid, exc)
+                    if outs is not None:
+                        outs.append(wire.out_item(m, engines[m].rejected_output(rid, prompt, str(exc))))
             elif k == wire.ABORT:
                 m, rid, reason = wire.read_abort(h, p)
                 if engines[m].abort(rid, reason):
@@ -779,6 +784,7 @@ class NodeLLM:
         from ..engine.llm_engine import SamplingParams
 
         params = params or SamplingParams()
+        self.engine.check_params(params)  # a bad schema fails this caller here, not a replica's step
         rid = next(self._ids) if request_id is None else int(request_id)
         replica = min(range(len(self._load)), key=lambda g: (self._load[g], g))
         it = wire.add_item(self.m, rid, [int(t) for t in prompt_ids], params)

@@ -42,6 +42,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+from django_assistant_bot_amd.engine.json_schema import SchemaError  # noqa: E402
+
 logging.basicConfig(level=os.environ.get("GPU_SERVICE_LOG_LEVEL", "INFO"),
                     format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
 logger = logging.getLogger("gpu_service")
@@ -148,7 +150,7 @@ async def get_response(request: DialogRequest):
         resp = await provider.get_response([{"role": m.role, "content": m.content} for m in request.messages],
                                            max_tokens=request.max_tokens, json_format=request.json_format, **kw)
         return {"response": asdict(resp)}
-    except ValueError as e:  # e.g. a JSON Schema the constrained decoder cannot compile
+    except SchemaError as e:  # a JSON Schema the constrained decoder cannot compile: the client's fault
         raise HTTPException(status_code=400, detail=str(e))
     except Exception as e:
         logger.exception("dialog failed")

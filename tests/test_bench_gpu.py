@@ -66,3 +66,37 @@ def test_bench_four_ranks_on_one_gpu():
            "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4"] + TINY
     d = _run(cmd, DAB_DIST_BACKEND="gloo")
     assert d["n_gpus"] == 4 and d["config"]["parallelism"] == "dp4" and d["config"]["global_batch"] == 32
+
+
+def test_bench_self_launches_four_ranks_on_one_gpu():
+    """The driver's form ``python bench.py --gpus 4`` as ONE plain command: bench.py starts the four
+    ranks itself (parallel/launch.py) and reports the world that formed (gloo: all on one card)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DAB_DIST_BACKEND"] = "gloo"
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *TINY], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 4 and d["backend"] == "gloo" and len(d["config"]["per_rank_qps"]) == 4
+    assert d["config"]["parallelism"] == "dp4" and d["value"] > 0
+
+
+def test_bench_config5_eight_rank_rehearsal():
+    """BASELINE config 5 as one command, ``bench.py --config 5 --gpus 8``: bge-large retriever and
+    Llama-3-70B's attention layout (hidden 8192, 64 / 8 heads of D = 128) at 2 layers with TP = 8,
+    open-loop serve at a fixed QPS -- 8 ranks on the one card over gloo, IPC all-reduce in the graphs."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["DAB_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, "bench.py", "--config", "5", "--gpus", "8", "--llm-model", "tiny-llama-70b-d128",
+           "--index-rows", "20000", "--batch", "8", "--max-new-tokens", "8", "--qps", "20", "--steps", "1",
+           "--warmup", "1", "--no-fast-steps"]
+    p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp1xtp8" and "70B" in d["metric"]
+    assert d["config"]["model"] == "bge-large-en + tiny-llama-70b-d128"
+    assert d["value"] > 0 and d["config"]["graphs"] is True

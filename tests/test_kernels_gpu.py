@@ -850,6 +850,10 @@ def test_paged_decode_8k_context(part, split):
     # longest-first dispatch order: same result (each item writes its own sequence's rows)
     order = torch.argsort(ctxt, descending=True).to(torch.int32)
     assert torch.equal(ops.paged_decode(q, kc, vc, bt, ctxt, part, ws, order=order), out)
+    # any other permutation too: the partition bound is the kernel's own max over ctx_lens, so an
+    # order that does not start at the longest context skips nothing
+    for order in (torch.argsort(ctxt).to(torch.int32), torch.tensor([5, 2, 0, 4, 1, 3], dtype=torch.int32, device=DEV)):
+        assert torch.equal(ops.paged_decode(q, kc, vc, bt, ctxt, part, ws, order=order), out)
 
 
 def test_empty_batches_on_gpu():

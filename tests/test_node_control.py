@@ -5,7 +5,9 @@
 * an index search is answered while the replicas are in the middle of a generation;
 * an upsert sends each index shard only the rows it owns (bytes per shard ~ 1/W of the batch);
 * malformed /index payloads are answered 400 on rank 0 and never reach the other ranks: the group
-  stays healthy and keeps serving.
+  stays healthy and keeps serving;
+* a /dialog/ request with a JSON schema the constrained decoder cannot compile is answered 400
+  before it is queued; an ADD a replica still refuses fails only that request.
 Reference: /root/reference/gpu_service/gunicorn_conf.py:9, /root/reference/assistant/rag/services/search_service.py:185-196.
 """
 import os
@@ -107,6 +109,32 @@ def _drive(node, out_path):
           worker.submit(list(range(4, 25)), SamplingParams(max_new_tokens=12, ignore_eos=True, json_schema={
               "type": "object", "properties": {"q": {"type": "integer"}}}))]
     res["json_ok"] = [isinstance(json.loads(f.result(timeout=120).text), dict) for f in jf]
+    # ---- unsupported JSON schemas: 400 for the caller, the group keeps serving
+    msg = [{"role": "user", "content": "hi"}]
+    bad_schemas = [{"$ref": "#"}, {"type": "object", "properties": {"a": {}}}, {"type": "string"}, {"type": "array"}]
+    res["schema_status"] = [c.post("/dialog/", json={"model": "tiny-llama", "messages": msg, "max_tokens": 8,
+                                                     "json_schema": sch}).status_code for sch in bad_schemas]
+    res["health_after_schema"] = c.get("/health").status_code
+    # a refused ADD that slipped past the pre-check fails only its request, on whichever replica got it
+    eng0 = worker.engine.engine
+    orig = eng0.check_params
+    eng0.check_params = lambda params, matcher=False: orig(params, matcher) if matcher else None
+    try:
+        rf = [worker.submit(list(range(3, 12)), SamplingParams(max_new_tokens=4, json_schema={"$ref": "#"}))
+              for _ in range(W)]
+        errs = []
+        for f in rf:
+            try:
+                f.result(timeout=120)
+                errs.append("")
+            except Exception as exc:
+                errs.append(str(exc))
+        res["refused"] = ["refused" in e for e in errs]
+    finally:
+        eng0.check_params = orig
+    after = worker.submit(list(range(3, 12)), SamplingParams(max_new_tokens=5, ignore_eos=True))
+    res["gen_after_refused"] = len(after.result(timeout=120).token_ids)
+    res["health_after_refused"] = c.get("/health").status_code
     res["placed"] = worker.engine.stats_node["placed"]
     st = node.command("stats")
     res["ctrl_s"] = st[:, 0].tolist()
@@ -131,6 +159,8 @@ def test_node_control_plane_world4(tmp_path):
     assert res["gen_tokens"] == [40] * 8
     assert res["json_ok"] == [True, True]
     assert min(res["placed"]) > 0
+    assert res["schema_status"] == [400] * 4 and res["health_after_schema"] == 200
+    assert res["refused"] == [True] * W and res["gen_after_refused"] == 5 and res["health_after_refused"] == 200
     # per-step control cost on the replica leaders (ranks 1..3, each stepping its own replica)
     for r in range(1, W):
         assert res["llm_steps"][r] >= 40

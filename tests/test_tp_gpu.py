@@ -19,7 +19,11 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
-CFG = dict(hidden=4096, intermediate=2048)  # D = 64: the head layout of Llama-3-70B at toy depth / vocab
+# (preset, overrides): D = 64 at the 70B head counts, and Llama-3-70B's real attention layout (hidden
+# 8192, 64 / 8 heads of D = 128: at TP 8 each rank runs flash_d128 / paged_decode<128> with 8 query
+# heads over 1 KV head and all-reduces B x 8192 rows), both at toy depth / vocab / MLP width
+LAYOUTS = {"d64": ("tiny-llama-70b-layout", dict(hidden=4096, intermediate=2048)),
+           "d128": ("tiny-llama-70b-d128", {})}
 
 
 def _free_port():
@@ -30,10 +34,11 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(layout):
     from django_assistant_bot_amd.models.configs import decoder_config
 
-    return decoder_config("tiny-llama-70b-layout", **CFG)
+    name, over = LAYOUTS[layout]
+    return decoder_config(name, **over)
 
 
 def _prompts():
@@ -41,7 +46,7 @@ def _prompts():
     return [torch.randint(0, 1000, (int(n),), generator=g).tolist() for n in (40, 200, 7, 120, 64, 300)]
 
 
-def _body(rank, world, port, out_path):
+def _body(rank, world, layout, port, out_path):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     import torch.distributed as dist
@@ -53,7 +58,8 @@ def _body(rank, world, port, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(0)
     try:
-        cfg = _cfg()
+        cfg = _cfg(layout)
+        assert cfg.head_dim == int(layout[1:])
         full = random_decoder_weights(cfg, dtype=torch.float32, seed=31, interleave_mlp=False)
         group, tp_rank, _ = pdist.tp_groups(world)
         shard = shard_decoder_weights(full, cfg, tp_rank, world, interleave_mlp=True)
@@ -75,17 +81,18 @@ def _body(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("layout", ["d64", "d128"])
 @pytest.mark.parametrize("world", [2, 4, 8])
-def test_tp_engine_on_gpu_matches_tp1(tmp_path, world):
+def test_tp_engine_on_gpu_matches_tp1(tmp_path, world, layout):
     from django_assistant_bot_amd.models.llama import AttnMeta, KVCache, LlamaModel
     from django_assistant_bot_amd.models.weights import _gate_up, random_decoder_weights
 
     out = str(tmp_path / "toks.pt")
-    mp.spawn(_body, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_body, args=(world, layout, _free_port(), out), nprocs=world, join=True)
     toks = torch.load(out, weights_only=True)
     assert [len(t) for t in toks] == [12] * 6
     # teacher-forced TP = 1 scores of the TP-generated sequences
-    cfg = _cfg()
+    cfg = _cfg(layout)
     full = random_decoder_weights(cfg, dtype=torch.float32, seed=31, interleave_mlp=False)
     wm = {}
     for k, v in full.items():
@@ -115,5 +122,5 @@ def test_tp_engine_on_gpu_matches_tp1(tmp_path, world):
                 continue
             gap = float(top2.values[j, 0] - lg[j, tok])
             assert gap <= 0.02 * float(lg[j].abs().max()), (j, tok, best, gap)
-    print(f"TP{world}: {exact}/{total} tokens equal the TP=1 argmax")
+    print(f"TP{world} {layout}: {exact}/{total} tokens equal the TP=1 argmax")
     assert exact >= 0.9 * total
