@@ -20,6 +20,7 @@ from assistant.conf import settings
 from assistant.rag.aggregation import aggregate_documents
 
 logger = logging.getLogger(__name__)
+_REFILL_ROUNDS = 4
 
 
 def cosine_similarity(a, b) -> float:
@@ -70,17 +71,29 @@ async def _objects_embedding_search(query_embedding, qs, n: int = 10, field: str
     from assistant.storage.index import get_index_service
 
     def run():
-        hits = get_index_service().search(qs, query_embedding, n, field)
-        if not hits:
-            return []
-        objs = _load_within(qs, [pk for pk, _ in hits])
-        out = []
-        for pk, dist in hits:
-            o = objs.get(pk)
-            if o is not None:
-                o.distance = float(dist)
-                out.append(o)
-        return out
+        svc = get_index_service()
+        want = n
+        for _ in range(_REFILL_ROUNDS):
+            hits = svc.search(qs, query_embedding, want, field)
+            if not hits:
+                return []
+            objs = _load_within(qs, [pk for pk, _ in hits])
+            out = []
+            for pk, dist in hits:
+                o = objs.get(pk)
+                if o is not None:
+                    o.distance = float(dist)
+                    out.append(o)
+            dropped = [pk for pk, _ in hits if pk not in objs]
+            # LIMIT n semantics (reference search_service.py:191-195): n qualifying rows whenever
+            # they exist.  Hits the QuerySet rejected mean stale mirrored metadata: re-mirror those
+            # rows and search again, over-fetching by what was lost, until n rows qualify or the
+            # index has no more candidates under the filter.
+            if len(out) >= n or not dropped or len(hits) < want:
+                break
+            svc.refresh_rows(qs.model, dropped, field)
+            want = max(2 * want, n + len(dropped))
+        return out[:n]
 
     return await sync_to_async(run)()
 

@@ -291,6 +291,23 @@ class IndexService:
         with self._lock:
             self._be.upsert(name, ids, vecs, docs, groups)
 
+    def refresh_rows(self, model, pks, field="embedding"):
+        """Re-mirror the given rows from the DB (current group bits / document ids); rows that no
+        longer exist or lost their vector leave the index.  Called by a search whose hits the
+        QuerySet rejected, i.e. whose mirrored metadata went stale."""
+        if self._be is None:
+            return
+        name = _key(model, field)
+        if not self._be.loaded(name):
+            return
+        pks = [int(p) for p in pks]
+        ids, docs, groups, vecs = _meta_values(model, field, model.objects.filter(pk__in=pks))
+        with self._lock:
+            self._be.upsert(name, ids, vecs, docs, groups)
+            gone = set(pks) - set(np.asarray(ids).tolist())
+            if gone:
+                self._be.remove(name, np.asarray(sorted(gone), dtype=np.int64))
+
     def refresh_wiki(self, wiki_id):
         """Re-mirror every searchable row of one wiki (finalize flips its completed bit and deletes the
         older runs' rows through the cascade)."""

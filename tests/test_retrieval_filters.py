@@ -216,3 +216,48 @@ def test_hits_are_rechecked_against_the_queryset():
 
     got = _load_within(_FilterQS({1, 2, 5}), [5, 9, 1])
     assert sorted(got) == [1, 5]
+
+
+def test_stale_group_bits_refill_to_n(data, monkeypatch):
+    """LIMIT n semantics under a stale mirror: the index still files rows under bot 2 /
+    COMPLETED that the DB has since moved elsewhere.  ``embedding_search_questions(..., n=5)`` drops
+    them, re-mirrors them from the DB and searches again: 5 rows, the exact top 5 of the rows the
+    QuerySet admits."""
+    import asyncio
+
+    from assistant.rag.services import search_service
+
+    vecs, ids, docs, groups = data
+    bot, g_hot = 2, int(index_mod.row_group(2, 1))
+    q = np.random.default_rng(11).standard_normal(DIM).astype(np.float32)
+    hot_rows = np.flatnonzero(groups == g_hot)
+    order = [int(i) for i in ids[hot_rows][np.argsort(-(vecs[hot_rows] / np.linalg.norm(vecs[hot_rows], axis=1,
+                                                                                      keepdims=True)) @ q)]]
+    stale = set(order[:3])  # the 3 best mirrored rows no longer belong to the filter in the DB
+    db_groups = {int(i): int(g) for i, g in zip(ids, groups)}
+    for pk in stale:
+        db_groups[pk] = int(index_mod.row_group(3, 1))
+
+    svc = index_mod.IndexService(backend="engine")
+    name = "assistant_storage.question.embedding"
+    svc._be.upsert(name, ids, vecs, docs, groups)
+    monkeypatch.setattr(svc, "ensure_loaded", lambda *a: None)
+    row_of = {int(i): r for r, i in enumerate(ids)}
+
+    def meta(model, field, rows):  # the DB's current view of the requested rows
+        pks = np.asarray([o.pk for o in rows], dtype=np.int64)
+        r = np.asarray([row_of[int(p)] for p in pks], dtype=np.int64)
+        return pks, docs[r], np.asarray([db_groups[int(p)] for p in pks], dtype=np.int32), vecs[r]
+
+    monkeypatch.setattr(index_mod, "_meta_values", meta)
+    members = {pk for pk, g in db_groups.items() if g == g_hot}
+    qs = index_mod.with_index_filter(StubQS([]), bot=bot, completed=True)
+    fqs = _FilterQS(members)
+    qs.filter, qs.model = fqs.filter, types.SimpleNamespace(_meta=_Meta("assistant_storage.question"), objects=fqs)
+    monkeypatch.setattr(index_mod, "get_index_service", lambda: svc)
+    got = asyncio.run(search_service.embedding_search_questions(q, qs, n=5))
+    assert [o.pk for o in got] == order[3:8]
+    assert all(a.distance <= b.distance + 1e-6 for a, b in zip(got, got[1:]))
+    # the mirror is repaired: the next search needs no refill
+    hits = svc.search(qs, q, 5)
+    assert [p for p, _ in hits] == order[3:8]
