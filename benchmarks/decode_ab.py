@@ -5,8 +5,9 @@ under it than in the bench (profiles/round3_layout_and_parity.md: a fused prolog
 rocprof lost 0.18 ms per step without it).  This harness builds the bench's decode state once
 (Llama-3-8B, 128 sequences of ~1.1k-token prompts, pipelined HIP-graph decode), then times each
 arm for ``--steps`` decode steps, arms interleaved over ``--rounds`` rounds, with graphs
-re-captured per arm and every arm starting from the same contexts (prefix-cache re-admission).  An arm sets per-projection (stream_gemm cfg, K-slices) overrides and/or the
-decode attention partition.
+re-captured per arm and every arm starting from the same contexts (prefix-cache re-admission).  An arm sets per-projection
+(stream_gemm cfg, K-slices) overrides (``TunedLlama``: a subclass of the production model whose
+``_stream_choice`` consults them) and/or the decode attention partition.
 
     python benchmarks/decode_ab.py --arms base,qkv21,o4 --rounds 3 --steps 40
 """
@@ -40,21 +41,13 @@ ARMS = {
     "gu15": {"gate_up": (15, 1)},
     "qkv15": {"qkv": (15, 4)},
     "o15": {"o": (15, 8)},
-    "rope": {"_rope": True},
     "o9_4": {"o": (9, 4)},
     "o11_4": {"o": (11, 4)},
     "down9_4": {"down": (9, 4)},
     "down11_4": {"down": (11, 4)},
     "qkv9_2": {"qkv": (9, 2)},
     "od9_4": {"o": (9, 4), "down": (9, 4)},
-    "no_norm": {"_ablate": {"norm"}},       # upper bound of fusing the two RMSNorms away (wrong results)
-    "no_rope": {"_ablate": {"rope"}},       # upper bound of fusing the RoPE / KV write away
-    "no_norm_rope": {"_ablate": {"norm", "rope"}},
     "part1024": {"_part": 1024},
-    "nofuse": {"_nofuse": True},            # RMSNorms as their own kernels (base fuses them when run with DAB_DECODE_NORM_FUSED=1)
-    "fn_o10": {"o": (10, 8)},               # fused-norm producers on 128-row tiles x 8 slices
-    "fn_d10": {"down": (10, 8)},
-    "fn_od10": {"o": (10, 8), "down": (10, 8)},
     "part512": {"_part": 512},
     "m16via13": {"_m16": 13},                # batches <= 16 on the M <= 64 configuration (cfg 13)
     "m32via13": {"_m32": 13},                # batches 17..32 on cfg 13
@@ -63,6 +56,22 @@ ARMS = {
     "part640": {"_part": 640},              # ~2 equal partitions of a ~1.2k context
     "part768": {"_part": 768},
 }
+
+
+def tuned_model_class():
+    from django_assistant_bot_amd.models.llama import LlamaModel
+
+    class TunedLlama(LlamaModel):
+        """The production decoder with per-projection (stream_gemm cfg, K-slices) overrides."""
+
+        overrides: dict = {}
+
+        def _stream_choice(self, name, M, N, K):
+            if name in self.overrides:
+                return self.overrides[name]
+            return super()._stream_choice(name, M, N, K)
+
+    return TunedLlama
 
 
 def main():
@@ -75,11 +84,11 @@ def main():
     ap.add_argument("--block-size", type=int, default=64, help="paged-KV block (tokens): one engine per value")
     args = ap.parse_args()
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
-    from django_assistant_bot_amd.models import llama as llama_mod
 
     torch.manual_seed(0)
     eng = LLMEngine("llama-3-8b", device="cuda", max_batch=args.batch, kv_cache_gb=120, max_prefill_tokens=32768,
                     block_size=args.block_size)
+    eng.model.__class__ = tuned_model_class()  # same object, overridable stream choice
     g = torch.Generator().manual_seed(1)
     sp = SamplingParams(max_new_tokens=6000, ignore_eos=True)
     prompts = [torch.randint(0, 128000, (args.prompt + int(torch.randint(-100, 100, (1,), generator=g)),),
@@ -104,14 +113,11 @@ def main():
         for a in arms:
             spec = dict(ARMS[a])
             restart()
-            eng.model.stream_overrides = {k: v for k, v in spec.items() if not k.startswith("_")}
-            eng.model.ablate = set(spec.get("_ablate", ()))
-            eng.model.decode_norm_fusion = not spec.get("_nofuse", False)
+            eng.model.overrides = {k: v for k, v in spec.items() if not k.startswith("_")}
             eng.long_part_size = spec.get("_part", base_part)
             eng.part_size = spec.get("_spart", base_spart)
             eng.model.STREAM_CFG_M16 = spec.get("_m16", type(eng.model).STREAM_CFG_M16)
             eng.model.STREAM_CFG_M32 = spec.get("_m32", type(eng.model).STREAM_CFG_M32)
-            llama_mod._FUSED_DECODE_ROPE = spec.get("_rope", False)
             eng._graphs.clear()
             for _ in range(4):
                 eng.step()

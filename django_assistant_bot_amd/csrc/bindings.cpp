@@ -131,20 +131,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("destroy_stream", [](u s) { check(hipStreamDestroy(ST(s)), "hipStreamDestroy"); });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
                                      u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
-                                     float scale, u s, u order, u rope_qkv, u rope_slabs, int rope_S,
-                                     long rope_slab_stride, int rope_ld, u rope_pos, u rope_cs, u rope_slots) {
-    dab::DecodeRopeArgs rope{CVP(rope_qkv), (const float*)rope_slabs, rope_S, rope_slab_stride, rope_ld,
-                             (const int*)rope_pos, CVP(rope_cs), (const int64_t*)rope_slots};
+                                     float scale, u s, u order) {
     check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
                                       (float*)po, (float*)pm, (float*)pl, (int*)cnt, batch, Hq, Hkv, D, part_size,
-                                      max_parts, scale, ST(s), (const int*)order, rope_pos ? &rope : nullptr),
+                                      max_parts, scale, ST(s), (const int*)order),
           "paged_decode_attention");
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("max_blocks"), py::arg("bs"), py::arg("ctx"),
      py::arg("out"), py::arg("po"), py::arg("pm"), py::arg("pl"), py::arg("cnt"), py::arg("batch"), py::arg("Hq"),
      py::arg("Hkv"), py::arg("D"), py::arg("part_size"), py::arg("max_parts"), py::arg("scale"), py::arg("s"),
-     py::arg("order") = 0, py::arg("rope_qkv") = 0, py::arg("rope_slabs") = 0, py::arg("rope_S") = 0,
-     py::arg("rope_slab_stride") = 0, py::arg("rope_ld") = 0, py::arg("rope_pos") = 0, py::arg("rope_cs") = 0,
-     py::arg("rope_slots") = 0);
+     py::arg("order") = 0);
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s, int b_rows) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
@@ -197,13 +192,6 @@ PYBIND11_MODULE(_native, m) {
     check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
                            cfg),
           "stream_gemm");
-  });
-  m.def("stream_gemm_norm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N,
-                               int K, int S, int epilogue, u s, int nt, int cfg, u h_out, u ss_out, u counters, u ss_in,
-                               int ss_tiles, float eps) {
-    check(dab::stream_gemm_norm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s),
-                                nt, cfg, VP(h_out), (float*)ss_out, (int*)counters, (const float*)ss_in, ss_tiles, eps),
-          "stream_gemm_norm");
   });
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);

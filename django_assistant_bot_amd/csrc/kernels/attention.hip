@@ -661,16 +661,6 @@ struct DecodeParams {
   const int* order;  // optional [B] sequence visit order (longest first: see paged_decode_attention)
   int Hq, Hkv, part_size, max_parts;
   float scale_log2;
-  // fused RoPE + KV-cache write of the step's new token (ROPE kernels): q is built from the QKV
-  // projection -- bf16 rows `qkv` or S fp32 split-K slabs -- and the new key / value are rotated /
-  // copied into the cache by the workgroup whose partition holds position ctx - 1
-  const bf16* qkv;
-  const float* slabs;
-  int S, ld;
-  long slab_stride;
-  const int* positions;
-  const float2* cos_sin;
-  const int64_t* slots;
 };
 
 // DMA (D = 128): each wave streams its 32-key K / V sub-tiles straight into its LDS slot by LDS-DMA
@@ -679,23 +669,14 @@ struct DecodeParams {
 // a register double buffer + ds_write; one slot per wave, the 8 waves of a CU's two workgroups keep
 // ~128 KB in flight.  The next sub-tile's block id is fetched under the current sub-tile's DMA.
 //
-// ROPE: the kernel also does what rope_kv_kernel did as its own launch before it (one dependent
-// launch less per layer).  Each item rotates its G query heads straight from the QKV projection
-// (the same rope_chunk body, so q is bitwise the rope_kv_kernel result), issued after the item's
-// first K/V sub-tile copy so the two latencies overlap.  The new token's key / value (position
-// ctx - 1) are built by the wave whose sub-tile holds that position, in the item of the last
-// partition: it stores them to the cache for the next steps (no wait) and writes the same bf16
-// rows over that sub-tile's LDS image once the copy has landed, so nothing in this launch reads
-// the fresh cache row back.
-//
-// NSLOT 2 (small batches, DMA without ROPE): two LDS slots per wave, so sub-tile i + 1's copy is in
+// NSLOT 2 (small batches, DMA): two LDS slots per wave, so sub-tile i + 1's copy is in
 // flight while sub-tile i computes, and the wave's block ids are fetched once, one per lane, before
 // the first copy.  At batch 1 - 8 a workgroup's waves walk their sub-tiles back to back with the
 // whole GPU otherwise idle: one copy round trip per sub-tile was the critical path.  128 KB of LDS:
 // one workgroup per CU, which small batches never fill anyway.
-template <int D, bool KV_NT, bool DMA = false, bool ROPE = false, int NSLOT = 1>
+template <int D, bool KV_NT, bool DMA = false, int NSLOT = 1>
 __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(DecodeParams p, int total_items) {
-  static_assert(NSLOT == 1 || (NSLOT == 2 && DMA && !ROPE), "two slots: DMA staging without RoPE only");
+  static_assert(NSLOT == 1 || (NSLOT == 2 && DMA), "two slots: DMA staging only");
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
@@ -707,8 +688,7 @@ __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(D
   // one LDS array (a second __shared__ object can cost vmcnt(0) waits); the last-arriver flag
   // lives right after the reduction area
   constexpr int AREA_BYTES = STAGE_BYTES > RED_BYTES + 16 ? STAGE_BYTES : RED_BYTES + 16;
-  // ROPE: the item's rotated q heads [16][D] bf16 live after the staging / reduction area
-  __shared__ __attribute__((aligned(16))) char smem[AREA_BYTES + (ROPE ? 16 * D * 2 : 0)];
+  __shared__ __attribute__((aligned(16))) char smem[AREA_BYTES];
   int* last_flag = reinterpret_cast<int*>(smem + RED_BYTES);
 
   const int G = p.Hq / p.Hkv;
@@ -737,206 +717,12 @@ __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(D
     const int bh = item - part * BH;
     const int hk = bh % p.Hkv, b = p.order ? p.order[bh / p.Hkv] : bh / p.Hkv;
     const int ctx = p.ctx_lens[b];
-    const int pos = ROPE ? p.positions[b] : 0;  // in flight with ctx
     const int k_begin = part * p.part_size;
     if (k_begin >= ctx) continue;
     const int k_end = min(ctx, k_begin + p.part_size);
 
     bf16x8 qf[NKK];
-    // ROPE: q heads and the new token's key / value from the QKV projection.  Lane roles per wave:
-    // lanes 0..D/8-1 rotate 4-dim pair chunks (dims 4c..4c+3 with 4c+D/2..) of q head h = w, w+4, ..
-    // (< G), lanes 16.. / 32.. (writer wave only) the key / value chunks of the new token.  Summed in
-    // slab order and rounded to bf16 before the rotation: bitwise rope_kv_kernel's result.
-    const int j_new = (ctx - 1 - k_begin) / KT;  // sub-tile of position ctx - 1 (last partition)
-    const bool writer = ROPE && k_end == ctx && w == (j_new & 3) && p.slots[b] >= 0;
-    constexpr int PC = D / 8;  // 4-dim rotation-pair chunks per head
-    u32x2 nk1 = {0, 0}, nk2 = {0, 0};
-    auto rope4 = [&](int head, int c, bool rotate, u32x2& o1, u32x2& o2) DAB_ALWAYS_INLINE {
-      const int i0 = 4 * c, half = D / 2;
-      float x1[4], x2[4];
-      if (p.slabs) {
-        const float* src = p.slabs + (size_t)b * p.ld + (size_t)head * D;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) x1[j] = x2[j] = 0.f;
-        int sl = 0;
-        for (; sl + 4 <= p.S; sl += 4, src += 4 * p.slab_stride) {
-          f32x4 u[4], v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            u[q] = *reinterpret_cast<const f32x4*>(src + q * p.slab_stride + i0);
-            v[q] = *reinterpret_cast<const f32x4*>(src + q * p.slab_stride + i0 + half);
-          }
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              x1[j] += u[q][j];
-              x2[j] += v[q][j];
-            }
-        }
-        for (; sl < p.S; ++sl, src += p.slab_stride) {
-          const f32x4 u = *reinterpret_cast<const f32x4*>(src + i0), v = *reinterpret_cast<const f32x4*>(src + i0 + half);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            x1[j] += u[j];
-            x2[j] += v[j];
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x1[j] = bf2f(f2bf(x1[j]));
-          x2[j] = bf2f(f2bf(x2[j]));
-        }
-      } else {
-        const bf16* src = p.qkv + (size_t)b * p.ld + (size_t)head * D;
-        const u32x2 u = *reinterpret_cast<const u32x2*>(src + i0), v = *reinterpret_cast<const u32x2*>(src + i0 + half);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          x1[2 * j] = __uint_as_float(u[j] << 16);
-          x1[2 * j + 1] = __uint_as_float(u[j] & 0xffff0000u);
-          x2[2 * j] = __uint_as_float(v[j] << 16);
-          x2[2 * j + 1] = __uint_as_float(v[j] & 0xffff0000u);
-        }
-      }
-      if (rotate) {
-        const float4* csp = reinterpret_cast<const float4*>(p.cos_sin + (size_t)pos * half + i0);
-        const float4 c01 = csp[0], c23 = csp[1];
-        rope_rot(x1[0], x2[0], make_float2(c01.x, c01.y));
-        rope_rot(x1[1], x2[1], make_float2(c01.z, c01.w));
-        rope_rot(x1[2], x2[2], make_float2(c23.x, c23.y));
-        rope_rot(x1[3], x2[3], make_float2(c23.z, c23.w));
-      }
-      o1 = u32x2{pack2bf(x1[0], x1[1]), pack2bf(x1[2], x1[3])};
-      o2 = u32x2{pack2bf(x2[0], x2[1]), pack2bf(x2[2], x2[3])};
-    };
-    // Prologue in two phases around the first K/V copy: pro_load issues this lane's slab and
-    // cos / sin loads (before the copy's 32 LDS-DMA pieces, whose issue alone takes ~1 us), and
-    // build_q finishes after the copy is in flight.  One code path for q / k / v lanes: role 0 =
-    // q head hk G + w, role 1 / 2 = the new token's key / value (writer wave only).
-    const int role = lane >> 4, pc = lane & 15;
-    const bool pro_on = ROPE && pc < PC && (role == 0 ? w < G : (writer && role <= 2));
-    const int pro_head = role == 0 ? hk * G + w : p.Hq + hk + (role - 1) * p.Hkv;
-    f32x4 ra[4], rb[4];
-    u32x2 qa = {0, 0}, qb = {0, 0};
-    float4 c01 = {1.f, 0.f, 1.f, 0.f}, c23 = {1.f, 0.f, 1.f, 0.f};
-    auto pro_load = [&]() DAB_ALWAYS_INLINE {
-      if (!pro_on) return;
-      const int i0 = 4 * pc;
-      if (p.slabs) {
-        const float* src = p.slabs + (size_t)b * p.ld + (size_t)pro_head * D + i0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (q < p.S) {
-            ra[q] = *reinterpret_cast<const f32x4*>(src + q * p.slab_stride);
-            rb[q] = *reinterpret_cast<const f32x4*>(src + q * p.slab_stride + D / 2);
-          }
-      } else {
-        const bf16* src = p.qkv + (size_t)b * p.ld + (size_t)pro_head * D + i0;
-        qa = *reinterpret_cast<const u32x2*>(src);
-        qb = *reinterpret_cast<const u32x2*>(src + D / 2);
-      }
-      if (role < 2) {
-        const float4* csp = reinterpret_cast<const float4*>(p.cos_sin + (size_t)pos * (D / 2) + i0);
-        c01 = csp[0];
-        c23 = csp[1];
-      }
-    };
-    // every wave of the item runs this once (it holds a workgroup barrier), after its first copy
-    auto build_q = [&]() {
-      char* qs = smem + AREA_BYTES;
-      if (pro_on) {
-        float x1[4], x2[4];
-        if (p.slabs) {  // slab order, from 0: bitwise rope_chunk's sum
-#pragma unroll
-          for (int j = 0; j < 4; ++j) x1[j] = x2[j] = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (q < p.S)
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                x1[j] += ra[q][j];
-                x2[j] += rb[q][j];
-              }
-          const float* src = p.slabs + (size_t)b * p.ld + (size_t)pro_head * D + 4 * pc;
-          for (int sl = 4; sl < p.S; ++sl) {
-            const f32x4 u = *reinterpret_cast<const f32x4*>(src + sl * p.slab_stride);
-            const f32x4 v = *reinterpret_cast<const f32x4*>(src + sl * p.slab_stride + D / 2);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              x1[j] += u[j];
-              x2[j] += v[j];
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            x1[j] = bf2f(f2bf(x1[j]));
-            x2[j] = bf2f(f2bf(x2[j]));
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            x1[2 * j] = __uint_as_float(qa[j] << 16);
-            x1[2 * j + 1] = __uint_as_float(qa[j] & 0xffff0000u);
-            x2[2 * j] = __uint_as_float(qb[j] << 16);
-            x2[2 * j + 1] = __uint_as_float(qb[j] & 0xffff0000u);
-          }
-        }
-        if (role < 2) {
-          rope_rot(x1[0], x2[0], make_float2(c01.x, c01.y));
-          rope_rot(x1[1], x2[1], make_float2(c01.z, c01.w));
-          rope_rot(x1[2], x2[2], make_float2(c23.x, c23.y));
-          rope_rot(x1[3], x2[3], make_float2(c23.z, c23.w));
-        }
-        const u32x2 o1 = {pack2bf(x1[0], x1[1]), pack2bf(x1[2], x1[3])};
-        const u32x2 o2 = {pack2bf(x2[0], x2[1]), pack2bf(x2[2], x2[3])};
-        if (role == 0) {
-          *reinterpret_cast<u32x2*>(qs + (w * D + 4 * pc) * 2) = o1;
-          *reinterpret_cast<u32x2*>(qs + (w * D + 4 * pc + D / 2) * 2) = o2;
-        } else {
-          nk1 = o1;
-          nk2 = o2;
-        }
-      }
-      if (role == 0 && pc < PC) {  // G > 4 (70B-layout groups of 8 at TP 1): the extra heads
-        for (int h = w + 4; h < G; h += 4) {
-          u32x2 o1, o2;
-          rope4(hk * G + h, pc, true, o1, o2);
-          *reinterpret_cast<u32x2*>(qs + (h * D + 4 * pc) * 2) = o1;
-          *reinterpret_cast<u32x2*>(qs + (h * D + 4 * pc + D / 2) * 2) = o2;
-        }
-      }
-      __syncthreads();
-      bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int kk = 0; kk < NKK; ++kk)
-        qf[kk] = li < G ? *reinterpret_cast<const bf16x8*>(qs + (li * D + 32 * kk + 8 * g) * 2) : z;
-    };
-    // the new row into the cache for the next steps; issued right after a vmcnt wait, so the next
-    // sub-tile's wait (in-order counter) finds these stores long done
-    auto store_new = [&]() {
-      const int c = pc;
-      if (writer && (role == 1 || role == 2) && c < PC) {
-        const int64_t slot = p.slots[b];
-        const int64_t blk = slot / p.block_size, off = slot - blk * p.block_size;
-        bf16* dst = const_cast<bf16*>(role == 1 ? p.k_cache : p.v_cache) +
-                    (((size_t)blk * p.Hkv + hk) * p.block_size + off) * D;
-        *reinterpret_cast<u32x2*>(dst + 4 * c) = nk1;
-        *reinterpret_cast<u32x2*>(dst + 4 * c + D / 2) = nk2;
-      }
-    };
-    // after sub-tile k0's LDS image is complete and before compute(k0): the writer puts the new row
-    auto inject = [&](int k0) {
-      const int c = pc;
-      if (writer && k0 <= ctx - 1 && ctx - 1 < k0 + KT && (role == 1 || role == 2) && c < PC) {
-        const int row = ctx - 1 - k0;
-        char* dst = role == 1 ? ks : vs;
-        *reinterpret_cast<u32x2*>(dst + swz<D>(row, c >> 1) + 8 * (c & 1)) = nk1;
-        *reinterpret_cast<u32x2*>(dst + swz<D>(row, (c >> 1) + D / 16) + 8 * (c & 1)) = nk2;
-      }
-    };
-    if constexpr (ROPE) {
-      // q is built below, once this wave's first K/V copy is in flight
-    } else {
+    {
       const bool qv = li < G;
       const bf16* qrow = p.q + ((size_t)b * p.Hq + hk * G + (qv ? li : 0)) * D;
 #pragma unroll
@@ -1090,47 +876,25 @@ __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(D
         }
       } else {
       int blk = __builtin_amdgcn_readfirstlane(blk_at(kw));
-      if constexpr (ROPE) {  // q's loads ahead of the first copy: both latencies overlap
-        pro_load();
-        if (kw < k_end) {
-          dma(kw, blk);
-          blk = blk_at(kw + 4 * KT);
-        }
-        build_q();
-        blk = __builtin_amdgcn_readfirstlane(blk);
-      }
       for (int k0 = kw; k0 < k_end; k0 += 4 * KT) {
-        if (!ROPE || k0 != kw) {
-          dma(k0, blk);
-          blk = blk_at(k0 + 4 * KT);  // in flight under this sub-tile's copy and math
-        }
+        dma(k0, blk);
+        blk = blk_at(k0 + 4 * KT);  // in flight under this sub-tile's copy and math
         asm volatile("s_waitcnt vmcnt(1)" ::: "memory");  // this sub-tile's 16 pieces landed
-        if constexpr (ROPE) {
-          if (k0 == kw) store_new();
-          inject(k0);
-        }
         compute(k0);
         blk = __builtin_amdgcn_readfirstlane(blk);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     } else {
-      if constexpr (ROPE) pro_load();
       load_sub(kA, vA, kw);
       load_sub(kB, vB, kw + 4 * KT);
-      if constexpr (ROPE) {
-        build_q();
-        store_new();
-      }
       for (int k0 = kw; k0 < k_end; k0 += 8 * KT) {
         stage(kA, vA);
         load_sub(kA, vA, k0 + 8 * KT);
-        if constexpr (ROPE) inject(k0);
         compute(k0);
         if (k0 + 4 * KT >= k_end) break;
         stage(kB, vB);
         load_sub(kB, vB, k0 + 12 * KT);
-        if constexpr (ROPE) inject(k0 + 4 * KT);
         compute(k0 + 4 * KT);
       }
     }
@@ -1301,16 +1065,11 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
-                           int part_size, int max_parts, float scale, hipStream_t s, const int* order,
-                           const DecodeRopeArgs* rope) {
+                           int part_size, int max_parts, float scale, hipStream_t s, const int* order) {
   if (batch <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1 || block_size % 32) return hipErrorInvalidValue;
   if (max_parts > 1 && !counters) return hipErrorInvalidValue;
-  if (rope && (!rope->positions || !rope->cos_sin || !rope->slots || (!rope->qkv && !rope->slabs) ||
-               (rope->slabs && (rope->S < 1 || rope->slab_stride % 4)) || rope->ld % 8 ||
-               rope->ld != (Hq + 2 * Hkv) * D))
-    return hipErrorInvalidValue;
-  if (!rope && !q) return hipErrorInvalidValue;
+  if (!q) return hipErrorInvalidValue;
   DecodeParams prm;
   prm.q = (const bf16*)q;
   prm.k_cache = (const bf16*)k_cache;
@@ -1330,14 +1089,6 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_size = part_size;
   prm.max_parts = max_parts;
   prm.scale_log2 = scale * 1.4426950408889634f;
-  prm.qkv = rope ? (const bf16*)rope->qkv : nullptr;
-  prm.slabs = rope ? rope->slabs : nullptr;
-  prm.S = rope ? rope->S : 0;
-  prm.slab_stride = rope ? rope->slab_stride : 0;
-  prm.ld = rope ? rope->ld : 0;
-  prm.positions = rope ? rope->positions : nullptr;
-  prm.cos_sin = rope ? (const float2*)rope->cos_sin : nullptr;
-  prm.slots = rope ? rope->slots : nullptr;
   const int total_items = max_parts * Hkv * batch;
   dim3 grid(total_items < 2048 ? total_items : 2048);
   // K/V are read exactly once per step: non-temporal loads (aux = 2) -- in the Llama-3-8B decode step
@@ -1345,15 +1096,13 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   // profiles/decode_round2.md).  D = 128 stages K / V by LDS-DMA (100.7 vs 102.6 us isolated, same
   // section); D = 64 (small test models) keeps the register path.
   if (D == 128) {
-    if (rope) hipLaunchKernelGGL((paged_decode_kernel<128, true, true, true>), grid, dim3(256), 0, s, prm, total_items);
     // small batches: two LDS slots per wave (at batch 128 the one-slot kernel's two workgroups per CU
     // are 2.8 % faster per step: 7.44 vs 7.65 ms, profiles/low_load_latency.md)
-    else if (batch * Hkv <= 64 && part_size <= 64 * 4 * 32)
-      hipLaunchKernelGGL((paged_decode_kernel<128, true, true, false, 2>), grid, dim3(256), 0, s, prm, total_items);
+    if (batch * Hkv <= 64 && part_size <= 64 * 4 * 32)
+      hipLaunchKernelGGL((paged_decode_kernel<128, true, true, 2>), grid, dim3(256), 0, s, prm, total_items);
     else hipLaunchKernelGGL((paged_decode_kernel<128, true, true>), grid, dim3(256), 0, s, prm, total_items);
   } else if (D == 64) {
-    if (rope) hipLaunchKernelGGL((paged_decode_kernel<64, true, false, true>), grid, dim3(256), 0, s, prm, total_items);
-    else hipLaunchKernelGGL((paged_decode_kernel<64, true>), grid, dim3(256), 0, s, prm, total_items);
+    hipLaunchKernelGGL((paged_decode_kernel<64, true>), grid, dim3(256), 0, s, prm, total_items);
   } else {
     return hipErrorInvalidValue;
   }

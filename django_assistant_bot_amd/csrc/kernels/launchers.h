@@ -40,23 +40,11 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     long o_stride_head, const int* cu_q, const int* cu_k, const int* ctx_k, int batch,
                     int max_seqlen_q, int Hq, int Hkv, int D, int causal, int paged, float scale, hipStream_t s,
                     const int* rope_pos = nullptr, const void* rope_cs = nullptr);
-// decode prologue inputs of the fused RoPE + KV-write form (q == nullptr then): the step's QKV
-// projection as bf16 rows (`qkv`) or S fp32 split-K slabs, row width ld = (Hq + 2 Hkv) D
-struct DecodeRopeArgs {
-  const void* qkv;
-  const float* slabs;
-  int S;
-  long slab_stride;
-  int ld;
-  const int* positions;
-  const void* cos_sin;
-  const int64_t* slots;
-};
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
                            int part_size, int max_parts, float scale, hipStream_t s,
-                           const int* order = nullptr, const DecodeRopeArgs* rope = nullptr);
+                           const int* order = nullptr);
 
 // gemm.hip
 // b_rows > 0: B is an ops.shuffle_weights copy of b_rows (>= N) rows; epilogue 4 = SwiGLU over 8-row
@@ -80,11 +68,6 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
-// ... with the decode RMSNorm fused across a projection pair (StreamParams in stream_gemm.hip):
-// producer h_out / ss_out / counters, consumer ss_in / ss_tiles / eps
-int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual,
-                     long ldr, int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg,
-                     void* h_out, float* ss_out, int* counters, const float* ss_in, int ss_tiles, float eps);
 int stream_gemm_bn(int cfg);
 // fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
 int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,

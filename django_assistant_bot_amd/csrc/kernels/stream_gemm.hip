@@ -19,8 +19,8 @@
 //     as A and X as B (one LDS fragment feeds RT MFMAs); partial tiles of the k-groups meet in LDS.
 //
 // Outputs: S == 1 -> bf16 (optional residual add, or SwiGLU over 16- / 8-row interleaved [gate | up]
-// weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue (rmsnorm /
-// the decode attention's RoPE + KV-write prologue) or by slab_reduce below.  Block -> (tile, slice)
+// weights); S > 1 -> fp32 K-slice slabs [S][M][N] summed by the consumer's prologue (rmsnorm,
+// rope_kv_write) or by slab_reduce below.  Block -> (tile, slice)
 // keeps a tile's slices on one XCD (bijective remap, slice-minor).
 #include <cstdlib>
 #include <type_traits>
@@ -52,24 +52,7 @@ struct StreamParams {
   float* cand_val;       // [M, cap]
   int* cand_idx;         // [M, cap]
   int cap;
-  // Decode RMSNorm fused across a projection pair (the norm weight is folded into the consumer's
-  // weight columns, models/llama.py):
-  //   producer (h_out != null, fp32 slabs written first): the LAST slice to finish a tile (per-tile
-  //     arrival counter, reset by that slice) sums the tile's S slabs, adds the residual, writes the
-  //     new residual stream h = bf16(bf16(sum) + residual) and the tile's per-row sum of h^2
-  //     (ss_out[tile][m]) -- the rmsnorm_slab kernel's arithmetic, without its launch;
-  //   consumer (ss_in != null, X = h): r[m] = rsqrt(sum_t ss_in[t][m] / K + eps) is summed by the
-  //     loader waves while the first X stages land and applied to the accumulators in the epilogue
-  //     (x_norm . W'^T = r[m] (h . W'^T)).
-  bf16* h_out;          // [M, N]
-  float* ss_out;        // [N / BN][M]
-  int* counters;        // [N / BN] arrival counters (zero between launches)
-  const float* ss_in;   // [ss_tiles][M]
-  int ss_tiles;
-  float eps;
 };
-constexpr int ST_SS_MAX = 64;  // producer tiles a consumer can sum (BN 64 x 64 = 4096 columns)
-constexpr int ST_PROD_IT = 4;  // fused-norm producer: 8-column items per thread it holds in flight
 
 constexpr int ST_EPI_NONE = 0, ST_EPI_SWIGLU = 2, ST_EPI_SWIGLU8 = 4, ST_EPI_CAND = 8;
 
@@ -119,10 +102,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   static_assert(CPR >= 16 && CPW >= 1 && KW % 32 == 0, "stage shape");
   static_assert(NB >= 2 && (NB - 2) * GPL <= 63 && GPS % NL == 0, "loader vmcnt range");
   static_assert(NWC % KG == 0, "k groups");
-  // + r[MP] of the fused norm (consumer) and the producer's last-slice flag, past the ring / partials
-  __shared__ __attribute__((aligned(16))) char smem[SMEM + MP * 4 + 16];
-  float* rs = reinterpret_cast<float*>(smem + SMEM);
-  int* last_flag = reinterpret_cast<int*>(smem + SMEM + MP * 4);
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tiles = (p.N + BN - 1) / BN;  // partial last tile: candidates only (rows >= N read zeros)
   const int nwg = tiles * p.S;
@@ -163,30 +143,9 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
         return true;
       });
     };
-    // fused norm (consumer): loader thread lt owns row lt; its producer-tile partials are issued
-    // before the X prologue, so the in-order vmcnt retire below lands them too (no extra wait)
-    float ssp[ST_SS_MAX];
-    const int lt = l * 64 + lane;
-    if constexpr (MP <= 64 * NL) {
-      if (p.ss_in) {
-        const int row = min(lt, p.M - 1);
-#pragma unroll
-        for (int j = 0; j < ST_SS_MAX; ++j) ssp[j] = p.ss_in[(size_t)min(j, p.ss_tiles - 1) * p.M + row];
-      }
-      __builtin_amdgcn_sched_barrier(0);  // keep them ahead of the X prologue in the vmcnt queue
-    }
     const int pre = (ABL & 1) ? 1 : min(NB - 1, nst);
     for (int s = 0; s < pre; ++s) issue(s);
     retire(pre - 1);
-    if constexpr (MP <= 64 * NL) {
-      if (p.ss_in && lt < MP) {
-        float tot = 0.f;
-#pragma unroll
-        for (int j = 0; j < ST_SS_MAX; ++j) tot += j < p.ss_tiles ? ssp[j] : 0.f;
-        rs[lt] = rsqrtf(tot / (float)p.K + p.eps);
-        wait_lgkm0();
-      }
-    }
     __builtin_amdgcn_s_barrier();
     for (int st = 0; st < nst; ++st) {
       if (ABL & 1) {
@@ -301,8 +260,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     return v;
   };
   constexpr int NT = 64 * (NWC + NL);
-  const bool scale = p.ss_in != nullptr;  // fused norm consumer: rows scaled by r[m] (set by the loaders)
-  if (p.S > 1 || p.h_out) {
+  if (p.S > 1) {
     float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
     // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
     // instead of sitting dirty until the kernel-end write-back, which the next kernel's start
@@ -312,92 +270,10 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     const auto srd = __builtin_amdgcn_make_buffer_rsrc(slab + n0, 0, (p.M - 1) * p.N * 4 + BN * 4, 0x00020000);
     for (int e = tid; e < MP * (BN / 4); e += NT) {
       const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
-      if (m < p.M) {
-        f32x4 v = tile4(m, c4);
-        if (scale) v *= rs[m];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), srd, (m * p.N + c4) * 4, 0, 16);
-      }
-    }
-    if constexpr ((MP * (BN / 8) + NT - 1) / NT > ST_PROD_IT) {
-      return;  // no fused-norm producer in this configuration (the host rejects h_out for it)
-    } else {
-    if (!p.h_out) return;
-    // ---- fused norm producer: the last slice of this tile to arrive finishes it.  No fences
-    // (cdna_hip_programming.md Guideline 16, R1, as the decode attention's partition combine): the
-    // slab stores above are write-through, each wave drains them, one lane takes an agent-scope
-    // arrival ticket, and the last arriver reads the slabs with sc1 loads.  (A __threadfence pair
-    // here writes back and invalidates the L2 per workgroup: measured +2.4 ms per decode step.)
-    constexpr int GL = BN / 8;  // lanes per row (8 columns each); divides 64, so a row's lanes share a wave
-    constexpr int IT = (MP * GL + NT - 1) / NT;  // items per thread; MP * GL is a multiple of 64
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the residual rows are in flight while the ticket is taken (every slice loads them: 16-32 KB of
-    // L2 reads each, so the last arriver does not wait a round trip for them)
-    u32x4 rraw[IT];
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int e = tid + it * NT, m = min(min(e, MP * GL - 1) / GL, p.M - 1), c8 = (e % GL) * 8;
-      rraw[it] = *reinterpret_cast<const u32x4*>(p.residual + (size_t)m * p.ldr + n0 + c8);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const int prev = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = prev == p.S - 1;
-      if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *last_flag = last;
-    }
-    __syncthreads();
-    if (!*last_flag) return;
-    const auto ard = __builtin_amdgcn_make_buffer_rsrc((float*)p.out + n0, 0, (p.S * p.M - 1) * p.N * 4 + BN * 4,
-                                                       0x00020000);
-    float o[IT][8];
-#pragma unroll
-    for (int it = 0; it < IT; ++it)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) o[it][j] = 0.f;
-    // slabs 4 at a time, every item's loads issued before the first add (one round trip per 4 slabs)
-    for (int s0 = 0; s0 < p.S; s0 += 4) {
-      f32x4 a[4][IT], b[4][IT];
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-#pragma unroll
-        for (int it = 0; it < IT; ++it) {
-          const int e = tid + it * NT, m = min(min(e, MP * GL - 1) / GL, p.M - 1), c8 = (e % GL) * 8;
-          const int off = ((min(s0 + q, p.S - 1) * p.M + m) * p.N + c8) * 4;
-          a[q][it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ard, off, 0, 16));
-          b[q][it] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ard, off + 16, 0, 16));
-        }
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (s0 + q < p.S)
-#pragma unroll
-          for (int it = 0; it < IT; ++it)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              o[it][j] += a[q][it][j];
-              o[it][4 + j] += b[q][it][j];
-            }
-    }
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int e = tid + it * NT, m = e / GL, c8 = (e % GL) * 8;
-      if (e >= MP * GL) break;  // wave-uniform
-      float r[8];
-      unpack8(rraw[it], r);
-      float ss = 0.f;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        o[it][j] = bf2f(f2bf(bf2f(f2bf(o[it][j])) + r[j]));  // rmsnorm_slab_kernel's rounding
-        ss += o[it][j] * o[it][j];
-      }
-#pragma unroll
-      for (int d = GL / 2; d >= 1; d /= 2) ss += __shfl_xor(ss, d, 64);
-      if (m < p.M) {
-        *reinterpret_cast<u32x4*>(p.h_out + (size_t)m * p.N + n0 + c8) = pack8(o[it]);
-        if (e % GL == 0) p.ss_out[(size_t)tile * p.M + m] = ss;
-      }
+      if (m < p.M)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, tile4(m, c4)), srd, (m * p.N + c4) * 4, 0, 16);
     }
     return;
-    }
   }
   if (p.epi == ST_EPI_CAND) {
     for (int e = tid; e < MP * (BN / 4); e += NT) {
@@ -430,11 +306,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
       const int m = e / (BN / 8), part = e % (BN / 8);
       if (m >= p.M) continue;
       const int i = part / pp, j0 = (part % pp) * 4;
-      f32x4 gt = tile4(m, 2 * hg * i + j0), up = tile4(m, 2 * hg * i + hg + j0);
-      if (scale) {
-        gt *= rs[m];
-        up *= rs[m];
-      }
+      const f32x4 gt = tile4(m, 2 * hg * i + j0), up = tile4(m, 2 * hg * i + hg + j0);
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) o[j] = silu_f(gt[j]) * up[j];
@@ -448,11 +320,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   for (int e = tid; e < MP * (BN / 8); e += NT) {
     const int m = e / (BN / 8), c8 = (e % (BN / 8)) * 8;
     if (m >= p.M) continue;
-    f32x4 lo = tile4(m, c8), hi = tile4(m, c8 + 4);
-    if (scale) {
-      lo *= rs[m];
-      hi *= rs[m];
-    }
+    const f32x4 lo = tile4(m, c8), hi = tile4(m, c8 + 4);
     float o[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     if (p.residual) {
       const u32x4 rv = *reinterpret_cast<const u32x4*>(p.residual + (size_t)m * p.ldr + n0 + c8);
@@ -548,13 +416,6 @@ static void launch_any(int cfg, const StreamParams& p, hipStream_t s, bool nt) {
 
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg) {
-  return stream_gemm_norm(X, ldx, W, ldw, out, ldo, residual, ldr, M, N, K, S, epilogue, s, nt_weights, cfg, nullptr,
-                          nullptr, nullptr, nullptr, 0, 0.f);
-}
-
-int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual,
-                     long ldr, int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg,
-                     void* h_out, float* ss_out, int* counters, const float* ss_in, int ss_tiles, float eps) {
   constexpr int KS = 128;
   if (M <= 0 || N <= 0) return 0;
   const int bn = stream_gemm_bn(cfg);
@@ -562,25 +423,11 @@ int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out
   if (N % bn || S < 1 || K % (S * KS) || ldx % 8 || ldw % 8 || ldo % 8) return hipErrorInvalidValue;
   if (epilogue != ST_EPI_NONE && epilogue != ST_EPI_SWIGLU && epilogue != ST_EPI_SWIGLU8) return hipErrorInvalidValue;
   if (epilogue == ST_EPI_SWIGLU && bn % 32) return hipErrorInvalidValue;  // whole 16 + 16 row pairs per tile
-  if (h_out) {
-    // producer: slabs (ldo == N) + residual -> h, per-tile sums of squares; no other epilogue
-    if (epilogue != ST_EPI_NONE || !residual || !ss_out || !counters || ldo != N || ldr % 8) return hipErrorInvalidValue;
-    if ((long)S * M * N * 4 >= (1L << 31)) return hipErrorInvalidValue;  // slab buffer descriptor range
-    const StreamCfg& c = kStreamCfgs[cfg];
-    const int nt = 64 * (c.nwc + c.nl), items = 16 * c.mt * (bn / 8);
-    if ((items + nt - 1) / nt > ST_PROD_IT) return hipErrorInvalidValue;  // compiled out there
-  } else if (S > 1 && (epilogue != ST_EPI_NONE || residual)) {
-    return hipErrorInvalidValue;
-  }
-  if (ss_in) {
-    // consumer: one loader thread per padded row; K is the normalised width
-    const StreamCfg& c = kStreamCfgs[cfg];
-    if (ss_tiles < 1 || ss_tiles > ST_SS_MAX || 16 * c.mt > 64 * c.nl || h_out) return hipErrorInvalidValue;
-  }
+  if (S > 1 && (epilogue != ST_EPI_NONE || residual)) return hipErrorInvalidValue;
   if (residual && ldr % 8) return hipErrorInvalidValue;
   if ((long)bn * ldw * 2 >= (1L << 31)) return hipErrorInvalidValue;  // buffer descriptor range
   if (kStreamCfgs[cfg].shuf && (ldw != K || K % 32)) return hipErrorInvalidValue;
-  StreamParams p;
+  StreamParams p{};
   p.X = (const bf16*)X;
   p.ldx = ldx;
   p.W = (const bf16*)W;
@@ -595,12 +442,6 @@ int stream_gemm_norm(const void* X, long ldx, const void* W, long ldw, void* out
   p.S = S;
   p.kc = K / S;
   p.epi = epilogue;
-  p.h_out = (bf16*)h_out;
-  p.ss_out = ss_out;
-  p.counters = counters;
-  p.ss_in = ss_in;
-  p.ss_tiles = ss_tiles;
-  p.eps = eps;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();
 }

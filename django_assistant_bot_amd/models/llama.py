@@ -15,7 +15,6 @@ columns (Megatron split); the two all-reduces per layer run on the RCCL process 
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import torch
@@ -74,33 +73,6 @@ class KVCache:
         return 2 * layers * kv_heads * block_size * head_dim * torch.finfo(dtype).bits // 8
 
 
-# Decode RoPE + KV write inside the paged attention launch (``ops.paged_decode_rope``) instead of
-# its own kernel: numerically identical (tests/test_kernels_gpu.py::test_paged_decode_rope_fused)
-# and 1-6 us per layer faster under rocprof, but 0.18 ms per 32-layer step SLOWER in the un-profiled
-# bench (7.75 vs 7.56 ms, same box, profiles/round3_layout_and_parity.md): off by default, kept as
-# an A/B switch (DAB_DECODE_ROPE_FUSED=1).
-_FUSED_DECODE_ROPE = os.environ.get("DAB_DECODE_ROPE_FUSED", "0") == "1"
-
-# Decode RMSNorms inside the GEMMs (``NormPending``: the o / down producers finish their split-K
-# tiles in-launch and leave per-tile sums of squares, qkv / gate_up scale their rows by the norm;
-# gains folded into the weights).  The norm kernel's arithmetic (the gain rounded into the weight
-# instead of the activation) and tested against fp32, but 2.3 % per decode
-# step SLOWER un-profiled (7.65 vs 7.47 ms, profiles/decode_norm_fusion.md): the in-launch tile
-# finish costs three dependent memory round trips (store drain, arrival ticket, slab read), ~6 us,
-# more than the 5 us norm launch it replaces.  Off by default; DAB_DECODE_NORM_FUSED=1 is the A/B
-# switch (benchmarks/decode_ab.py arms base / nofuse).
-_FUSED_DECODE_NORM = os.environ.get("DAB_DECODE_NORM_FUSED", "0") == "1"
-
-
-@dataclass
-class NormPending:
-    """Layer input of the fused decode RMSNorm: the residual stream holds the un-normalised input and
-    ``ss`` [tiles, T] its per-tile row sums of squares (``ops.stream_gemm_res_norm``); the next
-    projection applies the norm (its weight is folded into that projection's columns)."""
-
-    ss: torch.Tensor
-
-
 class LlamaModel:
     def __init__(self, cfg: DecoderConfig, weights: dict, device, tp_group=None, tp_size: int = 1,
                  interleaved_mlp: bool = False, fragment_layout: bool = True, consume: bool = False):
@@ -122,22 +94,9 @@ class LlamaModel:
         self.frag = fragment_layout and self.device.type == "cuda" and self._fragment_ok(weights)
         take = weights.pop if consume else weights.__getitem__
 
-        def proj(key, gain=None):
+        def proj(key):
             t = take(key).to(self.device)
-            if gain is not None:
-                t = (t.float() * gain.float()[None, :]).to(t.dtype)
             return ops.shuffle_weights(t) if self.frag else t
-
-        # On the fragment-layout (GPU) path each RMSNorm gain is folded into the columns of the
-        # projection it feeds (rmsnorm(x) W^T = (x r) (W diag(g))^T) and the norm runs with unit gain:
-        # the decode step can then apply the norm as a per-row scale in the consumer GEMM's epilogue
-        # (``NormPending``), which needs no gain vector.  Same bf16 precision: the rounding moves from
-        # the normalised activation to the folded weight.
-        self.folded_norms = self.frag and _FUSED_DECODE_NORM
-
-        def gain_of(key):
-            g = take(key).to(self.device)
-            return (g, torch.ones_like(g)) if self.folded_norms else (None, g)
 
         self.embed = take("embed").to(self.device)
         self.final_norm = take("final_norm").to(self.device)
@@ -147,19 +106,13 @@ class LlamaModel:
             self.lm_head = ops.shuffle_weights(self.embed) if self.frag else self.embed
         self.layers = []
         for i in range(cfg.layers):
-            g_attn, attn_norm = gain_of(f"l{i}.attn_norm")
-            g_mlp, mlp_norm = gain_of(f"l{i}.mlp_norm")
-            self.layers.append(DecoderLayer(attn_norm, proj(f"l{i}.qkv_w", g_attn), proj(f"l{i}.o_w"), mlp_norm,
-                                            proj(f"l{i}.gate_up_w", g_mlp), proj(f"l{i}.down_w")))
+            self.layers.append(DecoderLayer(take(f"l{i}.attn_norm").to(self.device), proj(f"l{i}.qkv_w"),
+                                            proj(f"l{i}.o_w"), take(f"l{i}.mlp_norm").to(self.device),
+                                            proj(f"l{i}.gate_up_w"), proj(f"l{i}.down_w")))
         if self.frag and consume:
             torch.cuda.empty_cache()
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
-        self.stream_overrides: dict = {}  # projection name -> (stream_gemm cfg, K-slices): tuning runs only
-        # decode-step ablations for upper-bound timing (benchmarks/decode_ab.py; WRONG results):
-        # "norm" skips the two slab-summing RMSNorms, "rope" the RoPE / KV-write kernel
-        self.ablate: set = set()
-        self.decode_norm_fusion = True  # A/B switch of the fused decode RMSNorms (benchmarks/decode_ab.py)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -225,37 +178,15 @@ class LlamaModel:
                 break
         return best
 
-    def _res_norm_cfg(self, name: str, M: int, N: int, K: int):
-        """(stream_gemm cfg, K-slices) of a fused-norm producer (o / down), or None.  64-row tiles x 4
-        slices at M 65..128 (the last slice of a tile sums 4 x 128 x 64 fp32; measured o9_4 -0.6 %,
-        down9_4 +0.6 % as plain slabs), at most 64 tiles (the consumer's loader sums one per row)."""
-        if name in self.stream_overrides:
-            return self.stream_overrides[name]
-        nat = ops.native()
-        if M > 128:
-            return None
-        cfg = 13 if M <= 64 else (9 if N // 64 <= ops.STREAM_SS_MAX else 10)
-        bn = nat.stream_gemm_bn(cfg)
-        if N % bn or N // bn > ops.STREAM_SS_MAX or K % 128:
-            return None
-        return cfg, self._stream_splits(N, K, bn)
+    def _stream_choice(self, name: str, M: int, N: int, K: int) -> tuple[int, int]:
+        """(stream_gemm cfg, K-slices) of a decode projection; cfg -1 = not streamable.  (The tuning
+        harness benchmarks/decode_ab.py overrides this in a subclass.)"""
+        cfg = self._stream_cfg(name, M, N)
+        if cfg < 0 or K % 128:
+            return -1, 1
+        return cfg, self._stream_splits(N, K, ops.native().stream_gemm_bn(cfg))
 
-    def fused_norm_ok(self, T: int) -> bool:
-        """Decode steps of T rows apply the RMSNorms inside the GEMMs (TP 1, fragment layout,
-        folded gains, <= 128 rows: the consumer configurations have a loader thread per row)."""
-        H, F = self.cfg.hidden, self.cfg.intermediate
-        return (self.decode_norm_fusion and self.folded_norms and self.tp_size == 1 and not self.ablate and T <= 128
-                and self._res_norm_cfg("o", T, H, self.hq * self.cfg.head_dim) is not None
-                and self._res_norm_cfg("down", T, H, F) is not None and H % 128 == 0
-                and self._stream_cfg("qkv", T, self.layers[0].qkv_w.shape[0]) >= 0
-                and self._stream_cfg("gate_up", T, self.layers[0].gate_up_w.shape[0]) >= 0)
-
-    def _proj_res_norm(self, x, w, residual, meta: AttnMeta, name: str):
-        cfg, s = self._res_norm_cfg(name, x.shape[0], w.shape[0], w.shape[1])
-        h, ss = ops.stream_gemm_res_norm(x, w, residual, meta.workspace.gemm_cnt, splits=s, cfg=cfg)
-        return h, ss
-
-    def _proj(self, x, w, dec: bool, allow_slabs: bool = True, name: str = "", epilogue=ops.EPI_NONE, ss=None):
+    def _proj(self, x, w, dec: bool, allow_slabs: bool = True, name: str = "", epilogue=ops.EPI_NONE):
         """One projection.  Decode-sized batches (``dec``) stream the fragment-layout weights
         through stream_gemm, as fp32 split-K slabs when a consumer sums them (RMSNorm, the decode
         attention's RoPE prologue) and ``allow_slabs``; everything else runs the MFMA GEMM on the
@@ -266,19 +197,12 @@ class LlamaModel:
                 return ops.silu_mul(y, group=8 if self.interleaved_mlp else 0)
             return ops.linear(x, w)
         if dec and self.frag:
-            cfg = self._stream_cfg(name, x.shape[0], w.shape[0])
-            s = None
-            if name in self.stream_overrides:  # (cfg, splits) of a tuning run (benchmarks/decode_ab.py)
-                cfg, s = self.stream_overrides[name]
-            if cfg >= 0 and w.shape[1] % 128 == 0:
-                eps = self.cfg.eps
+            cfg, s = self._stream_choice(name, x.shape[0], w.shape[0], w.shape[1])
+            if cfg >= 0:
                 if epilogue != ops.EPI_NONE:
-                    return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg, ss=ss, eps=eps)
-                s = s or self._stream_splits(w.shape[0], w.shape[1], ops.native().stream_gemm_bn(cfg))
-                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True, ss=ss, eps=eps)
+                    return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg)
+                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True)
                 return ops.slab_reduce(out) if (s > 1 and not allow_slabs) else out
-        if ss is not None:
-            raise RuntimeError("the fused decode norm needs the streaming GEMM path")
         return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag)
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: KVCache) -> torch.Tensor:
@@ -290,39 +214,32 @@ class LlamaModel:
         # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
         # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
         sk = meta.decode and T <= self.STREAM_MAX_M and x.is_cuda
-        fn = sk and meta.workspace is not None and self.fused_norm_ok(T)
         residual = None
         for li, L in enumerate(self.layers):
-            x, residual = self._layer(li, L, x, residual, meta, kv, sk, fn)
+            x, residual = self._layer(li, L, x, residual, meta, kv, sk)
         return self._final_norm(x, residual)
 
     def _final_norm(self, x, residual):
-        if x is None or isinstance(x, NormPending):  # the residual stream holds the last layer's output
+        if x is None:  # the residual stream holds the last layer's output
             return ops.rmsnorm(residual, self.final_norm, self.cfg.eps)[0]
         return ops.rmsnorm(x, self.final_norm, self.cfg.eps, residual=residual)[0]
 
-    def _layer(self, li: int, L: DecoderLayer, x, residual, meta: AttnMeta, kv: KVCache, sk: bool, fn: bool = False):
-        """One decoder layer: (layer input, residual stream) -> (next layer input, residual stream).
-        ``fn``: decode step with the RMSNorms fused into the GEMMs (x is a ``NormPending`` after layer 0)."""
+    def _layer(self, li: int, L: DecoderLayer, x, residual, meta: AttnMeta, kv: KVCache, sk: bool):
+        """One decoder layer: (layer input, residual stream) -> (next layer input, residual stream)."""
         cfg, D, T = self.cfg, self.cfg.head_dim, meta.positions.numel()  # x may be [S, T, H] split-K slabs
         slabs_ok = self.tp_size == 1  # under TP the partial sums go through the all-reduce as bf16
         # prefill (TP 1): the o / down GEMMs add the residual in their epilogue (gemm256 RES, rounded
         # like the separate bf16 add), so the RMSNorms read and write one tensor instead of two each;
         # x is None then: the residual stream already holds the layer input
         fuse = not sk and self.tp_size == 1 and (x if x is not None else residual).is_cuda
-        ss = None
-        if isinstance(x, NormPending):  # the qkv GEMM applies the norm to the residual stream
-            h, ss = residual, x.ss
-        elif x is None:
+        if x is None:
             h, _ = ops.rmsnorm(residual, L.attn_norm, cfg.eps)
         elif residual is None:
             h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
             residual = x
-        elif sk and "norm" in self.ablate:
-            h = self._ablation_buf(x.shape[-2], x.shape[-1])
         else:
             h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
-        qkv = self._proj(h, L.qkv_w, sk, name="qkv", ss=ss)
+        qkv = self._proj(h, L.qkv_w, sk, name="qkv")
         if (not meta.decode and not meta.n_decode and qkv.is_cuda and qkv.dtype == torch.bfloat16
                 and ops.kernels.flash_rope_ok(D, kv.block_size)):
             # prefill: the RoPE/KV-write kernel writes only K / V; the attention rotates Q on load
@@ -332,18 +249,8 @@ class LlamaModel:
             q = qkv[:, :self.hq * D].view(T, self.hq, D)
             a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                           meta.max_q, causal=True, rope=(meta.positions, self.cos_sin))
-            return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D, fn)
-        if meta.decode and qkv.is_cuda and _FUSED_DECODE_ROPE:
-            # RoPE + KV-cache write in the attention's prologue (one dependent launch less per layer)
-            a = ops.paged_decode_rope(qkv, meta.positions, self.cos_sin, meta.slots, kv.k[li], kv.v[li],
-                                      meta.block_tables, meta.ctx_lens, self.hq, meta.part_size, meta.workspace,
-                                      order=meta.order)
-            return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D, fn)
-        if sk and "rope" in self.ablate:
-            q = self._ablation_buf(T, self.hq * D).view(T, self.hq, D)
-        else:
-            q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv,
-                                  D)
+            return self._layer_tail(L, a, residual, sk, fuse, slabs_ok, T, D)
+        q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
         if meta.decode:
             a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
                                  meta.workspace, order=meta.order)
@@ -352,27 +259,17 @@ class LlamaModel:
         else:
             a = ops.flash_attention_paged(q, kv.k[li], kv.v[li], meta.block_tables, meta.cu_q, meta.ctx_lens,
                                           meta.max_q, causal=True)
-        return self._layer_tail(li, L, a, residual, meta, sk, fuse, slabs_ok, T, D, fn)
+        return self._layer_tail(L, a, residual, sk, fuse, slabs_ok, T, D)
 
-    def _layer_tail(self, li, L, a, residual, meta, sk, fuse, slabs_ok, T, D, fn=False):
+    def _layer_tail(self, L, a, residual, sk, fuse, slabs_ok, T, D):
         """o projection, MLP norm, gate_up (+SwiGLU), down: -> (next layer input, residual stream)."""
         cfg = self.cfg
-        if fn:
-            # decode, norms inside the GEMMs: o adds the residual and leaves per-tile sums of squares,
-            # gate_up scales its rows by the norm before SwiGLU, down does what o did for the next qkv
-            h, ss = self._proj_res_norm(a.view(T, self.hq * D), L.o_w, residual, meta, "o")
-            act = self._proj(h, L.gate_up_w, sk, name="gate_up", epilogue=ops.EPI_SWIGLU8, ss=ss)
-            x, ss = self._proj_res_norm(act, L.down_w, h, meta, "down")
-            return NormPending(ss), x
         if fuse:
             residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual, shuffled=self.frag)
             h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)
         else:
             o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o"))
-            if sk and "norm" in self.ablate:
-                h = self._ablation_buf(T, cfg.hidden)
-            else:
-                h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
+            h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
         # SwiGLU in the GEMM epilogue (8-row [gate | up] groups) on the GPU
         epi = ops.EPI_SWIGLU8 if (self.interleaved_mlp and h.is_cuda) else ops.EPI_NONE
         act = self._proj(h, L.gate_up_w, sk, name="gate_up", epilogue=epi)
@@ -382,12 +279,6 @@ class LlamaModel:
             return None, ops.gemm_bt(act, L.down_w, residual=residual, shuffled=self.frag)
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
         return x, residual
-
-    def _ablation_buf(self, rows: int, cols: int) -> torch.Tensor:
-        buf = getattr(self, "_abl", None)
-        if buf is None or buf.numel() < rows * cols:
-            buf = self._abl = torch.zeros(rows * cols, dtype=torch.bfloat16, device=self.device)
-        return buf[:rows * cols].view(rows, cols)
 
     @staticmethod
     def _mixed_attention(q, kv: KVCache, li: int, meta: AttnMeta) -> torch.Tensor:

@@ -285,8 +285,6 @@ class DecodeWorkspace:
         # partition arrival counters of the in-launch combine (one per (sequence, kv head) <= Hq);
         # zero at rest: the last arriving workgroup resets its counter
         self.cnt = torch.zeros((max_batch * Hq,), dtype=torch.int32, device=device)
-        # per-tile arrival counters of the fused-norm producer GEMMs (stream_gemm_res_norm), same rule
-        self.gemm_cnt = torch.zeros((STREAM_CNT_MAX,), dtype=torch.int32, device=device)
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
@@ -323,59 +321,6 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
     native().paged_decode_attention(ptr(q), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
                                     ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
                                     D, int(part_size), int(max_parts), float(scale), stream(q), ptr(order))
-    return out
-
-
-def paged_decode_rope(qkv, positions, cos_sin, slots, k_cache, v_cache, block_tables, ctx_lens, Hq, part_size=512,
-                      workspace: DecodeWorkspace | None = None, scale=None, out=None, order=None):
-    """``rope_kv_write`` + ``paged_decode`` in ONE launch: the decode attention builds q from the step's
-    QKV projection (bf16 [B, (Hq+2Hkv)D] or fp32 split-K slabs [S, B, (Hq+2Hkv)D]) with RoPE, and the
-    workgroup covering each sequence's last position writes the new rotated key and value into the
-    cache before it streams that partition.  Returns the attention output [B, Hq, D]; the cache
-    holds the new token afterwards, bitwise as after ``rope_kv_write``."""
-    Hkv, bs, D = k_cache.shape[1], k_cache.shape[2], k_cache.shape[3]
-    slabs = qkv.dtype == torch.float32 and qkv.dim() == 3
-    B = qkv.shape[-2]
-    if not qkv.is_cuda:
-        q = rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D)
-        return paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size, workspace, scale, out, order)
-    scale = 1.0 / math.sqrt(D) if scale is None else scale
-    ld = (Hq + 2 * Hkv) * D
-    expect(qkv.shape[-1] == ld, "qkv width mismatch")
-    _i32(positions)
-    _i32(ctx_lens)
-    _i32(block_tables)
-    expect(slots.dtype == torch.int64 and slots.is_contiguous() and slots.numel() >= B, "slots must be int64 [B]")
-    expect(positions.numel() >= B, "positions shorter than the batch")
-    expect(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[1] == D // 2, "cos/sin table")
-    expect_bf16_contig(k_cache, v_cache)
-    expect(k_cache.shape == v_cache.shape, "cache shape mismatch")
-    expect(D in (64, 128), "decode head dim must be 64 or 128")
-    expect(Hq % Hkv == 0 and Hq // Hkv <= 16, "GQA group must be <= 16")
-    expect(part_size % 128 == 0, "part_size must be a multiple of 128")
-    expect(block_tables.shape[0] >= B and ctx_lens.numel() >= B, "block table / ctx_lens rows < batch")
-    if slabs:
-        expect(qkv.is_contiguous(), "slabs must be contiguous")
-    else:
-        expect_bf16_contig(qkv)
-    max_parts = workspace.max_parts if workspace is not None else 1
-    if workspace is None:
-        part_size = max(part_size, ((block_tables.shape[1] * bs + 127) // 128) * 128)
-        ws_o = ws_m = ws_l = ws_c = None
-    else:
-        expect(workspace.o.numel() >= B * Hq * max_parts * D and workspace.cnt.numel() >= B * Hkv,
-               "decode workspace too small")
-        ws_o, ws_m, ws_l, ws_c = workspace.o, workspace.m, workspace.l, workspace.cnt
-    out = torch.empty((B, Hq, D), dtype=torch.bfloat16, device=qkv.device) if out is None else out
-    if order is not None:
-        _i32(order)
-        expect(order.is_cuda and order.numel() >= B, "decode order must hold the batch")
-    native().paged_decode_attention(0, ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
-                                    ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
-                                    D, int(part_size), int(max_parts), float(scale), stream(qkv), ptr(order),
-                                    0 if slabs else ptr(qkv), ptr(qkv) if slabs else 0,
-                                    qkv.shape[0] if slabs else 0, B * ld if slabs else 0, ld, ptr(positions),
-                                    ptr(cos_sin), ptr(slots))
     return out
 
 
@@ -570,55 +515,16 @@ def unshuffle_weights(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
 
 
-STREAM_CNT_MAX = 4096  # producer tiles per fused-norm GEMM (DecodeWorkspace.gemm_cnt)
-STREAM_SS_MAX = 64  # producer tiles a fused-norm consumer sums (stream_gemm.hip ST_SS_MAX)
 
 
-def stream_gemm_res_norm(x, w, residual, counters, splits=1, cfg=0, nt=True):
-    """Producer half of the decode RMSNorm fused across a projection pair: (x w^T + residual) ->
-    (h, ss) where h = bf16(bf16(x w^T) + residual) is the new residual stream [M, N] and ss [N / BN, M]
-    fp32 holds each weight tile's per-row sum of h^2.  The split-K slabs are summed inside the
-    launch by the last slice to finish each tile (``counters``: int32, zero at rest, >= N / BN).  A
-    consumer ``stream_gemm(h, w', ss=ss, eps=eps)`` with w' = w diag(norm weight) then computes
-    rmsnorm(h) w^T without the norm kernel."""
-    if not x.is_cuda:
-        y = (x.float() @ w.float().t()).to(torch.bfloat16)
-        h = (y.float() + residual.float()).to(torch.bfloat16)
-        return h, (h.float() ** 2).sum(1)[None]
-    expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
-    expect(x.stride(-1) == 1 and w.stride(-1) == 1 and w.is_contiguous(), "operands must be K-contiguous")
-    M, K = x.shape
-    N = w.shape[0]
-    bn = native().stream_gemm_bn(cfg)
-    expect(bn > 0 and M <= native().stream_gemm_max_m(cfg), f"stream_gemm cfg {cfg}: bad config or M too large")
-    expect(w.shape[1] == K and N % bn == 0 and K % (splits * STREAM_KS) == 0,
-           f"stream_gemm needs N % {bn} == 0 and K % ({STREAM_KS}*splits) == 0")
-    expect(x.stride(0) % 8 == 0, "row stride must be a multiple of 8")
-    expect(residual.dtype == torch.bfloat16 and residual.stride(-1) == 1 and tuple(residual.shape) == (M, N)
-           and residual.stride(0) % 8 == 0, "residual must be bf16 [M, N]")
-    expect(counters.dtype == torch.int32 and counters.is_cuda and counters.numel() >= N // bn, "counters")
-    slabs = torch.empty((splits, M, N), dtype=torch.float32, device=x.device)
-    h = torch.empty((M, N), dtype=torch.bfloat16, device=x.device)
-    ss = torch.empty((N // bn, M), dtype=torch.float32, device=x.device)
-    native().stream_gemm_norm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(slabs), N, ptr(residual),
-                              residual.stride(0), M, N, K, splits, EPI_NONE, stream(x), int(bool(nt)), int(cfg),
-                              ptr(h), ptr(ss), ptr(counters), 0, 0, 0.0)
-    return h, ss
-
-
-def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0, ss=None, eps=0.0):
+def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0):
     """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): bf16
     [M, N] (optional residual add), SwiGLU [M, N/2] over 16- / 8-row interleaved [gate | up] rows, or
     fp32 K-slice slabs [S, M, N] (their sum is the product; consumers sum them in their prologue or
     ``slab_reduce`` does).  ``cfg`` picks the tile / ring configuration
     (``native().stream_gemm_bn(cfg)`` weight rows per workgroup); ``nt`` streams the weights with
-    non-temporal loads.  ``ss`` ([tiles, M] from ``stream_gemm_res_norm``): x is an un-normalised
-    residual stream and every row of the product is scaled by rsqrt(sum(ss[:, m]) / K + eps) before
-    the epilogue (the fused RMSNorm; the norm weight lives in ``w``).  On the CPU ``w`` is row-major."""
+    non-temporal loads.  On the CPU ``w`` is row-major."""
     if not x.is_cuda:
-        if ss is not None:
-            r = torch.rsqrt(ss.float().sum(0) / x.shape[1] + eps)
-            x = (x.float() * r[:, None]).to(torch.bfloat16)
         return _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual)
     expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
     expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
@@ -648,13 +554,6 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
             out = torch.empty((M, n_out), dtype=torch.bfloat16, device=x.device)
         expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
         ldo = out.stride(0)
-    if ss is not None:
-        expect(ss.dtype == torch.float32 and ss.is_contiguous() and ss.dim() == 2 and ss.shape[1] == M
-               and 1 <= ss.shape[0] <= STREAM_SS_MAX, "ss must be fp32 [tiles <= 64, M]")
-        native().stream_gemm_norm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
-                                  residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue),
-                                  stream(x), int(bool(nt)), int(cfg), 0, 0, 0, ptr(ss), ss.shape[0], float(eps))
-        return out
     native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
                          residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
                          int(bool(nt)), int(cfg))

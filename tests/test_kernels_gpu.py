@@ -258,41 +258,6 @@ def test_paged_decode(Hq, Hkv, split):
         assert torch.equal(ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws), out)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 4, 2)])
-@pytest.mark.parametrize("src", ["slabs", "bf16"])
-@pytest.mark.parametrize("split", [False, True])
-def test_paged_decode_rope_fused(D, Hq, Hkv, src, split):
-    """paged_decode_rope (RoPE + KV write in the decode attention's prologue) against the two-launch
-    form (rope_kv_write, then paged_decode): same attention output and same cache contents, bitwise,
-    and against the fp32 reference.  Contexts straddle block and 512-key partition edges; one padding
-    row (slot -1) must leave the cache untouched."""
-    ctx = [1, 64, 65, 511, 512, 513, 1300, 2049]
-    bs = 64
-    B = len(ctx)
-    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, 160)
-    btc = bt.cpu()
-    slots = torch.tensor([int(btc[i, (c - 1) // bs]) * bs + (c - 1) % bs for i, c in enumerate(ctx)],
-                         dtype=torch.int64, device=DEV)
-    slots[2] = -1  # a padding row of a graph batch: no cache write
-    pos = torch.tensor([c - 1 for c in ctx], dtype=torch.int32, device=DEV)
-    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
-    inv = ref.llama3_inv_freq(D, 500000.0, {"factor": 8.0})
-    cs = ref.rope_cos_sin(inv, 4096).to(DEV)
-    W = (Hq + 2 * Hkv) * D
-    qkv = torch.randn(4, B, W, device=DEV) if src == "slabs" else bf(B, W)
-    ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / 512), DEV) if split else None
-    kc1, vc1 = kc.clone(), vc.clone()
-    q = ops.rope_kv_write(qkv, pos, cs, kc1, vc1, slots, Hq, Hkv, D)
-    exp = ops.paged_decode(q, kc1, vc1, bt, ctxt, 512, ws)
-    kc2, vc2 = kc.clone(), vc.clone()
-    got = ops.paged_decode_rope(qkv, pos, cs, slots, kc2, vc2, bt, ctxt, Hq, 512, ws)
-    assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1)
-    assert torch.equal(got, exp)
-    close(got, ref.paged_decode(q, kc1, vc1, bt, ctxt, 1 / math.sqrt(D)))
-    if split:
-        assert int(ws.cnt.abs().sum()) == 0
-
-
 @pytest.mark.parametrize("M,N,K", [(200, 384, 256), (1, 2304, 768), (513, 1000, 64), (128, 128, 4096)])
 def test_gemm_epilogues(M, N, K):
     A, B = bf(M, K), bf(N, K, scale=0.05)
@@ -418,42 +383,6 @@ def test_stream_gemm(cfg, M, N, K, S):
         close(slabs.sum(0), exp, atol=1e-2, rtol=1e-2)
         res = bf(M, N)
         close(ops.slab_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
-
-
-@pytest.mark.parametrize("pcfg,M,S", [(9, 128, 4), (9, 100, 4), (10, 128, 8), (13, 64, 8), (13, 5, 2), (9, 77, 1)])
-def test_stream_gemm_fused_rmsnorm(pcfg, M, S):
-    """Decode RMSNorm fused across a projection pair vs fp32: producer (slabs summed by the last
-    slice of each tile, + residual -> h, per-tile row sums of h^2), then consumers that apply
-    rmsnorm(h) * g through the folded weight W diag(g): SwiGLU8 (gate_up) and split-K slabs (qkv).
-    Twice with the same counters: the last slice re-arms them."""
-    H, K, F = 1024, 1024, 448
-    x, wo, res = bf(M, K), bf(H, K, scale=0.05), bf(M, H)
-    g = (0.5 + torch.rand(H, device=DEV)).to(torch.bfloat16)
-    cnt = torch.zeros(4096, dtype=torch.int32, device=DEV)
-    h_exp = (ref.gemm_bt(x, wo, out_f32=True).to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
-    eps = 1e-5
-    xn = h_exp.float() * torch.rsqrt((h_exp.float() ** 2).mean(1, keepdim=True) + eps) * g.float()
-    wg, wu, wq = bf(F, H, scale=0.05), bf(F, H, scale=0.05), bf(768, H, scale=0.05)
-    fold = lambda w: (w.float() * g.float()[None]).to(torch.bfloat16)  # noqa: E731
-    w8 = ops.shuffle_weights(ops.interleave_gate_up(fold(wg), fold(wu), 8))
-    wqs = ops.shuffle_weights(fold(wq))
-    gu_exp = torch.nn.functional.silu(xn @ wg.float().t()) * (xn @ wu.float().t())
-    q_exp = xn @ wq.float().t()
-    for _ in range(2):
-        h, ss = ops.stream_gemm_res_norm(x, ops.shuffle_weights(wo), res, cnt, splits=S, cfg=pcfg)
-        torch.cuda.synchronize()
-        assert int(cnt.abs().sum()) == 0
-        bn = ops.native().stream_gemm_bn(pcfg)
-        assert ss.shape == (H // bn, M)
-        close(h, h_exp, atol=3e-2, rtol=2e-2)
-        ss_exp = (h.float() ** 2).view(M, H // bn, bn).sum(-1).t()
-        close(ss, ss_exp, atol=1e-3, rtol=1e-4)
-        gcfg = 20 if M > 64 else 13
-        gu = ops.stream_gemm(h, w8, epilogue=ops.EPI_SWIGLU8, cfg=gcfg, ss=ss, eps=eps, nt=True)
-        close(gu, gu_exp, atol=3e-2, rtol=3e-2)
-        qcfg = 10 if M > 64 else 13
-        q = ops.stream_gemm(h, wqs, splits=4, cfg=qcfg, ss=ss, eps=eps, nt=True)
-        close(q.sum(0), q_exp, atol=3e-2, rtol=3e-2)
 
 
 @pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([0, 1, 3, 5, 6, 8, 10, 13], [5, 64, 128])])

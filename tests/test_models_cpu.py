@@ -238,23 +238,3 @@ def test_tp_checkpoint_load_reads_only_the_rank_slices(tmp_path):
             assert st.bytes_read <= repl + proj / tp * 1.001, (tp, st.bytes_read, repl, proj)
 
 
-def test_fused_norm_op_semantics_cpu():
-    """CPU semantics of the fused decode RMSNorm ops (stream_gemm_res_norm -> stream_gemm(ss=)):
-    the producer returns h = bf16(bf16(x w^T) + residual) and sums of squares whose total is
-    sum(h^2); the consumer with the gain folded into its weight equals rmsnorm(h, g) w2^T."""
-    from django_assistant_bot_amd import ops
-    from django_assistant_bot_amd.ops import reference as ref
-
-    g = torch.Generator().manual_seed(0)
-    M, K, H, N = 5, 64, 128, 96
-    bf = lambda *s: (torch.randn(*s, generator=g) * 0.5).to(torch.bfloat16)  # noqa: E731
-    x, wo, res, w2 = bf(M, K), bf(H, K), bf(M, H), bf(N, H)
-    gain = (0.5 + torch.rand(H, generator=g)).to(torch.bfloat16)
-    h, ss = ops.stream_gemm_res_norm(x, wo, res, counters=None)
-    h_exp = ((x.float() @ wo.float().t()).to(torch.bfloat16).float() + res.float()).to(torch.bfloat16)
-    assert torch.equal(h, h_exp)
-    assert torch.allclose(ss.sum(0), (h.float() ** 2).sum(1), rtol=1e-5)
-    w2f = (w2.float() * gain.float()[None]).to(torch.bfloat16)
-    y = ops.stream_gemm(h, w2f, ss=ss, eps=1e-5)
-    xn = ref.rmsnorm(h, gain, 1e-5)[0]
-    assert torch.allclose(y.float(), xn.float() @ w2.float().t(), atol=0.1, rtol=0.05)

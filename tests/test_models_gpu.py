@@ -271,21 +271,19 @@ def test_engine_json_schema_on_gpu_graphs(bpe_dir):
     assert any(k[2] for k in eng._graphs) and eng.stats.get("json_broken", 0) == 0
 
 
-@pytest.mark.parametrize("fold", [False, True])
-def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32(fold, monkeypatch):
+def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32():
     """Two decoder layers at full Llama-3-8B width (H 4096, 32 / 8 heads, D 128, F 14336, 128k
     vocabulary, Llama-3 RoPE scaling) on the production kernels, vs an independent fp32 PyTorch
     forward of the same bf16-rounded weights:
       * one packed prefill of 128 sequences, 8.3k tokens (gemm256 over fragment-layout weights with
         the residual / SwiGLU8 epilogues, RoPE-on-load flash attention, 8-row-group MLP);
       * one decode step at B = 128 (stream_gemm split-K slabs incl. down at K = 14336, streamed LM
-        head); with ``fold`` the gains are folded into qkv / gate_up and both decode RMSNorms run
-        inside the GEMMs (the DAB_DECODE_NORM_FUSED path)."""
+        head; the slab-summing RMSNorms with non-unit gains)."""
     from django_assistant_bot_amd.models.weights import _gate_up
 
     cfg = decoder_config("llama-3-8b", layers=2)
     w32 = random_decoder_weights(cfg, device=DEV, dtype=torch.float32, seed=3)
-    for i in range(cfg.layers):  # non-unit gains: they are folded into the qkv / gate_up columns
+    for i in range(cfg.layers):  # non-unit norm gains
         for n in ("attn_norm", "mlp_norm"):
             w32[f"l{i}.{n}"] = 0.5 + torch.rand(cfg.hidden, device=DEV, generator=torch.Generator(DEV).manual_seed(i))
     w32 = {k: v.bfloat16().float() for k, v in w32.items()}
@@ -298,11 +296,8 @@ def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32(fold, monkeypatch):
             F_ = v.shape[0] // 2
             v = _gate_up(v[:F_], v[F_:], True)
         wm[k] = v.to(torch.bfloat16)
-    from django_assistant_bot_amd.models import llama as llama_mod
-
-    monkeypatch.setattr(llama_mod, "_FUSED_DECODE_NORM", fold)
     model = LlamaModel(cfg, wm, DEV, interleaved_mlp=True)
-    assert model.frag and model.folded_norms == fold
+    assert model.frag
     del wm
     bs = 64
     nblk = [-(-(n + 1) // bs) for n in lens]
@@ -328,7 +323,6 @@ def test_llama3_8b_width_prefill_8k_and_decode_b128_vs_fp32(fold, monkeypatch):
     ws = ops.DecodeWorkspace(128, cfg.heads, cfg.head_dim, -(-max(lens) // 512) + 1, DEV)
     dmeta = AttnMeta(decode=True, positions=dpos, slots=dslots, block_tables=bt, ctx_lens=dpos + 1, workspace=ws,
                      part_size=2048, order=torch.argsort(-dpos).to(torch.int32))
-    assert model.fused_norm_ok(128) == fold  # both decode RMSNorms inside the GEMMs
     h_dec = model.forward(torch.tensor([s_[-1] for s_ in seqs], **i32), dmeta, kv)
     lg_dec = model.logits(h_dec)
     torch.cuda.synchronize()
