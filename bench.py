@@ -406,6 +406,8 @@ def main():
         while done < total_n:
             if args.qps > 0:  # open loop: everything scheduled to have arrived by now is submitted
                 due = min(len(my_q), int((time.perf_counter() - t_open) * args.qps) + 1)
+                if args.tp > 1:  # the TP group's engines must admit the same requests at the same step
+                    due = pdist.broadcast_int(due, tp_group, dev)
                 if due > next_q:
                     rids = rag.submit(my_q[next_q:due], params, bot_group=0)
                     for j, rid in enumerate(rids):

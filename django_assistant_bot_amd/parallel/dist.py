@@ -110,6 +110,18 @@ def gather_floats(value: float, device) -> list[float]:
     return [float(x.item()) for x in out]
 
 
+def broadcast_int(value: int, group=None, device=None) -> int:
+    """``value`` of the group's first rank on every rank of ``group`` (the world when None): keeps
+    host-side decisions that depend on a rank's own clock (open-loop arrivals) identical across the
+    ranks of a tensor-parallel engine, whose schedulers must see the same requests at the same step."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return value
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    t = torch.tensor([value], dtype=torch.int64, device=device)
+    dist.broadcast(t, src=src, group=group)
+    return int(t.item())
+
+
 def shutdown() -> None:
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()

@@ -93,6 +93,10 @@ def test_bench_config5_eight_rank_rehearsal():
            "--index-rows", "20000", "--batch", "8", "--max-new-tokens", "8", "--qps", "20", "--steps", "1",
            "--warmup", "1", "--no-fast-steps"]
     p = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=420)
+    if p.returncode:  # the launcher's summary ends stderr: keep the ranks' own tracebacks too
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        with open(os.path.join(ROOT, "gpurun_out", "config5_rehearsal.stderr"), "w") as f:
+            f.write(p.stderr)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]
