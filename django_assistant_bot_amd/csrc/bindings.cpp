@@ -150,6 +150,7 @@ PYBIND11_MODULE(_native, m) {
      py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
+  m.def("gemm256_set_m32", &dab::gemm256_set_m32);
   m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, u s, int b_shuf) {
     check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s),
@@ -177,7 +178,7 @@ PYBIND11_MODULE(_native, m) {
     auto* cv = reinterpret_cast<float*>(cand_val);
     auto* ci = reinterpret_cast<int*>(cand_idx);
     int rc = hipErrorInvalidValue;
-    if (M <= 16 && K % 256 == 0 && K <= 1024)
+    if (K % 256 == 0 && ((M <= 64 && K <= 1024) || (M <= 96 && K <= 768)))
       rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
     else if (M < 128)  // 128+ queries fill the persistent 256x256 kernel's tiles (gemm256 G_CAND)
       rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));

@@ -312,11 +312,7 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_f
 //   * LDS rows are 256 B; the 16-B chunk c of row r lives at c ^ f(r), f(r) = (r & 3) << 2 | (r >> 2) & 3:
 //     conflict-free for the 16-row ds_read_b128 lane groups of the K reads AND for the 4-row x 64-B
 //     pieces of the transposed V reads (each row of a 4-row group lands in its own 64-B bank range).
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
+// (f32x16 / mfma32: common.h)
 
 // f(integral_constant<I>) for I in [B, E)
 template <int B, int E, typename F>

@@ -107,6 +107,13 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f32_32x32x16_bf16: lane l (r = l & 31, h = l >> 5) holds A[r][8h..8h+7] / B[8h..8h+7][r];
+// C[row][col = l & 31] with row = (reg & 3) + 8 (reg >> 2) + 4 h
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
 typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 
 // ds_read_b64_tr_b16: per 16-lane group, lane 4q+p supplies the address of row q, columns 4p..4p+3

@@ -333,10 +333,10 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   if (M >= 128 && K % 128 == 0)
     return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s,
                               b_rows);
-  // 1..16 queries: the persistent scan with the queries in LDS; 32..64: the index streams through the
-  // decode GEMM's weight ring (64 queries x 10M rows: 5.88 -> 5.05 ms).  Row-major copies only here;
-  // shuffled copies go through score_candidates_shuf (VectorIndex picks).
-  if (b_rows == 0 && M <= 16 && K % 256 == 0 && K <= 1024)
+  // 1..64 queries (K <= 1024) or 65..96 (K <= 768): the persistent scan with the queries in LDS once
+  // per workgroup (K % 256 == 0); 32..64 at other widths: the index streams through the decode GEMM's weight ring.
+  // Row-major copies only here; shuffled copies go through score_candidates_shuf (VectorIndex picks).
+  if (b_rows == 0 && K % 256 == 0 && ((M <= 64 && K <= 1024) || (M <= 96 && K <= 768)))
     return index_scan_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   if (b_rows == 0 && M >= 32 && M <= 64 && K % 128 == 0)
     return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);

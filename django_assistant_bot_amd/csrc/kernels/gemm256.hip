@@ -77,6 +77,10 @@ __device__ __forceinline__ void wait_vm() {
 
 constexpr int kEpiStores = 16;  // VMEM stores per wave in every epilogue variant
 
+__device__ __forceinline__ unsigned lds_off(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -85,6 +89,12 @@ __device__ __forceinline__ void bar() {
 
 constexpr int kBuf = 65536;   // one K-tile: A0 | A1 | B0 | B1, 16 KB each
 constexpr int kHalf = 16384;  // 128 rows x 128 B
+// G_CAND, M <= kCandMaxM: after the two K-tile buffers, the thresholds [kCandMaxM] fp32, 8 per-wave
+// list counters (64 B) and 8 per-wave candidate lists of kCandW (n, m, score) entries
+constexpr int kCandMaxM = 1024;
+constexpr int kCandW = 288;
+constexpr int kCandExtra = 4 * kCandMaxM + 64 + 8 * kCandW * 12;
+static_assert(2 * kBuf + kCandExtra <= 163840, "LDS");
 
 }  // namespace
 
@@ -98,9 +108,19 @@ __device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int G
   n0 = (inner / gsz) << 8;
 }
 
-template <int EPI, bool BIAS, bool RES, bool SHUF = false>
+// M32: the same schedule, wave tile and staging on v_mfma_f32_32x32x16_bf16 -- per quadrant a wave
+// owns 2 (M) x 1 (N) 32x32 blocks over 4 k-steps of 16 (8 MFMAs of 32 cycles where the 16x16x32 form
+// issues 16 of 16).  The LDS operand bytes per FLOP are those of the 16x16 form (they are set by the
+// wave tile, 64 x 32 per quadrant, not by the MFMA shape); what changes is half the MFMA issue slots
+// and the clock the chip holds on each shape (MI355X_MICROARCH.md 'DVFS give-back' item 7).  The
+// epilogues get 8 contiguous columns per lane from one v_permlane32_swap per register quad pair.
+template <int EPI, bool BIAS, bool RES, bool SHUF = false, bool M32 = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + (EPI == G_CAND ? kCandExtra : 0)];
+  // stores per wave in the epilogue (the next tile's first waits count past them; the candidate
+  // epilogue issues none, or drains the queue itself)
+  constexpr int kEpi = EPI == G_CAND ? 0 : (M32 && (EPI == G_SWIGLU || EPI == G_SWIGLU8)) ? 8 : kEpiStores;
+  static_assert(!(M32 && EPI == G_CAND), "the index candidate scan runs the 16x16x32 form");
 
   // Persistent: one workgroup per CU walks a strided list of tiles.  Blocks b and b+8 share an XCD,
   // so the tile ids are split into 8 contiguous chunks (bijective for any count) and the nper
@@ -123,6 +143,58 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = w >> 2, wc = w & 3;
   const int li = lane & 15, g = lane >> 4;
+
+  // ---- G_CAND candidate lists (see the epilogue): a hit is appended to this wave's LDS list
+  // (LDS atomic slot); a flush applies the row / query group filters and appends to the global
+  // per-query lists.  A full list falls back to the global append directly.
+  float* const thr_s = reinterpret_cast<float*>(smem + 2 * kBuf);
+  int* const ccnt = reinterpret_cast<int*>(smem + 2 * kBuf + 4 * kCandMaxM);
+  int* const c_n = ccnt + 16 + w * kCandW;
+  int* const c_m = ccnt + 16 + 8 * kCandW + w * kCandW;
+  float* const c_v = reinterpret_cast<float*>(ccnt + 16 + 16 * kCandW + w * kCandW);
+  auto cand_global = [&](int m, int n, float v) {
+    const int rg = p.row_group ? p.row_group[n] : 0;
+    const int qg = p.q_group ? p.q_group[m] : -1;
+    if (rg >= 0 && (qg < 0 || rg == qg)) {
+      const int slot = atomicAdd(p.cnt + m, 1);
+      if (slot < p.cap) {
+        p.cand_val[(size_t)m * p.cap + slot] = v;
+        p.cand_idx[(size_t)m * p.cap + slot] = n;
+      }
+    }
+  };
+  // The slot claim, the entry writes and the count read are asm: before a compiler-visible LDS
+  // atomic or store hipcc waits vmcnt(0) for every LDS-DMA in flight (the next tile's K-tiles),
+  // which is the drain these lists exist to avoid.  Each asm waits for its own LDS ops.
+  const unsigned a_cnt = lds_off(ccnt + w);
+  auto cand_push = [&](int m, int n, float v) {
+    int slot;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(slot) : "v"(a_cnt), "v"(1) : "memory");
+    if (slot < kCandW) {
+      asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b32 %4, %5" ::"v"(lds_off(c_n + slot)),
+                   "v"(n), "v"(lds_off(c_m + slot)), "v"(m), "v"(lds_off(c_v + slot)), "v"(v)
+                   : "memory");
+    } else {
+      cand_global(m, n, v);
+    }
+  };
+  auto cand_count = [&]() {
+    int c;
+    asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(c) : "v"(a_cnt) : "memory");
+    return __builtin_amdgcn_readfirstlane(c);
+  };
+  auto cand_flush = [&]() {  // wave-uniform call (rare: the list's high-water mark, and the kernel end)
+    const int c = min(cand_count(), kCandW);
+    for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
+    if (lane == 0) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a_cnt), "v"(0) : "memory");
+  };
+  if constexpr (EPI == G_CAND) {
+    if (p.M <= kCandMaxM) {  // before any LDS-DMA is issued: the barrier drains nothing
+      for (int e = tid; e < p.M; e += 512) thr_s[e] = p.thr[e];
+      if (tid < 8) ccnt[tid] = 0;
+      __syncthreads();
+    }
+  }
 
   // ---- LDS-DMA staging: piece j (0/1) of wave w = half-tile rows 8(8j + w) .. +7
   const int sw = (4 * (w & 1) + (lane >> 4)) & 7;
@@ -170,39 +242,79 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   const int rdB0 = SHUF ? wc * 4096 + lane * 16 : (32 * wc + li) * 128 + 16 * (g ^ swr);
   const int rdB1 = SHUF ? rdB0 + 1024 : (32 * wc + li) * 128 + 16 * ((4 + g) ^ swr);
 
+  // ---- M32 fragment reads: lane (r = lane & 31, h = lane >> 5) reads row r of a 32-row block,
+  // k-step ks's chunk 2 ks + h (row-major halves: physical chunk ^ ((r >> 1) & 7), conflict-free for
+  // the 16-row lane groups; SHUF B: block 2 wc + (r >> 4), 32-k block ks >> 1, fragment lane
+  // (r & 15) + 16 (2 (ks & 1) + h) -- 256 contiguous bytes per 16-lane group)
+  const int r32 = lane & 31, h32 = lane >> 5, s32 = (r32 >> 1) & 7;
+  auto off32 = [&](int row, int ks) { return row * 128 + 16 * ((2 * ks + h32) ^ s32); };
+  const int rdB32s = (2 * wc + (r32 >> 4)) * 2048 + 16 * ((r32 & 15) + 16 * h32);
+
   bf16x8 af[4][2];
   bf16x8 bfr[2][2][2];  // [jh][jn][ks]
   f32x4 acc[2][2][4][2];
+  bf16x8 af32[2][4];    // [i][ks]
+  bf16x8 bf32[2][4];    // [jh][ks]
+  f32x16 acc32[2][2][2];  // [ih][jh][i]
   auto zero_acc = [&]() {
+    if constexpr (M32) {
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+      for (int a = 0; a < 2; ++a)
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int e = 0; e < 16; ++e) acc32[a][b][i][e] = 0.f;
+    } else {
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   zero_acc();
 
 #define G256_READ_A(BUF, IH)                                                                     \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
-    const char* base = smem + (BUF) * kBuf + (IH) * kHalf + i * 2048;                            \
-    af[i][0] = *reinterpret_cast<const bf16x8*>(base + rdA0);                                    \
-    af[i][1] = *reinterpret_cast<const bf16x8*>(base + rdA1);                                    \
+  if constexpr (M32) {                                                                           \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                \
+    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) af32[i][ks] = *reinterpret_cast<const bf16x8*>( \
+        smem + (BUF) * kBuf + (IH) * kHalf + off32(64 * wr + 32 * i + r32, ks));                  \
+  } else {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                              \
+      const char* base = smem + (BUF) * kBuf + (IH) * kHalf + i * 2048;                          \
+      af[i][0] = *reinterpret_cast<const bf16x8*>(base + rdA0);                                  \
+      af[i][1] = *reinterpret_cast<const bf16x8*>(base + rdA1);                                  \
+    }                                                                                            \
   }
 #define G256_READ_B(BUF, JH)                                                                     \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
-    const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf + j * 2048;                \
-    bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                               \
-    bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                               \
+  if constexpr (M32) {                                                                           \
+    const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf;                           \
+    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) bf32[JH][ks] = *reinterpret_cast<const bf16x8*>( \
+        base + (SHUF ? rdB32s + (ks >> 1) * 1024 + (ks & 1) * 512 : off32(32 * wc + r32, ks)));   \
+  } else {                                                                                       \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                              \
+      const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf + j * 2048;              \
+      bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                             \
+      bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                             \
+    }                                                                                            \
   }
 #define G256_MFMA(IH, JH)                                                                        \
   __builtin_amdgcn_s_setprio(1);                                                                 \
-  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                               \
-  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
-  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
-    acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                    \
+  if constexpr (M32) {                                                                           \
+    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                                             \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                \
+      acc32[IH][JH][i] = mfma32(bf32[JH][ks], af32[i][ks], acc32[IH][JH][i]);                    \
+  } else {                                                                                       \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
+      acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                  \
+  }                                                                                              \
   __builtin_amdgcn_s_setprio(0);
 
   const int T = p.K >> 6;  // K-tiles (even, >= 2)
@@ -244,7 +356,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     for (int it = 0; it < iters; ++it) {
       const bool last = it == iters - 1;
       const bool st = !last || more;  // stage phases 3-8
-      // first iteration after an epilogue: kEpiStores younger stores sit in the VM queue
+      // first iteration after an epilogue: kEpi younger stores sit in the VM queue
       const bool fe = after_epi && it == 0;
       const int e = 2 * it, o = e + 1;
       const int ke = last ? 0 : e + 2, ko = last ? 1 : o + 2;
@@ -253,7 +365,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       G256_READ_A(0, 0)
       G256_READ_B(0, 0)
       stage(1, 3, o, rA, rB);
-      if (fe) wait_vm<8 + kEpiStores>();
+      if (fe) wait_vm<8 + kEpi>();
       else wait_vm<8>();
       bar();
       G256_MFMA(0, 0)
@@ -261,7 +373,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       // phase 2
       G256_READ_B(0, 1)
       stage(1, 1, o, rA, rB);
-      if (fe) wait_vm<8 + kEpiStores>();
+      if (fe) wait_vm<8 + kEpi>();
       else wait_vm<8>();
       bar();
       G256_MFMA(0, 1)
@@ -275,7 +387,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       // phase 4
       if (st) {
         stage(0, 2, ke, sa, sb);
-        if (fe) wait_vm<8 + kEpiStores>();
+        if (fe) wait_vm<8 + kEpi>();
         else wait_vm<8>();
       } else {
         wait_vm<0>();
@@ -328,63 +440,235 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
     const long c_rows = min(256, p.M - m0);
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
-    if constexpr (EPI == G_CAND) {
-      // Same lane map as the plain epilogue below (permlane16 pairs: 8 contiguous columns per lane).
-      // The per-row threshold / group and per-column row-group loads are waited for here, which
-      // also retires the next tile's prefetched pieces (as the bias epilogue does); the appends that
-      // follow are younger than every piece a later counted wait looks for, so they only make those
-      // waits stricter.
-      const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
-      float thr_r[2][4];
-      int qg_r[2][4];
-      int rg[2][8];
+    if constexpr (M32) {
+      // acc32[ih][jh][i][reg] = C[m0 + 128 ih + 64 wr + 32 i + r][n0 + 128 jh + 32 wc + 8 (reg >> 2) + 4 h + (reg & 3)]
+      // (r = lane & 31, h = lane >> 5).  One v_permlane32_swap per register of quads 2 pp / 2 pp + 1
+      // leaves lane h with the 8 contiguous columns 16 pp + 8 h .. + 7 of its row.
+      int e_r = r32, e_h = h32, e_wc = wc;
+      asm volatile("" : "+v"(e_r), "+v"(e_h), "+v"(e_wc));
+      auto cols8 = [](const f32x16& a, int pp, float(&o)[8]) {
 #pragma unroll
-      for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = min(m0 + 128 * ih + 64 * wr + 16 * i + e_li, p.M - 1);
-          thr_r[ih][i] = p.thr[m];
-          qg_r[ih][i] = p.q_group ? p.q_group[m] : -1;
+        for (int r = 0; r < 4; ++r) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[8 * pp + r]),
+                                                           __float_as_uint(a[8 * pp + 4 + r]), false, false);
+          o[r] = __uint_as_float(sw[0]);
+          o[4 + r] = __uint_as_float(sw[1]);
         }
-#pragma unroll
-      for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int n = n0 + 128 * jh + 32 * e_wc + cq + r;
-          rg[jh][r] = n >= p.N ? -1 : p.row_group ? p.row_group[n] : 0;
-        }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int m = m0 + 128 * ih + 64 * wr + 16 * i + e_li;
+      };
+      if constexpr (EPI == G_SWIGLU || EPI == G_SWIGLU8) {
+        // G_SWIGLU: 32-row block = [gate 16 | up 16] -> gate reg r pairs with up reg r + 8;
+        // G_SWIGLU8: [gate 8 | up 8] x 2 -> gate reg r with up reg r + 4.  Outputs j = 4 h + r
+        // (quads 0 / 1 of the block's first output group) and 8 + 4 h + r; one swap per pair makes
+        // them 8 contiguous output columns per lane: exactly kEpi = 8 stores per wave.
+        constexpr int UP = EPI == G_SWIGLU ? 8 : 4;
+        float bg[2][8], bu[2][8];
+        if constexpr (BIAS) {
 #pragma unroll
           for (int jh = 0; jh < 2; ++jh) {
-            float o[8];
+            const bf16* bp = p.bias + n0 + 128 * jh + 32 * e_wc + 4 * e_h;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[ih][jh][i][0][r]),
-                                                         __float_as_uint(acc[ih][jh][i][1][r]), false, false);
-              o[r] = __uint_as_float(sw[0]);
-              o[4 + r] = __uint_as_float(sw[1]);
+            for (int q = 0; q < 4; ++q) {  // quad q: 4 columns at 8 q
+              const u32x2 v = *reinterpret_cast<const u32x2*>(bp + 8 * q);
+              float f[4] = {__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
+                            __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u)};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const int reg = 4 * q + r;
+                const bool is_up = EPI == G_SWIGLU ? reg >= 8 : ((reg >> 2) & 1);
+                const int gi = EPI == G_SWIGLU ? (reg & 7) : ((reg >> 3) << 2 | (reg & 3));
+                if (is_up) bu[jh][gi] = f[r];
+                else bg[jh][gi] = f[r];
+              }
             }
-            if (m >= p.M) continue;
-            const int nb = n0 + 128 * jh + 32 * e_wc + cq;
-            const int qg = qg_r[ih][i];
+          }
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
 #pragma unroll
-            for (int r = 0; r < 8; ++r) {
-              const bool ok = rg[jh][r] >= 0 && (qg < 0 || rg[jh][r] == qg);
-              if (ok && o[r] >= thr_r[ih][i]) {
-                const int slot = atomicAdd(p.cnt + m, 1);
-                if (slot < p.cap) {
-                  p.cand_val[(size_t)m * p.cap + slot] = o[r];
-                  p.cand_idx[(size_t)m * p.cap + slot] = nb + r;
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int mr = 128 * ih + 64 * wr + 32 * i + e_r;
+#pragma unroll
+            for (int jh = 0; jh < 2; ++jh) {
+              const f32x16& a = acc32[ih][jh][i];
+              float o0[4], o1[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                // output j = 4 h + r: gate / up registers g0 / g0 + UP; j = 8 + 4 h + r: g1 / g1 + UP
+                const int g0 = r, g1 = EPI == G_SWIGLU ? 4 + r : 8 + r;
+                float gt0 = a[g0], up0 = a[g0 + UP], gt1 = a[g1], up1 = a[g1 + UP];
+                if constexpr (BIAS) {
+                  gt0 += bg[jh][r];
+                  up0 += bu[jh][r];
+                  gt1 += bg[jh][4 + r];
+                  up1 += bu[jh][4 + r];
+                }
+                o0[r] = silu_f(gt0) * up0;
+                o1[r] = silu_f(gt1) * up1;
+              }
+              float o[8];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(o0[r]), __float_as_uint(o1[r]), false,
+                                                                 false);
+                o[r] = __uint_as_float(sw[0]);
+                o[4 + r] = __uint_as_float(sw[1]);
+              }
+              u32x4 v;
+#pragma unroll
+              for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
+              const int oc = (n0 + 128 * jh) / 2 + 16 * e_wc + 8 * e_h;
+              __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, 0);
+            }
+          }
+      } else {
+        u32x4 bq[2][2];  // bias of columns n0 + 128 jh + 32 wc + 16 pp + 8 h .. + 7, packed bf16
+        if constexpr (BIAS) {
+#pragma unroll
+          for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+            for (int pp = 0; pp < 2; ++pp)
+              bq[jh][pp] = *reinterpret_cast<const u32x4*>(p.bias + n0 + 128 * jh + 32 * e_wc + 16 * pp + 8 * e_h);
+        }
+        __amdgpu_buffer_rsrc_t rR = rC;
+        if constexpr (RES) rR = make_rsrc(p.residual + (size_t)m0 * p.ldr, (unsigned)(c_rows * p.ldr * 2));
+        u32x4 rvv[2][2][2][2];  // [ih][i][jh][pp]
+        if constexpr (RES) {
+#pragma unroll
+          for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+              for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+                for (int pp = 0; pp < 2; ++pp)
+                  rvv[ih][i][jh][pp] = __builtin_amdgcn_raw_buffer_load_b128(
+                      rR,
+                      (unsigned)(((128 * ih + 64 * wr + 32 * i + e_r) * p.ldr + n0 + 128 * jh + 32 * e_wc + 16 * pp +
+                                  8 * e_h) *
+                                 2),
+                      0, 0);
+        }
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const int mr = 128 * ih + 64 * wr + 32 * i + e_r;
+#pragma unroll
+            for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+              for (int pp = 0; pp < 2; ++pp) {
+                float o[8];
+                cols8(acc32[ih][jh][i], pp, o);
+                if constexpr (BIAS) {
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) {
+                    o[2 * q] += __uint_as_float(bq[jh][pp][q] << 16);
+                    o[2 * q + 1] += __uint_as_float(bq[jh][pp][q] & 0xffff0000u);
+                  }
+                }
+                if constexpr (EPI == G_GELU) {
+#pragma unroll
+                  for (int k = 0; k < 8; ++k) o[k] = gelu_erf(o[k]);
+                }
+                if constexpr (RES) {
+                  const u32x4 rv = rvv[ih][i][jh][pp];
+#pragma unroll
+                  for (int q = 0; q < 4; ++q) {  // round like a bf16 GEMM output, then the bf16 add (HF)
+                    o[2 * q] = bf2f(f2bf(o[2 * q])) + __uint_as_float(rv[q] << 16);
+                    o[2 * q + 1] = bf2f(f2bf(o[2 * q + 1])) + __uint_as_float(rv[q] & 0xffff0000u);
+                  }
+                }
+                u32x4 v;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
+                if constexpr (BIAS || RES) {
+                  if (ih == 0 && i == 0 && jh == 0 && pp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                const int nc = n0 + 128 * jh + 32 * e_wc + 16 * pp + 8 * e_h;
+                __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
+              }
+          }
+      }
+    } else if constexpr (EPI == G_CAND) {
+      // acc[ih][jh][i][jn][r] = score of query m0 + 128 ih + 64 wr + 16 i + li against index row
+      // n0 + 128 jh + 32 wc + 16 jn + 4 g + r.  M <= kCandMaxM: the thresholds sit in LDS and a hit
+      // (rare: ~26 per 256x256 tile at k = 250) goes to this wave's LDS list; the group filters and
+      // the global appends run when the list is flushed.  The epilogue then issues no vector-memory
+      // op, so the next tile's prefetched K-tiles stay in flight (a vmcnt(0) here drained them on
+      // every tile).  Larger M: per-tile threshold / group loads, waited here.
+      if (p.M <= kCandMaxM) {
+        const float* thr_s = reinterpret_cast<const float*>(smem + 2 * kBuf);
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 128 * ih + 64 * wr + 16 * i + e_li;
+            const float t = m < p.M ? thr_s[m] : __builtin_huge_valf();
+#pragma unroll
+            for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+              for (int jn = 0; jn < 2; ++jn)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                  const int n = n0 + 128 * jh + 32 * e_wc + 16 * jn + 4 * e_g + r;
+                  if (acc[ih][jh][i][jn][r] >= t && n < p.N) cand_push(m, n, acc[ih][jh][i][jn][r]);
+                }
+          }
+        if (cand_count() > kCandW - 64) cand_flush();
+      } else {
+        const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
+        float thr_r[2][4];
+        int qg_r[2][4];
+        int rg[2][8];
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = min(m0 + 128 * ih + 64 * wr + 16 * i + e_li, p.M - 1);
+            thr_r[ih][i] = p.thr[m];
+            qg_r[ih][i] = p.q_group ? p.q_group[m] : -1;
+          }
+#pragma unroll
+        for (int jh = 0; jh < 2; ++jh)
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int n = n0 + 128 * jh + 32 * e_wc + cq + r;
+            rg[jh][r] = n >= p.N ? -1 : p.row_group ? p.row_group[n] : 0;
+          }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int m = m0 + 128 * ih + 64 * wr + 16 * i + e_li;
+#pragma unroll
+            for (int jh = 0; jh < 2; ++jh) {
+              float o[8];
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[ih][jh][i][0][r]),
+                                                           __float_as_uint(acc[ih][jh][i][1][r]), false, false);
+                o[r] = __uint_as_float(sw[0]);
+                o[4 + r] = __uint_as_float(sw[1]);
+              }
+              if (m >= p.M) continue;
+              const int nb = n0 + 128 * jh + 32 * e_wc + cq;
+              const int qg = qg_r[ih][i];
+#pragma unroll
+              for (int r = 0; r < 8; ++r) {
+                const bool ok = rg[jh][r] >= 0 && (qg < 0 || rg[jh][r] == qg);
+                if (ok && o[r] >= thr_r[ih][i]) {
+                  const int slot = atomicAdd(p.cnt + m, 1);
+                  if (slot < p.cap) {
+                    p.cand_val[(size_t)m * p.cap + slot] = o[r];
+                    p.cand_idx[(size_t)m * p.cap + slot] = nb + r;
+                  }
                 }
               }
             }
           }
-        }
+      }
     } else if constexpr (EPI == G_SWIGLU || EPI == G_SWIGLU8) {
       // G_SWIGLU: weight rows interleaved in 16-row groups [gate 16 | up 16]: jn = 0 gate, jn = 1 up.
       // G_SWIGLU8: 8-row groups [gate 8 | up 8] inside every 16-row MFMA block (the decode layout:
@@ -525,6 +809,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     zero_acc();
   }
   if (wr == 0) bar();  // balance the stagger barrier
+  if constexpr (EPI == G_CAND) {
+    if (p.M <= kCandMaxM) cand_flush();
+  }
 #undef G256_READ_A
 #undef G256_READ_B
 #undef G256_MFMA
@@ -566,6 +853,11 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   return hipGetLastError();
 }
 
+// MFMA shape of the 256x256 kernel: 0 = 16x16x32 (default), 1 = 32x32x16 (benchmarks/gemm_bench.py
+// --m32 A/B; see the M32 note at the kernel)
+static int g_gemm256_m32 = 0;
+void gemm256_set_m32(int on) { g_gemm256_m32 = on != 0; }
+
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.
 int gemm256_ok(int M, int N, int K, long lda, long ldb) {
   if (M <= 0 || N <= 0 || N % 256 || K % 128 || K <= 0 || lda % 8 || ldb % 8) return 0;
@@ -603,10 +895,15 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   // persistent: one workgroup (128 KB of LDS) per CU walks a strided tile list
   const int nwg = tiles > cus ? cus : tiles;
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define G256_LAUNCH(E, B, R)                                                                            \
-  do {                                                                                                   \
-    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);  \
-    else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);       \
+#define G256_LAUNCH(E, B, R)                                                                              \
+  do {                                                                                                     \
+    if (g_gemm256_m32) {                                                                                   \
+      if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true, true>), dim3(nwg), dim3(512), 0, s, p); \
+      else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false, true>), dim3(nwg), dim3(512), 0, s, p);       \
+    } else {                                                                                               \
+      if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);      \
+      else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);            \
+    }                                                                                                      \
   } while (0)
   switch (epilogue) {
     case G_NONE:

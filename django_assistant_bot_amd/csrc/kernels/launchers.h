@@ -61,6 +61,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
                        hipStream_t s, int b_rows = 0);
 // b_shuf: B in the ops.shuffle_weights layout (the decode GEMM's copy); epilogue 4 = SwiGLU over
 // 8-row [gate | up] groups
+void gemm256_set_m32(int on);  // MFMA shape A/B switch (benchmarks/gemm_bench.py --m32)
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
             const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
 
@@ -72,7 +73,8 @@ int stream_gemm_bn(int cfg);
 // fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
 int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
                 hipStream_t s);
-// index_scan.hip: persistent scan for 1..16 queries (queries staged in LDS once), K % 256 == 0, K <= 1024
+// index_scan.hip: persistent scan for 1..64 queries at K <= 1024, 65..96 at K <= 768 (queries staged in
+// LDS once), K % 256 == 0
 int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                           hipStream_t s);

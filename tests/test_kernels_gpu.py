@@ -520,7 +520,7 @@ def test_index_threshold_search_matches_full_scan(groups, nq):
     assert (i1 == i2).float().mean() > 0.999
 
 
-@pytest.mark.parametrize("M", [1, 5, 24, 40, 300])
+@pytest.mark.parametrize("M", [1, 5, 24, 40, 300, 1100])
 def test_score_candidates_exact_set(M):
     """Every filtered score >= thr[m] is appended exactly once (the 128x128, streaming and gemm256
     candidate kernels; N not a multiple of 64 / 256)."""
@@ -544,11 +544,35 @@ def test_score_candidates_exact_set(M):
         torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 17, 37, 64, 65, 127, 128, 300])
+@pytest.mark.parametrize("q", [0.9, 0.999])
+def test_score_candidates_gemm256_lds_lists(q):
+    """gemm256's candidate epilogue keeps each wave's hits in an LDS list that is flushed at a high-
+    water mark and at the kernel end; a tile with more hits than the list holds appends the rest
+    directly.  q = 0.9 (~320 hits per wave per tile) drives both; 0.999 the sparse case."""
+    M, N, K = 200, 50_000, 256
+    A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
+    qg = torch.tensor([(-1 if i % 3 == 0 else i % 3) for i in range(M)], device=DEV, dtype=torch.int32)
+    full = ops.gemm_bt(A, B, epilogue=ops.EPI_SCORES, out_f32=True, row_group=rg, q_group=qg)
+    thr = torch.quantile(full.clamp_min(-1.0), q, dim=1).contiguous()
+    cap = 8192
+    cv, ci, cnt = ops.score_candidates(A, B, thr, cap, rg, qg)
+    assert int(cnt.max()) <= cap
+    for m in range(0, M, 7):
+        k = int(cnt[m])
+        got = ci[m, :k].tolist()
+        exp = set((full[m] >= thr[m]).nonzero().flatten().tolist())
+        near = set(((full[m] - thr[m]).abs() < 1e-5).nonzero().flatten().tolist())
+        assert len(set(got)) == len(got) == k and (set(got) ^ exp) <= near
+        torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 17, 37, 64, 65, 96, 97, 127, 128, 300])
 def test_score_candidates_shuffled_exact_set(M):
-    """The scans over a shuffle_weights copy of the rows (1..16 queries: index_scan.hip SHUF;
-    17..64: the streaming kernel's cfg 12; 65..127: cfg 10; 128+: gemm256 G_CAND reading the fragment
-    layout) append exactly the filtered scores >=
+    """The scans over a shuffle_weights copy of the rows (1..96 queries: index_scan.hip SHUF with
+    1-6 16-query tiles in LDS; 97..127: the streaming kernel's cfg 10; 128+: gemm256 G_CAND reading
+    the fragment layout) append exactly the filtered scores >=
     thr[m] (N not a multiple of 128: the copy is zero-padded)."""
     N, K = 100_004, 768
     A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
