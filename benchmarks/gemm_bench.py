@@ -71,8 +71,6 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
     ap.add_argument("--only", default="", help="comma list of op names to run")
-    ap.add_argument("--m32", action="store_true",
-                    help="also time gemm256 on the 32x32x16 MFMA (arm 'm32', numerics checked too)")
     ap.add_argument("--ab-layout", action="store_true",
                     help="llama shapes: also time the row-major weight layout (arm 'rowmajor')")
     args = ap.parse_args()
@@ -98,22 +96,6 @@ def main():
                 arms = arms[:1]
             if args.ab_layout and frag:
                 arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
-            m32 = {}
-            if args.m32:
-                nat_lib = ops.native()
-
-                def run_m32():
-                    nat_lib.gemm256_set_m32(1)
-                    try:
-                        return run_native(a, ws, b, kind, out, frag)
-                    finally:
-                        nat_lib.gemm256_set_m32(0)
-                out.zero_()
-                run_m32()
-                torch.cuda.synchronize()
-                e32, _ = check(a, w, b, kind, out, 256)
-                m32 = {"m32_max_abs_err": round(e32, 5), "m32_ok": e32 <= 0.02 * max(scale, 1.0)}
-                arms.append(("m32", run_m32))
             extra = {}
             for _ in range(args.rounds):
                 for arm, fn in arms:
@@ -137,8 +119,7 @@ def main():
                               "native_tflops": round(flop / tn / 1e6, 1), "lib_tflops": round(flop / tl / 1e6, 1),
                               "speedup": round(tl / tn, 3), "max_abs_err": round(err, 5),
                               "ref_max": round(scale, 3), "ok": err <= 0.02 * max(scale, 1.0),
-                              **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()},
-                              **m32}),
+                              **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()}}),
                   flush=True)
             del a, w, ws, b, out
             torch.cuda.empty_cache()

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[1, 64, 512], help="queries per rank per call")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sample-stride", type=int, default=0,
+                    help="A/B: the threshold search's row-sample stride (0 = VectorIndex default)")
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
                     help="ranks; from a plain process the script starts them itself (parallel/launch.py)")
     args = ap.parse_args()
@@ -51,6 +53,10 @@ def main():
     from django_assistant_bot_amd.parallel import dist as pdist
     from django_assistant_bot_amd.parallel.sharded_index import ShardedIndex
 
+    if args.sample_stride:
+        from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+        VectorIndex.sample_stride = args.sample_stride
     info = pdist.init()
     check_world(args.gpus, info.world_size)
     dev, W, R = info.device, info.world_size, info.rank

@@ -150,7 +150,6 @@ PYBIND11_MODULE(_native, m) {
      py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
-  m.def("gemm256_set_m32", &dab::gemm256_set_m32);
   m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, u s, int b_shuf) {
     check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s),

@@ -108,19 +108,12 @@ __device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int G
   n0 = (inner / gsz) << 8;
 }
 
-// M32: the same schedule, wave tile and staging on v_mfma_f32_32x32x16_bf16 -- per quadrant a wave
-// owns 2 (M) x 1 (N) 32x32 blocks over 4 k-steps of 16 (8 MFMAs of 32 cycles where the 16x16x32 form
-// issues 16 of 16).  The LDS operand bytes per FLOP are those of the 16x16 form (they are set by the
-// wave tile, 64 x 32 per quadrant, not by the MFMA shape); what changes is half the MFMA issue slots
-// and the clock the chip holds on each shape (MI355X_MICROARCH.md 'DVFS give-back' item 7).  The
-// epilogues get 8 contiguous columns per lane from one v_permlane32_swap per register quad pair.
-template <int EPI, bool BIAS, bool RES, bool SHUF = false, bool M32 = false>
+template <int EPI, bool BIAS, bool RES, bool SHUF = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + (EPI == G_CAND ? kCandExtra : 0)];
   // stores per wave in the epilogue (the next tile's first waits count past them; the candidate
   // epilogue issues none, or drains the queue itself)
-  constexpr int kEpi = EPI == G_CAND ? 0 : (M32 && (EPI == G_SWIGLU || EPI == G_SWIGLU8)) ? 8 : kEpiStores;
-  static_assert(!(M32 && EPI == G_CAND), "the index candidate scan runs the 16x16x32 form");
+  constexpr int kEpi = EPI == G_CAND ? 0 : kEpiStores;
 
   // Persistent: one workgroup per CU walks a strided list of tiles.  Blocks b and b+8 share an XCD,
   // so the tile ids are split into 8 contiguous chunks (bijective for any count) and the nper
@@ -242,79 +235,39 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   const int rdB0 = SHUF ? wc * 4096 + lane * 16 : (32 * wc + li) * 128 + 16 * (g ^ swr);
   const int rdB1 = SHUF ? rdB0 + 1024 : (32 * wc + li) * 128 + 16 * ((4 + g) ^ swr);
 
-  // ---- M32 fragment reads: lane (r = lane & 31, h = lane >> 5) reads row r of a 32-row block,
-  // k-step ks's chunk 2 ks + h (row-major halves: physical chunk ^ ((r >> 1) & 7), conflict-free for
-  // the 16-row lane groups; SHUF B: block 2 wc + (r >> 4), 32-k block ks >> 1, fragment lane
-  // (r & 15) + 16 (2 (ks & 1) + h) -- 256 contiguous bytes per 16-lane group)
-  const int r32 = lane & 31, h32 = lane >> 5, s32 = (r32 >> 1) & 7;
-  auto off32 = [&](int row, int ks) { return row * 128 + 16 * ((2 * ks + h32) ^ s32); };
-  const int rdB32s = (2 * wc + (r32 >> 4)) * 2048 + 16 * ((r32 & 15) + 16 * h32);
-
   bf16x8 af[4][2];
   bf16x8 bfr[2][2][2];  // [jh][jn][ks]
   f32x4 acc[2][2][4][2];
-  bf16x8 af32[2][4];    // [i][ks]
-  bf16x8 bf32[2][4];    // [jh][ks]
-  f32x16 acc32[2][2][2];  // [ih][jh][i]
   auto zero_acc = [&]() {
-    if constexpr (M32) {
 #pragma unroll
-      for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b)
+      for (int b = 0; b < 2; ++b)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) acc32[a][b][i][e] = 0.f;
-    } else {
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
 
 #define G256_READ_A(BUF, IH)                                                                     \
-  if constexpr (M32) {                                                                           \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                \
-    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) af32[i][ks] = *reinterpret_cast<const bf16x8*>( \
-        smem + (BUF) * kBuf + (IH) * kHalf + off32(64 * wr + 32 * i + r32, ks));                  \
-  } else {                                                                                       \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                              \
-      const char* base = smem + (BUF) * kBuf + (IH) * kHalf + i * 2048;                          \
-      af[i][0] = *reinterpret_cast<const bf16x8*>(base + rdA0);                                  \
-      af[i][1] = *reinterpret_cast<const bf16x8*>(base + rdA1);                                  \
-    }                                                                                            \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                \
+    const char* base = smem + (BUF) * kBuf + (IH) * kHalf + i * 2048;                            \
+    af[i][0] = *reinterpret_cast<const bf16x8*>(base + rdA0);                                    \
+    af[i][1] = *reinterpret_cast<const bf16x8*>(base + rdA1);                                    \
   }
 #define G256_READ_B(BUF, JH)                                                                     \
-  if constexpr (M32) {                                                                           \
-    const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf;                           \
-    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks) bf32[JH][ks] = *reinterpret_cast<const bf16x8*>( \
-        base + (SHUF ? rdB32s + (ks >> 1) * 1024 + (ks & 1) * 512 : off32(32 * wc + r32, ks)));   \
-  } else {                                                                                       \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                              \
-      const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf + j * 2048;              \
-      bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                             \
-      bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                             \
-    }                                                                                            \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j) {                                                \
+    const char* base = smem + (BUF) * kBuf + 2 * kHalf + (JH) * kHalf + j * 2048;                \
+    bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                               \
+    bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                               \
   }
 #define G256_MFMA(IH, JH)                                                                        \
   __builtin_amdgcn_s_setprio(1);                                                                 \
-  if constexpr (M32) {                                                                           \
-    _Pragma("unroll") for (int ks = 0; ks < 4; ++ks)                                             \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i)                                                \
-      acc32[IH][JH][i] = mfma32(bf32[JH][ks], af32[i][ks], acc32[IH][JH][i]);                    \
-  } else {                                                                                       \
-    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                             \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                \
-    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                \
-      acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                  \
-  }                                                                                              \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                               \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+    acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                    \
   __builtin_amdgcn_s_setprio(0);
 
   const int T = p.K >> 6;  // K-tiles (even, >= 2)
@@ -440,157 +393,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
     const long c_rows = min(256, p.M - m0);
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
-    if constexpr (M32) {
-      // acc32[ih][jh][i][reg] = C[m0 + 128 ih + 64 wr + 32 i + r][n0 + 128 jh + 32 wc + 8 (reg >> 2) + 4 h + (reg & 3)]
-      // (r = lane & 31, h = lane >> 5).  One v_permlane32_swap per register of quads 2 pp / 2 pp + 1
-      // leaves lane h with the 8 contiguous columns 16 pp + 8 h .. + 7 of its row.
-      int e_r = r32, e_h = h32, e_wc = wc;
-      asm volatile("" : "+v"(e_r), "+v"(e_h), "+v"(e_wc));
-      auto cols8 = [](const f32x16& a, int pp, float(&o)[8]) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(a[8 * pp + r]),
-                                                           __float_as_uint(a[8 * pp + 4 + r]), false, false);
-          o[r] = __uint_as_float(sw[0]);
-          o[4 + r] = __uint_as_float(sw[1]);
-        }
-      };
-      if constexpr (EPI == G_SWIGLU || EPI == G_SWIGLU8) {
-        // G_SWIGLU: 32-row block = [gate 16 | up 16] -> gate reg r pairs with up reg r + 8;
-        // G_SWIGLU8: [gate 8 | up 8] x 2 -> gate reg r with up reg r + 4.  Outputs j = 4 h + r
-        // (quads 0 / 1 of the block's first output group) and 8 + 4 h + r; one swap per pair makes
-        // them 8 contiguous output columns per lane: exactly kEpi = 8 stores per wave.
-        constexpr int UP = EPI == G_SWIGLU ? 8 : 4;
-        float bg[2][8], bu[2][8];
-        if constexpr (BIAS) {
-#pragma unroll
-          for (int jh = 0; jh < 2; ++jh) {
-            const bf16* bp = p.bias + n0 + 128 * jh + 32 * e_wc + 4 * e_h;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {  // quad q: 4 columns at 8 q
-              const u32x2 v = *reinterpret_cast<const u32x2*>(bp + 8 * q);
-              float f[4] = {__uint_as_float(v[0] << 16), __uint_as_float(v[0] & 0xffff0000u),
-                            __uint_as_float(v[1] << 16), __uint_as_float(v[1] & 0xffff0000u)};
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int reg = 4 * q + r;
-                const bool is_up = EPI == G_SWIGLU ? reg >= 8 : ((reg >> 2) & 1);
-                const int gi = EPI == G_SWIGLU ? (reg & 7) : ((reg >> 3) << 2 | (reg & 3));
-                if (is_up) bu[jh][gi] = f[r];
-                else bg[jh][gi] = f[r];
-              }
-            }
-          }
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-#pragma unroll
-        for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int mr = 128 * ih + 64 * wr + 32 * i + e_r;
-#pragma unroll
-            for (int jh = 0; jh < 2; ++jh) {
-              const f32x16& a = acc32[ih][jh][i];
-              float o0[4], o1[4];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                // output j = 4 h + r: gate / up registers g0 / g0 + UP; j = 8 + 4 h + r: g1 / g1 + UP
-                const int g0 = r, g1 = EPI == G_SWIGLU ? 4 + r : 8 + r;
-                float gt0 = a[g0], up0 = a[g0 + UP], gt1 = a[g1], up1 = a[g1 + UP];
-                if constexpr (BIAS) {
-                  gt0 += bg[jh][r];
-                  up0 += bu[jh][r];
-                  gt1 += bg[jh][4 + r];
-                  up1 += bu[jh][4 + r];
-                }
-                o0[r] = silu_f(gt0) * up0;
-                o1[r] = silu_f(gt1) * up1;
-              }
-              float o[8];
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(o0[r]), __float_as_uint(o1[r]), false,
-                                                                 false);
-                o[r] = __uint_as_float(sw[0]);
-                o[4 + r] = __uint_as_float(sw[1]);
-              }
-              u32x4 v;
-#pragma unroll
-              for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
-              const int oc = (n0 + 128 * jh) / 2 + 16 * e_wc + 8 * e_h;
-              __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, 0);
-            }
-          }
-      } else {
-        u32x4 bq[2][2];  // bias of columns n0 + 128 jh + 32 wc + 16 pp + 8 h .. + 7, packed bf16
-        if constexpr (BIAS) {
-#pragma unroll
-          for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-            for (int pp = 0; pp < 2; ++pp)
-              bq[jh][pp] = *reinterpret_cast<const u32x4*>(p.bias + n0 + 128 * jh + 32 * e_wc + 16 * pp + 8 * e_h);
-        }
-        __amdgpu_buffer_rsrc_t rR = rC;
-        if constexpr (RES) rR = make_rsrc(p.residual + (size_t)m0 * p.ldr, (unsigned)(c_rows * p.ldr * 2));
-        u32x4 rvv[2][2][2][2];  // [ih][i][jh][pp]
-        if constexpr (RES) {
-#pragma unroll
-          for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-              for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-                for (int pp = 0; pp < 2; ++pp)
-                  rvv[ih][i][jh][pp] = __builtin_amdgcn_raw_buffer_load_b128(
-                      rR,
-                      (unsigned)(((128 * ih + 64 * wr + 32 * i + e_r) * p.ldr + n0 + 128 * jh + 32 * e_wc + 16 * pp +
-                                  8 * e_h) *
-                                 2),
-                      0, 0);
-        }
-#pragma unroll
-        for (int ih = 0; ih < 2; ++ih)
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            const int mr = 128 * ih + 64 * wr + 32 * i + e_r;
-#pragma unroll
-            for (int jh = 0; jh < 2; ++jh)
-#pragma unroll
-              for (int pp = 0; pp < 2; ++pp) {
-                float o[8];
-                cols8(acc32[ih][jh][i], pp, o);
-                if constexpr (BIAS) {
-#pragma unroll
-                  for (int q = 0; q < 4; ++q) {
-                    o[2 * q] += __uint_as_float(bq[jh][pp][q] << 16);
-                    o[2 * q + 1] += __uint_as_float(bq[jh][pp][q] & 0xffff0000u);
-                  }
-                }
-                if constexpr (EPI == G_GELU) {
-#pragma unroll
-                  for (int k = 0; k < 8; ++k) o[k] = gelu_erf(o[k]);
-                }
-                if constexpr (RES) {
-                  const u32x4 rv = rvv[ih][i][jh][pp];
-#pragma unroll
-                  for (int q = 0; q < 4; ++q) {  // round like a bf16 GEMM output, then the bf16 add (HF)
-                    o[2 * q] = bf2f(f2bf(o[2 * q])) + __uint_as_float(rv[q] << 16);
-                    o[2 * q + 1] = bf2f(f2bf(o[2 * q + 1])) + __uint_as_float(rv[q] & 0xffff0000u);
-                  }
-                }
-                u32x4 v;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
-                if constexpr (BIAS || RES) {
-                  if (ih == 0 && i == 0 && jh == 0 && pp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
-                const int nc = n0 + 128 * jh + 32 * e_wc + 16 * pp + 8 * e_h;
-                __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
-              }
-          }
-      }
-    } else if constexpr (EPI == G_CAND) {
+    if constexpr (EPI == G_CAND) {
       // acc[ih][jh][i][jn][r] = score of query m0 + 128 ih + 64 wr + 16 i + li against index row
       // n0 + 128 jh + 32 wc + 16 jn + 4 g + r.  M <= kCandMaxM: the thresholds sit in LDS and a hit
       // (rare: ~26 per 256x256 tile at k = 250) goes to this wave's LDS list; the group filters and
@@ -853,11 +656,6 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   return hipGetLastError();
 }
 
-// MFMA shape of the 256x256 kernel: 0 = 16x16x32 (default), 1 = 32x32x16 (benchmarks/gemm_bench.py
-// --m32 A/B; see the M32 note at the kernel)
-static int g_gemm256_m32 = 0;
-void gemm256_set_m32(int on) { g_gemm256_m32 = on != 0; }
-
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.
 int gemm256_ok(int M, int N, int K, long lda, long ldb) {
   if (M <= 0 || N <= 0 || N % 256 || K % 128 || K <= 0 || lda % 8 || ldb % 8) return 0;
@@ -895,15 +693,10 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   // persistent: one workgroup (128 KB of LDS) per CU walks a strided tile list
   const int nwg = tiles > cus ? cus : tiles;
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define G256_LAUNCH(E, B, R)                                                                              \
-  do {                                                                                                     \
-    if (g_gemm256_m32) {                                                                                   \
-      if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true, true>), dim3(nwg), dim3(512), 0, s, p); \
-      else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false, true>), dim3(nwg), dim3(512), 0, s, p);       \
-    } else {                                                                                               \
-      if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);      \
-      else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);            \
-    }                                                                                                      \
+#define G256_LAUNCH(E, B, R)                                                                            \
+  do {                                                                                                   \
+    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);  \
+    else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);       \
   } while (0)
   switch (epilogue) {
     case G_NONE:

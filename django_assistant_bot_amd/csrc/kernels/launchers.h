@@ -61,7 +61,6 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
                        hipStream_t s, int b_rows = 0);
 // b_shuf: B in the ops.shuffle_weights layout (the decode GEMM's copy); epilogue 4 = SwiGLU over
 // 8-row [gate | up] groups
-void gemm256_set_m32(int on);  // MFMA shape A/B switch (benchmarks/gemm_bench.py --m32)
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
             const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
 
