@@ -1,0 +1,93 @@
+"""Where a gemm256 tile's time goes: per-tile s_memtime stamps (diagnostic STAMP instantiation of
+gemm256.hip) on short-K (bge, index-search) and long-K (Llama prefill) shapes.
+
+For every workgroup and tile, wave 0 records the clock at the tile's first K-iteration, the cycles
+of its K-loop and of its epilogue.  Reported per shape (medians over workgroups and tiles, shader
+clock cycles): K-loop cycles per tile and per 64-deep K-tile, epilogue cycles, the transition
+between one tile's epilogue end and the next tile's start, and the first tile's K-loop (which
+includes the workgroup's prologue wait).  The stamps cost wave 0 one vector store per tile.
+
+    python benchmarks/gemm_stamps.py [--shapes bge-qkv,llama-o]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from django_assistant_bot_amd import ops  # noqa: E402
+from django_assistant_bot_amd.ops.kernels import native, ptr, stream  # noqa: E402
+
+SHAPES = {
+    "bge-qkv": (65536, 2304, 768, "bias", False),
+    "bge-o": (65536, 768, 768, "bias+res", False),
+    "bge-up": (65536, 3072, 768, "gelu", False),
+    "bge-down": (65536, 768, 3072, "bias+res", False),
+    "cand-shape": (512, 262144, 768, "none", True),  # the index search's GEMM shape (plain epilogue)
+    "llama-qkv": (32768, 6144, 4096, "none", True),
+    "llama-o": (32768, 4096, 4096, "res", True),
+}
+
+
+def rand(shape, scale=1.0):
+    return ((torch.rand(shape, device="cuda") * 2 - 1) * scale).to(torch.bfloat16)
+
+
+def run(name, M, N, K, kind, shuf, reps):
+    a, w = rand((M, K)), rand((N, K), 0.05)
+    wb = ops.shuffle_weights(w) if shuf else w
+    c = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
+    bias = rand((N,), 0.5) if "bias" in kind or kind == "gelu" else None
+    res = rand((M, N)) if "res" in kind else None
+    tiles = (M + 255) // 256 * (N // 256)
+    per_wg = -(-tiles // 256) + 1
+    st = torch.zeros((256, per_wg, 4), dtype=torch.int32, device="cuda")
+    epi = 1 if kind == "gelu" else 0
+    nat = native()
+    out = []
+    for _ in range(reps):
+        st.zero_()
+        grid = nat.gemm256_stamped(ptr(a), K, ptr(wb), ptr(c), ptr(bias), ptr(res), M, N, K, epi, int(shuf), ptr(st),
+                                   per_wg, stream(a))
+        torch.cuda.synchronize()
+        out.append(st[:grid].cpu().numpy().astype(np.uint32))
+    s = out[-1]
+    t0 = s[:, :, 0].astype(np.uint64) | (s[:, :, 1].astype(np.uint64) << np.uint64(32))
+    loop, epi_c = s[:, :, 2].astype(np.int64), s[:, :, 3].astype(np.int64)
+    valid = t0 > 0
+    first = loop[:, 0][valid[:, 0]]
+    later = loop[:, 1:][valid[:, 1:]]
+    trans = []
+    for g in range(s.shape[0]):
+        n = int(valid[g].sum())
+        for i in range(n - 1):
+            trans.append(int(t0[g, i + 1]) - int(t0[g, i]) - int(loop[g, i]) - int(epi_c[g, i]))
+    span = [int(t0[g, int(valid[g].sum()) - 1]) + int(loop[g, int(valid[g].sum()) - 1]) +
+            int(epi_c[g, int(valid[g].sum()) - 1]) - int(t0[g, 0]) for g in range(s.shape[0]) if valid[g, 0]]
+    kt = K // 64
+    return {"shape": name, "M": M, "N": N, "K": K, "epilogue": kind, "tiles_per_wg": round(tiles / s.shape[0], 2),
+            "loop_cyc_median": int(np.median(later)) if later.size else None,
+            "loop_cyc_per_ktile": round(float(np.median(later)) / kt, 1) if later.size else None,
+            "first_tile_loop_cyc": int(np.median(first)),
+            "epilogue_cyc_median": int(np.median(epi_c[valid])),
+            "transition_cyc_median": int(np.median(trans)) if trans else None,
+            "wg_span_cyc_median": int(np.median(span)),
+            "loop_share": round(float(loop[valid].sum()) / float(np.sum(span)), 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default=",".join(SHAPES))
+    ap.add_argument("--reps", type=int, default=3)
+    args = ap.parse_args()
+    torch.manual_seed(0)
+    for name in args.shapes.split(","):
+        print(json.dumps(run(name, *SHAPES[name], args.reps)), flush=True)
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

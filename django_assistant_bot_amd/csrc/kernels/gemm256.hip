@@ -61,6 +61,11 @@ struct G256 {
   float* cand_val;       // [M, cap]
   int* cand_idx;         // [M, cap]
   int cap;
+  // STAMP (diagnostic instantiations only, benchmarks/gemm_stamps.py): per workgroup and tile,
+  // wave 0 records {s_memtime at the tile's first K-iteration (lo, hi), cycles of the K-loop, cycles
+  // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
+  u32x4* stamps;
+  int stamp_tiles;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -108,7 +113,7 @@ __device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int G
   n0 = (inner / gsz) << 8;
 }
 
-template <int EPI, bool BIAS, bool RES, bool SHUF = false>
+template <int EPI, bool BIAS, bool RES, bool SHUF = false, bool STAMP = false>
 __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + (EPI == G_CAND ? kCandExtra : 0)];
   // stores per wave in the epilogue (the next tile's first waits count past them; the candidate
@@ -300,7 +305,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // drains everything (one vmcnt(0) per workgroup).  One copy of the body: the variants differ
   // only in uniform (SGPR) values, which keeps hipcc's register allocation of the loop intact.
   bool after_epi = false;
+  int tile_no = 0;
+  unsigned long long st_t0 = 0, st_t1 = 0;
   for (;;) {
+    if constexpr (STAMP) st_t0 = __builtin_amdgcn_s_memtime();
     const int nsid = sid + nper;
     const bool more = nsid < cend;
     int nm0 = m0, nn0 = n0;
@@ -383,6 +391,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       bar();
     }
 
+    if constexpr (STAMP) st_t1 = __builtin_amdgcn_s_memtime();
     // ---- epilogue: acc[ih][jh][i][jn][r] = C[m0 + 128 ih + 64 wr + 16 i + li][n0 + 128 jh + 32 wc + 16 jn + 4 g + r]
     // The next tile's first K-tiles are already in flight; the stores overlap them.  Exactly
     // kEpiStores buffer stores per wave, unconditional (rows >= M fall outside the descriptor and
@@ -602,6 +611,19 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         }
       }
     }
+    if constexpr (STAMP) {
+      // one vector store by lane 0 of wave 0 (its next counted waits only get stricter by it)
+      const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+      if (w == 0 && lane == 0 && tile_no < p.stamp_tiles) {
+        u32x4 v;
+        v[0] = (unsigned)st_t0;
+        v[1] = (unsigned)(st_t0 >> 32);
+        v[2] = (unsigned)(st_t1 - st_t0);
+        v[3] = (unsigned)(t2 - st_t1);
+        p.stamps[(size_t)blockIdx.x * p.stamp_tiles + tile_no] = v;
+      }
+      ++tile_no;
+    }
     after_epi = true;
     if (!more) break;
     sid = nsid;
@@ -654,6 +676,49 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   if (b_rows > 0) hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false, true>), dim3(nwg), dim3(512), 0, s, p);
   else hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false>), dim3(nwg), dim3(512), 0, s, p);
   return hipGetLastError();
+}
+
+// Diagnostic: gemm256 with per-tile s_memtime stamps (epilogues 0 / 1 with optional bias / residual).
+// stamps: [grid][stamp_tiles] u32x4 {t0 lo, t0 hi, K-loop cycles, epilogue cycles}; returns the grid.
+int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
+                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s) {
+  if (!gemm256_ok(M, N, K, lda, K) || (epilogue != G_NONE && epilogue != G_GELU) || (epilogue == G_GELU && residual))
+    return -hipErrorInvalidValue;
+  G256 p{};
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.C = (bf16*)C;
+  p.bias = (const bf16*)bias;
+  p.residual = (const bf16*)residual;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = K;
+  p.ldc = N;
+  p.ldr = N;
+  p.rows_b = N;
+  p.gm = 4;
+  p.stamps = (u32x4*)stamps;
+  p.stamp_tiles = stamp_tiles;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int tiles = ((M + 255) / 256) * (N / 256);
+  const int nwg = tiles > cus ? cus : tiles;
+  const bool hb = bias != nullptr, hr = residual != nullptr;
+#define G256_STAMPED(E, BI, R)                                                                              \
+  do {                                                                                                      \
+    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, BI, R, true, true>), dim3(nwg), dim3(512), 0, s, p);  \
+    else hipLaunchKernelGGL((gemm256_kernel<E, BI, R, false, true>), dim3(nwg), dim3(512), 0, s, p);        \
+  } while (0)
+  if (epilogue == G_GELU) G256_STAMPED(G_GELU, true, false);
+  else if (hb && hr) G256_STAMPED(G_NONE, true, true);
+  else if (hr) G256_STAMPED(G_NONE, false, true);
+  else if (hb) G256_STAMPED(G_NONE, true, false);
+  else G256_STAMPED(G_NONE, false, false);
+#undef G256_STAMPED
+  const int rc = hipGetLastError();
+  return rc ? -rc : nwg;
 }
 
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.

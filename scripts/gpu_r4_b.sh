@@ -14,3 +14,5 @@ for b in 64 512; do
   python scripts/prof_summary.py "$d" run gpurun_out/prof_idx${b}_stats.md --drop-trace || exit $?
   tail -2 gpurun_out/prof_idx$b.log
 done
+cd "$GRAFT_REPO_ROOT" && S=scripts/gpu_step.sh &&
+$S r4b_stride64 300 python -u benchmarks/index_bench.py --iters 10 --warmup 3 --batch 128 512 --sample-stride 64
