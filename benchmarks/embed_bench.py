@@ -25,7 +25,8 @@ def main():
     ap.add_argument("--chunks", type=int, default=1_000_000)
     ap.add_argument("--words", type=int, default=48, help="mean words per chunk (+-50 %)")
     ap.add_argument("--model", default="bge-base-en")
-    ap.add_argument("--max-batch-tokens", type=int, default=65536)
+    ap.add_argument("--max-batch-tokens", type=int, default=262144,
+                    help="tokens per packed encoder batch (64k / 128k / 256k: 100.7k / 102.4k / 103.9k chunks/s, round 4)")
     ap.add_argument("--warmup-chunks", type=int, default=20000)
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
                     help="ranks; from a plain process the script starts them itself (parallel/launch.py)")

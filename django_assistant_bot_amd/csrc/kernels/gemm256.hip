@@ -113,7 +113,7 @@ __device__ __forceinline__ void tile_of(int sid, int tiles_m, int tiles_n, int G
   n0 = (inner / gsz) << 8;
 }
 
-template <int EPI, bool BIAS, bool RES, bool SHUF = false, bool STAMP = false>
+template <int EPI, bool BIAS, bool RES, bool SHUF = false, bool STAMP = false, int SAUX = 0>
 __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kBuf + (EPI == G_CAND ? kCandExtra : 0)];
   // stores per wave in the epilogue (the next tile's first waits count past them; the candidate
@@ -144,7 +144,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 
   // ---- G_CAND candidate lists (see the epilogue): a hit is appended to this wave's LDS list
   // (LDS atomic slot); a flush applies the row / query group filters and appends to the global
-  // per-query lists.  A full list falls back to the global append directly.
+  // per-query lists.  The list is flushed once it holds more than kCandW - 64 entries, so the
+  // (at most 64) hits of one epilogue step always fit.
   float* const thr_s = reinterpret_cast<float*>(smem + 2 * kBuf);
   int* const ccnt = reinterpret_cast<int*>(smem + 2 * kBuf + 4 * kCandMaxM);
   int* const c_n = ccnt + 16 + w * kCandW;
@@ -165,16 +166,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // atomic or store hipcc waits vmcnt(0) for every LDS-DMA in flight (the next tile's K-tiles),
   // which is the drain these lists exist to avoid.  Each asm waits for its own LDS ops.
   const unsigned a_cnt = lds_off(ccnt + w);
+  // the caller keeps the list at <= kCandW - 64 entries before a step's (<= 64) pushes
   auto cand_push = [&](int m, int n, float v) {
     int slot;
     asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(slot) : "v"(a_cnt), "v"(1) : "memory");
-    if (slot < kCandW) {
-      asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b32 %4, %5" ::"v"(lds_off(c_n + slot)),
-                   "v"(n), "v"(lds_off(c_m + slot)), "v"(m), "v"(lds_off(c_v + slot)), "v"(v)
-                   : "memory");
-    } else {
-      cand_global(m, n, v);
-    }
+    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b32 %4, %5" ::"v"(lds_off(c_n + slot)),
+                 "v"(n), "v"(lds_off(c_m + slot)), "v"(m), "v"(lds_off(c_v + slot)), "v"(v)
+                 : "memory");
   };
   auto cand_count = [&]() {
     int c;
@@ -185,6 +183,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     const int c = min(cand_count(), kCandW);
     for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
     if (lane == 0) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a_cnt), "v"(0) : "memory");
+    // retire the flush's memory ops here (the paths the compiler merges after it inherit nothing to
+    // wait for); a flush is rare and drains the prefetch queue anyway
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
   };
   if constexpr (EPI == G_CAND) {
     if (p.M <= kCandMaxM) {  // before any LDS-DMA is issued: the barrier drains nothing
@@ -424,10 +425,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const int n = n0 + 128 * jh + 32 * e_wc + 16 * jn + 4 * e_g + r;
-                  if (acc[ih][jh][i][jn][r] >= t && n < p.N) cand_push(m, n, acc[ih][jh][i][jn][r]);
+                  const bool hit = acc[ih][jh][i][jn][r] >= t && n < p.N;
+                  if (__builtin_amdgcn_ballot_w64(hit)) {
+                    if (hit) cand_push(m, n, acc[ih][jh][i][jn][r]);
+                    if (cand_count() > kCandW - 64) cand_flush();
+                  }
                 }
           }
-        if (cand_count() > kCandW - 64) cand_flush();
       } else {
         const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
         float thr_r[2][4];
@@ -526,7 +530,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             v[0] = pack2bf(o[0], o[1]);
             v[1] = pack2bf(o[2], o[3]);
             const int oc = (n0 + 128 * jh) / 2 + 16 * e_wc + 4 * e_g;
-            __builtin_amdgcn_raw_buffer_store_b64(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, SAUX);
           }
         }
     } else {
@@ -606,7 +610,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             if constexpr (BIAS || RES) {
               if (i == 0 && jh == 0 && ih == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
-            __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, SAUX);
           }
         }
       }
@@ -681,7 +685,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 // Diagnostic: gemm256 with per-tile s_memtime stamps (epilogues 0 / 1 with optional bias / residual).
 // stamps: [grid][stamp_tiles] u32x4 {t0 lo, t0 hi, K-loop cycles, epilogue cycles}; returns the grid.
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
-                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s) {
+                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux) {
   if (!gemm256_ok(M, N, K, lda, K) || (epilogue != G_NONE && epilogue != G_GELU) || (epilogue == G_GELU && residual))
     return -hipErrorInvalidValue;
   G256 p{};
@@ -706,10 +710,18 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
   const int tiles = ((M + 255) / 256) * (N / 256);
   const int nwg = tiles > cus ? cus : tiles;
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define G256_STAMPED(E, BI, R)                                                                              \
-  do {                                                                                                      \
-    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, BI, R, true, true>), dim3(nwg), dim3(512), 0, s, p);  \
-    else hipLaunchKernelGGL((gemm256_kernel<E, BI, R, false, true>), dim3(nwg), dim3(512), 0, s, p);        \
+  // store_aux: cache policy of the epilogue stores (0 default, 2 nt, 16 sc1, 18 sc1 + nt) -- A/B only
+#define G256_STAMPED_AUX(E, BI, R, AX)                                                                            \
+  do {                                                                                                            \
+    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, BI, R, true, true, AX>), dim3(nwg), dim3(512), 0, s, p);   \
+    else hipLaunchKernelGGL((gemm256_kernel<E, BI, R, false, true, AX>), dim3(nwg), dim3(512), 0, s, p);         \
+  } while (0)
+#define G256_STAMPED(E, BI, R)                          \
+  do {                                                  \
+    if (store_aux == 2) G256_STAMPED_AUX(E, BI, R, 2);   \
+    else if (store_aux == 16) G256_STAMPED_AUX(E, BI, R, 16); \
+    else if (store_aux == 18) G256_STAMPED_AUX(E, BI, R, 18); \
+    else G256_STAMPED_AUX(E, BI, R, 0);                  \
   } while (0)
   if (epilogue == G_GELU) G256_STAMPED(G_GELU, true, false);
   else if (hb && hr) G256_STAMPED(G_NONE, true, true);
@@ -717,9 +729,15 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
   else if (hb) G256_STAMPED(G_NONE, true, false);
   else G256_STAMPED(G_NONE, false, false);
 #undef G256_STAMPED
+#undef G256_STAMPED_AUX
   const int rc = hipGetLastError();
   return rc ? -rc : nwg;
 }
+
+// Cache policy of the epilogue's C stores (A/B in benchmarks/gemm_bench.py --store-aux): 0 default,
+// 2 non-temporal, 18 sc1 + non-temporal
+static int g_store_aux = 0;
+void gemm256_set_store_aux(int aux) { g_store_aux = aux; }
 
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.
 int gemm256_ok(int M, int N, int K, long lda, long ldb) {
@@ -758,10 +776,16 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   // persistent: one workgroup (128 KB of LDS) per CU walks a strided tile list
   const int nwg = tiles > cus ? cus : tiles;
   const bool hb = bias != nullptr, hr = residual != nullptr;
-#define G256_LAUNCH(E, B, R)                                                                            \
-  do {                                                                                                   \
-    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true>), dim3(nwg), dim3(512), 0, s, p);  \
-    else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false>), dim3(nwg), dim3(512), 0, s, p);       \
+#define G256_LAUNCH_AUX(E, B, R, AX)                                                                          \
+  do {                                                                                                         \
+    if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true, false, AX>), dim3(nwg), dim3(512), 0, s, p); \
+    else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false, false, AX>), dim3(nwg), dim3(512), 0, s, p);       \
+  } while (0)
+#define G256_LAUNCH(E, B, R)                                  \
+  do {                                                        \
+    if (g_store_aux == 2) G256_LAUNCH_AUX(E, B, R, 2);        \
+    else if (g_store_aux == 18) G256_LAUNCH_AUX(E, B, R, 18); \
+    else G256_LAUNCH_AUX(E, B, R, 0);                         \
   } while (0)
   switch (epilogue) {
     case G_NONE:
@@ -785,6 +809,7 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
     default: return hipErrorInvalidValue;
   }
 #undef G256_LAUNCH
+#undef G256_LAUNCH_AUX
   return hipGetLastError();
 }
 

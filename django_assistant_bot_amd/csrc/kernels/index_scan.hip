@@ -15,8 +15,10 @@
 //     are in flight under the current tile's epilogue;
 //   * queries [16 MT, K] in LDS with chunk c of row r at c ^ (r & 15): conflict-free ds_read_b128
 //     B fragments (one fragment feeds both A tiles' MFMAs; one A fragment feeds MT MFMAs);
-//   * epilogue straight from the accumulators: a score >= thr[query] (rare) loads its row's group
-//     and appends (score, row) to the query's list with one atomic (gemm.hip EPI_CANDIDATES);
+//   * epilogue straight from the accumulators: a score >= thr[query] (rare) takes a slot in the
+//     wave's LDS list; flushing the list applies the row / query group filters and appends to the
+//     query's global list with one returning atomic per hit (gemm.hip EPI_CANDIDATES) -- a wait
+//     that in the tile loop would drain the wave's whole load ring;
 //   * SHUF: the rows come from a copy in the decode-stream layout [rows/16][K/32][64 lanes][8]
 //     (ops.shuffle_weights), where each 16-row x 32-k A fragment is 1 KB contiguous in lane order:
 //     every load is one fully coalesced 1 KB read instead of 16 rows x 64 B.
@@ -48,17 +50,50 @@ constexpr int kScanMaxM = 96;
 constexpr int scan_kmax(int mt) { return mt <= 4 ? kScanKMax : 768; }
 constexpr int kScanRT = 2;     // 16-row A tiles per wave
 constexpr int kScanNWIN = 8;   // chunks (of 32 k) in flight per wave
+constexpr int kScanListW = 160;  // candidate list entries per wave (12 B each)
 
 }  // namespace
 
 template <bool SHUF, int MT, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void index_scan_kernel(ScanParams p) {
   constexpr int RT = kScanRT, NWIN = kScanNWIN, TR = 32 * NW;  // rows per workgroup tile
-  __shared__ __attribute__((aligned(16))) char xs[16 * MT * scan_kmax(MT) * 2];
+  constexpr int XS = 16 * MT * scan_kmax(MT) * 2;
+  __shared__ __attribute__((aligned(16))) char xs[XS + 64 + NW * kScanListW * 12];
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, g = lane >> 4;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int cpr = p.K / 8;  // 16-B chunks per query row
   const int RB = p.K * 2;
+
+  // ---- per-wave candidate lists (after the queries): a hit takes an LDS slot; the group filters
+  // and the global append (a returning atomic, whose wait would drain this wave's whole load ring)
+  // run when the list is flushed -- at a high-water mark and at the end
+  int* const lcnt = reinterpret_cast<int*>(xs + XS);
+  int* const l_n = lcnt + 16 + w * kScanListW;
+  int* const l_m = lcnt + 16 + NW * kScanListW + w * kScanListW;
+  float* const l_v = reinterpret_cast<float*>(lcnt + 16 + 2 * NW * kScanListW + w * kScanListW);
+  auto cand_global = [&](int m, int n, float v) {
+    const int rg = p.row_group ? p.row_group[n] : 0;
+    const int qgm = p.q_group ? p.q_group[m] : -1;
+    if (rg >= 0 && (qgm < 0 || rg == qgm)) {
+      const int slot = atomicAdd(p.cnt + m, 1);
+      if (slot < p.cap) {
+        p.cand_val[(size_t)m * p.cap + slot] = v;
+        p.cand_idx[(size_t)m * p.cap + slot] = n;
+      }
+    }
+  };
+  auto list_count = [&]() {
+    return __builtin_amdgcn_readfirstlane(__hip_atomic_load(lcnt + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  };
+  auto cand_flush = [&]() {  // wave-uniform
+    const int c = list_count();
+    for (int e = lane; e < c; e += 64) cand_global(l_m[e], l_n[e], l_v[e]);
+    if (lane == 0) __hip_atomic_store(lcnt + w, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // retire the flush's own memory ops here, so the code after it (and the hit test of every tile,
+    // which the compiler merges with this path) inherits no pending store or load to wait for
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+  };
+  if (tid < NW) lcnt[tid] = 0;
 
   // ---- queries -> LDS once (rows >= M repeat row M - 1; their scores are never appended)
   for (int e = tid; e < 16 * MT * cpr; e += 64 * NW) {
@@ -67,12 +102,10 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void index_scan_kernel(ScanParams 
     *reinterpret_cast<u32x4*>(xs + r * RB + 16 * (c ^ (r & 15))) = v;
   }
   float thr[MT];
-  int qg[MT];
 #pragma unroll
   for (int t = 0; t < MT; ++t) {
     const int m = 16 * t + li;
     thr[t] = m < p.M ? p.thr[m] : __builtin_huge_valf();
-    qg[t] = (m < p.M && p.q_group) ? p.q_group[m] : -1;
   }
   __syncthreads();
 
@@ -152,19 +185,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void index_scan_kernel(ScanParams 
         for (int r = 0; r < 4; ++r) {
           const int n = r0 + 16 * a + 4 * g + r;
           const float v = acc[a][t][r];
-          if (v >= thr[t] && n < p.N) {
-            const int rg = p.row_group ? p.row_group[n] : 0;
-            if (rg >= 0 && (qg[t] < 0 || rg == qg[t])) {
-              const int m = 16 * t + li;
-              const int slot = atomicAdd(p.cnt + m, 1);
-              if (slot < p.cap) {
-                p.cand_val[(size_t)m * p.cap + slot] = v;
-                p.cand_idx[(size_t)m * p.cap + slot] = n;
-              }
+          const bool hit = v >= thr[t] && n < p.N;
+          // the list holds <= kScanListW - 64 entries here, so the <= 64 hits of one step fit
+          if (__builtin_amdgcn_ballot_w64(hit)) {
+            if (hit) {
+              const int slot = __hip_atomic_fetch_add(lcnt + w, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              l_n[slot] = n;
+              l_m[slot] = 16 * t + li;
+              l_v[slot] = v;
             }
+            if (list_count() > kScanListW - 64) cand_flush();
           }
         }
   }
+  cand_flush();
 }
 
 static int index_scan_launch(bool shuf, const void* X, long ldx, const void* W, long ldw, int M, int N, int K,

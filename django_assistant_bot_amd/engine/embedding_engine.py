@@ -18,7 +18,7 @@ from .tokenizer import Tokenizer
 
 class EmbeddingEngine:
     def __init__(self, model: str | EncoderConfig = "bge-base-en", device=None, weights: dict | None = None,
-                 checkpoint: str | None = None, seed: int = 0, max_batch_tokens: int = 65536,
+                 checkpoint: str | None = None, seed: int = 0, max_batch_tokens: int = 262144,
                  normalize: bool | None = None):
         self.cfg = encoder_config(model) if isinstance(model, str) else model
         if checkpoint is None and weights is None:
