@@ -516,8 +516,16 @@ def test_index_threshold_search_matches_full_scan(groups, nq):
     idx.threshold_search = False
     v2, i2, d2 = idx.search(q, 250, q_groups=qg)
     torch.testing.assert_close(v1, v2)
-    # same scores; ids may differ only among exactly tied scores
-    assert (i1 == i2).float().mean() > 0.999
+    # same scores; ids may differ only among (fp32-rounding) ties: the candidate lists are in no
+    # particular row order and the two paths sum in different kernels.  Where the ids differ the
+    # scores agree, and the id sets differ only in rows tied with the k-th score.
+    diff = i1 != i2
+    torch.testing.assert_close(v1[diff], v2[diff])
+    for r in range(nq):
+        a, b = set(i1[r].tolist()), set(i2[r].tolist())
+        kth = v1[r, -1]
+        tied = set(i1[r][(v1[r] - kth).abs() <= 1e-5].tolist()) | set(i2[r][(v2[r] - kth).abs() <= 1e-5].tolist())
+        assert (a ^ b) <= tied
 
 
 @pytest.mark.parametrize("M", [1, 5, 24, 40, 300, 1100])
