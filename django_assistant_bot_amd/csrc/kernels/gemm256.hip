@@ -66,6 +66,10 @@ struct G256 {
   // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
   u32x4* stamps;
   int stamp_tiles;
+  // start-time stagger (cycles) for the workgroups with odd l = blockIdx / 8: their tiles then end
+  // half a phase-cycle apart from the even ones' and the epilogue store bursts of the chip halve
+  // (A/B via gemm256_stamped; 0 = off)
+  int stagger;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -279,6 +283,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   const int T = p.K >> 6;  // K-tiles (even, >= 2)
   const int iters = T >> 1;
 
+  if (p.stagger > 0 && (l & 1)) {  // s_memtime spin, no memory traffic
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    while (__builtin_amdgcn_s_memtime() - t_start < (unsigned long long)p.stagger) __builtin_amdgcn_s_sleep(8);
+  }
   // prologue (first tile only): K-tile 0 complete, K-tile 1's A0 / B0 in flight
   stage(0, 0, 0, rA, rB);
   stage(0, 2, 0, rA, rB);
@@ -685,7 +693,8 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 // Diagnostic: gemm256 with per-tile s_memtime stamps (epilogues 0 / 1 with optional bias / residual).
 // stamps: [grid][stamp_tiles] u32x4 {t0 lo, t0 hi, K-loop cycles, epilogue cycles}; returns the grid.
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
-                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux) {
+                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux,
+                    int stagger) {
   if (!gemm256_ok(M, N, K, lda, K) || (epilogue != G_NONE && epilogue != G_GELU) || (epilogue == G_GELU && residual))
     return -hipErrorInvalidValue;
   G256 p{};
@@ -705,6 +714,7 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
   p.gm = 4;
   p.stamps = (u32x4*)stamps;
   p.stamp_tiles = stamp_tiles;
+  p.stagger = stagger;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = ((M + 255) / 256) * (N / 256);
@@ -755,7 +765,7 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   if ((epilogue == G_SWIGLU || epilogue == G_SWIGLU8) && residual) return hipErrorInvalidValue;
   if (epilogue == G_SWIGLU8 && bias) return hipErrorInvalidValue;
   if (b_shuf && ldb != K) return hipErrorInvalidValue;
-  G256 p;
+  G256 p{};
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
   p.C = (bf16*)C;
