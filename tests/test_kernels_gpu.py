@@ -317,6 +317,28 @@ def test_gemm256(M, N, K, shuffled):
               ref.silu_mul(ref.gemm_bt(A, torch.cat([wg, wu], 0), torch.cat([bg, bu]))), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("aux,stagger", [(0, 0), (18, 0), (18, 20000)])
+def test_gemm256_stamped_matches_and_stamps(aux, stagger):
+    """The diagnostic STAMP instantiation (benchmarks/gemm_stamps.py) computes the same C as the
+    production launch, whatever its store cache policy and start stagger, and leaves one stamp per
+    tile it ran (K-loop / epilogue cycles > 0)."""
+    from django_assistant_bot_amd.ops.kernels import native, ptr, stream
+
+    M, N, K = 1100, 768, 768  # ragged M, 15 tiles: every workgroup runs 1, some workgroups 0
+    A, B, bias, res = bf(M, K), bf(N, K, scale=0.05), bf(N), bf(M, N)
+    exp = ops.kernels.gemm256(A, B, bias, res)
+    C = torch.empty((M, N), dtype=torch.bfloat16, device=DEV)
+    st = torch.zeros((256, 2, 4), dtype=torch.int32, device=DEV)
+    grid = native().gemm256_stamped(ptr(A), K, ptr(B), ptr(C), ptr(bias), ptr(res), M, N, K, 0, 0, ptr(st), 2,
+                                    stream(A), aux, stagger)
+    torch.cuda.synchronize()
+    assert torch.equal(C, exp)
+    tiles = (M + 255) // 256 * (N // 256)
+    s = st[:grid].cpu()
+    ran = s[:, :, 0] != 0
+    assert int(ran.sum()) == tiles and bool((s[:, :, 2][ran] > 0).all()) and bool((s[:, :, 3][ran] > 0).all())
+
+
 @pytest.mark.parametrize("shuffled", [False, True])
 def test_gemm256_exact_layout(shuffled):
     """Small-integer operands (exact in bf16 and fp32): every output element must match exactly, so a
