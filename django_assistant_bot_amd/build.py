@@ -52,6 +52,29 @@ def _compile(cmd: list[str]) -> tuple[list[str], int, str]:
     return cmd, p.returncode, p.stdout
 
 
+# Kernels allowed a scratch (stack) frame: stream_gemm tuning configurations that no model path
+# launches (cfg 14-16, 24, 26: benchmarks/decode_ab.py only).  Anything else with a frame is a build
+# error -- a runtime-indexed register array the compiler moved to memory (a fully unrolled
+# epilogue that stopped unrolling put gemm256's accumulators there in round 4: 3x slower).
+_SCRATCH_OK = ("stream_gemm_kernelILi8ELi2ELi1ELi128ELi4ELi4ELi4E", "stream_gemm_kernelILi8ELi2ELi1ELi128ELi4ELi4ELi2E",
+               "stream_gemm_kernelILi4ELi2ELi1ELi128ELi4ELi6ELi4E", "stream_gemm_kernelILi16ELi1ELi1ELi128ELi2ELi3ELi1E",
+               "stream_gemm_kernelILi16ELi2ELi1ELi128ELi2ELi2ELi2E")
+
+
+def scratch_kernels(log: str) -> list[tuple[str, int]]:
+    """(kernel, bytes per lane) of every kernel with a scratch frame in a
+    ``-Rpass-analysis=kernel-resource-usage`` compile log."""
+    out, name = [], None
+    for line in log.splitlines():
+        if "Function Name:" in line:
+            name = line.split("Function Name:", 1)[1].split()[0]
+        elif "ScratchSize [bytes/lane]:" in line and name:
+            n = int(line.split("ScratchSize [bytes/lane]:", 1)[1].split()[0])
+            if n:
+                out.append((name, n))
+    return out
+
+
 def build(force: bool = False, jobs: int | None = None, debug: bool = False, verbose: bool = False) -> Path:
     import pybind11
 
@@ -67,7 +90,8 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
         obj = BUILD / (src.stem + ".hip.o")
         objs.append(obj)
         if force or _needs(obj, src, deps):
-            jobs_list.append(([hipcc, f"--offload-arch={ARCH}", *common, "-c", str(src), "-o", str(obj)], obj))
+            jobs_list.append(([hipcc, f"--offload-arch={ARCH}", *common, "-Rpass-analysis=kernel-resource-usage", "-c",
+                               str(src), "-o", str(obj)], obj))
     host_srcs = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
     for src in host_srcs:
         obj = BUILD / (src.stem + ".cpp.o")
@@ -84,6 +108,10 @@ def build(force: bool = False, jobs: int | None = None, debug: bool = False, ver
                 print(log, file=sys.stderr)
             if rc:
                 failed.append(cmd[-1])
+            bad = [(k, b) for k, b in scratch_kernels(log) if not any(a in k for a in _SCRATCH_OK)]
+            if bad and not debug:
+                Path(cmd[-1]).unlink(missing_ok=True)  # rebuilt (and re-checked) next time
+                raise RuntimeError(f"kernels with a scratch frame (runtime-indexed registers): {bad}")
     if failed:
         raise RuntimeError(f"native build failed for: {failed}")
     if force or jobs_list or not out.exists():

@@ -148,8 +148,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 
   // ---- G_CAND candidate lists (see the epilogue): a hit is appended to this wave's LDS list
   // (LDS atomic slot); a flush applies the row / query group filters and appends to the global
-  // per-query lists.  The list is flushed once it holds more than kCandW - 64 entries, so the
-  // (at most 64) hits of one epilogue step always fit.
+  // per-query lists.  The list is flushed after a tile that leaves it more than kCandW - 64 entries
+  // full; a hit that finds it full is appended to the global list directly.
   float* const thr_s = reinterpret_cast<float*>(smem + 2 * kBuf);
   int* const ccnt = reinterpret_cast<int*>(smem + 2 * kBuf + 4 * kCandMaxM);
   int* const c_n = ccnt + 16 + w * kCandW;
@@ -170,13 +170,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // atomic or store hipcc waits vmcnt(0) for every LDS-DMA in flight (the next tile's K-tiles),
   // which is the drain these lists exist to avoid.  Each asm waits for its own LDS ops.
   const unsigned a_cnt = lds_off(ccnt + w);
-  // the caller keeps the list at <= kCandW - 64 entries before a step's (<= 64) pushes
   auto cand_push = [&](int m, int n, float v) {
     int slot;
     asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(slot) : "v"(a_cnt), "v"(1) : "memory");
-    asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b32 %4, %5" ::"v"(lds_off(c_n + slot)),
-                 "v"(n), "v"(lds_off(c_m + slot)), "v"(m), "v"(lds_off(c_v + slot)), "v"(v)
-                 : "memory");
+    if (slot < kCandW) {
+      asm volatile("ds_write_b32 %0, %1\n\tds_write_b32 %2, %3\n\tds_write_b32 %4, %5" ::"v"(lds_off(c_n + slot)),
+                   "v"(n), "v"(lds_off(c_m + slot)), "v"(m), "v"(lds_off(c_v + slot)), "v"(v)
+                   : "memory");
+    } else {
+      cand_global(m, n, v);
+    }
   };
   auto cand_count = [&]() {
     int c;
@@ -433,13 +436,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                   const int n = n0 + 128 * jh + 32 * e_wc + 16 * jn + 4 * e_g + r;
-                  const bool hit = acc[ih][jh][i][jn][r] >= t && n < p.N;
-                  if (__builtin_amdgcn_ballot_w64(hit)) {
-                    if (hit) cand_push(m, n, acc[ih][jh][i][jn][r]);
-                    if (cand_count() > kCandW - 64) cand_flush();
-                  }
+                  if (acc[ih][jh][i][jn][r] >= t && n < p.N) cand_push(m, n, acc[ih][jh][i][jn][r]);
                 }
           }
+        // (a per-step capacity check inside this fully unrolled loop made hipcc keep the loop and
+        // move the accumulators to scratch: the list is checked once per tile, and a step that
+        // finds it full appends directly)
+        if (cand_count() > kCandW - 64) cand_flush();
       } else {
         const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
         float thr_r[2][4];

@@ -137,3 +137,18 @@ def test_every_native_entry_point_called_from_python_is_bound(n):
     assert len(names) > 20
     missing = sorted(x for x in names if not hasattr(n, x))
     assert not missing, missing
+
+
+def test_build_scratch_guard_parses_resource_usage():
+    """The build refuses kernels with a scratch frame (runtime-indexed register arrays moved to
+    memory); the parser reads hipcc's -Rpass-analysis=kernel-resource-usage remarks."""
+    from django_assistant_bot_amd.build import scratch_kernels
+
+    log = "\n".join([
+        "a.hip:1:1: remark: Function Name: _ZN3dab1kILi1EEEvv [-Rpass-analysis=kernel-resource-usage]",
+        "a.hip:1:1: remark:     VGPRs: 96 [-Rpass-analysis=kernel-resource-usage]",
+        "a.hip:1:1: remark:     ScratchSize [bytes/lane]: 0 [-Rpass-analysis=kernel-resource-usage]",
+        "a.hip:9:1: remark: Function Name: _ZN3dab1kILi2EEEvv [-Rpass-analysis=kernel-resource-usage]",
+        "a.hip:9:1: remark:     ScratchSize [bytes/lane]: 528 [-Rpass-analysis=kernel-resource-usage]",
+    ])
+    assert scratch_kernels(log) == [("_ZN3dab1kILi2EEEvv", 528)]
