@@ -71,8 +71,6 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
     ap.add_argument("--only", default="", help="comma list of op names to run")
-    ap.add_argument("--store-aux", type=int, nargs="*", default=[],
-                    help="also time the native arm with these epilogue store cache policies (arms 'aux<N>')")
     ap.add_argument("--ab-layout", action="store_true",
                     help="llama shapes: also time the row-major weight layout (arm 'rowmajor')")
     args = ap.parse_args()
@@ -98,15 +96,6 @@ def main():
                 arms = arms[:1]
             if args.ab_layout and frag:
                 arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
-            nat_lib = ops.native()
-            for ax in args.store_aux:
-                def run_aux(ax=ax):
-                    nat_lib.gemm256_set_store_aux(ax)
-                    try:
-                        return run_native(a, ws, b, kind, out, frag)
-                    finally:
-                        nat_lib.gemm256_set_store_aux(0)
-                arms.append((f"aux{ax}", run_aux))
             extra = {}
             for _ in range(args.rounds):
                 for arm, fn in arms:

@@ -36,7 +36,7 @@ def rand(shape, scale=1.0):
     return ((torch.rand(shape, device="cuda") * 2 - 1) * scale).to(torch.bfloat16)
 
 
-def run(name, M, N, K, kind, shuf, reps, aux=0, stagger=0):
+def run(name, M, N, K, kind, shuf, reps, aux=0):
     a, w = rand((M, K)), rand((N, K), 0.05)
     wb = ops.shuffle_weights(w) if shuf else w
     c = torch.empty((M, N), dtype=torch.bfloat16, device="cuda")
@@ -51,14 +51,14 @@ def run(name, M, N, K, kind, shuf, reps, aux=0, stagger=0):
     for _ in range(reps):
         st.zero_()
         grid = nat.gemm256_stamped(ptr(a), K, ptr(wb), ptr(c), ptr(bias), ptr(res), M, N, K, epi, int(shuf), ptr(st),
-                                   per_wg, stream(a), aux, stagger)
+                                   per_wg, stream(a), aux)
         torch.cuda.synchronize()
         out.append(st[:grid].cpu().numpy().astype(np.uint32))
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     ev[0].record()
     for _ in range(10):
         nat.gemm256_stamped(ptr(a), K, ptr(wb), ptr(c), ptr(bias), ptr(res), M, N, K, epi, int(shuf), ptr(st), per_wg,
-                            stream(a), aux, stagger)
+                            stream(a), aux)
     ev[1].record()
     torch.cuda.synchronize()
     us = ev[0].elapsed_time(ev[1]) * 100.0
@@ -76,7 +76,7 @@ def run(name, M, N, K, kind, shuf, reps, aux=0, stagger=0):
     span = [int(t0[g, int(valid[g].sum()) - 1]) + int(loop[g, int(valid[g].sum()) - 1]) +
             int(epi_c[g, int(valid[g].sum()) - 1]) - int(t0[g, 0]) for g in range(s.shape[0]) if valid[g, 0]]
     kt = K // 64
-    return {"shape": name, "M": M, "N": N, "K": K, "epilogue": kind, "store_aux": aux, "stagger": stagger, "us": round(us, 1),
+    return {"shape": name, "M": M, "N": N, "K": K, "epilogue": kind, "store_aux": aux, "us": round(us, 1),
             "tiles_per_wg": round(tiles / s.shape[0], 2),
             "loop_cyc_median": int(np.median(later)) if later.size else None,
             "loop_cyc_per_ktile": round(float(np.median(later)) / kt, 1) if later.size else None,
@@ -93,18 +93,11 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--aux", type=int, nargs="+", default=[0],
                     help="epilogue store cache policies to compare (0, 2 = nt, 16 = sc1, 18 = sc1 + nt)")
-    ap.add_argument("--stagger", type=float, nargs="+", default=[0.0],
-                    help="start delay of every other workgroup, in tiles (first-tile K-loop cycles)")
     args = ap.parse_args()
     torch.manual_seed(0)
     for name in args.shapes.split(","):
-        base = None
         for aux in args.aux:
-            for st in args.stagger:
-                cyc = int(st * base["first_tile_loop_cyc"]) if (st and base) else 0
-                r = run(name, *SHAPES[name], args.reps, aux, cyc)
-                base = base or r
-                print(json.dumps(r), flush=True)
+            print(json.dumps(run(name, *SHAPES[name], args.reps, aux)), flush=True)
         torch.cuda.empty_cache()
 
 

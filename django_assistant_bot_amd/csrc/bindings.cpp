@@ -151,15 +151,14 @@ PYBIND11_MODULE(_native, m) {
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
   m.def("gemm256_stamped", [](u A, long lda, u B, u C, u bias, u residual, int M, int N, int K, int epilogue,
-                              int b_shuf, u stamps, int stamp_tiles, u s, int store_aux, int stagger) {
+                              int b_shuf, u stamps, int stamp_tiles, u s, int store_aux) {
     const int r = dab::gemm256_stamped(CVP(A), lda, CVP(B), VP(C), CVP(bias), CVP(residual), M, N, K, epilogue, b_shuf,
-                                       VP(stamps), stamp_tiles, ST(s), store_aux, stagger);
+                                       VP(stamps), stamp_tiles, ST(s), store_aux);
     if (r < 0) check(-r, "gemm256_stamped");
     return r;
   }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("C"), py::arg("bias"), py::arg("residual"), py::arg("M"),
      py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("b_shuf"), py::arg("stamps"), py::arg("stamp_tiles"),
-     py::arg("s"), py::arg("store_aux") = 0, py::arg("stagger") = 0);
-  m.def("gemm256_set_store_aux", &dab::gemm256_set_store_aux);
+     py::arg("s"), py::arg("store_aux") = 0);
   m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, u s, int b_shuf) {
     check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s),

@@ -66,10 +66,6 @@ struct G256 {
   // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
   u32x4* stamps;
   int stamp_tiles;
-  // start-time stagger (cycles) for the workgroups with odd l = blockIdx / 8: their tiles then end
-  // half a phase-cycle apart from the even ones' and the epilogue store bursts of the chip halve
-  // (A/B via gemm256_stamped; 0 = off)
-  int stagger;
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -286,10 +282,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   const int T = p.K >> 6;  // K-tiles (even, >= 2)
   const int iters = T >> 1;
 
-  if (p.stagger > 0 && (l & 1)) {  // s_memtime spin, no memory traffic
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    while (__builtin_amdgcn_s_memtime() - t_start < (unsigned long long)p.stagger) __builtin_amdgcn_s_sleep(8);
-  }
   // prologue (first tile only): K-tile 0 complete, K-tile 1's A0 / B0 in flight
   stage(0, 0, 0, rA, rB);
   stage(0, 2, 0, rA, rB);
@@ -696,8 +688,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 // Diagnostic: gemm256 with per-tile s_memtime stamps (epilogues 0 / 1 with optional bias / residual).
 // stamps: [grid][stamp_tiles] u32x4 {t0 lo, t0 hi, K-loop cycles, epilogue cycles}; returns the grid.
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
-                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux,
-                    int stagger) {
+                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux) {
   if (!gemm256_ok(M, N, K, lda, K) || (epilogue != G_NONE && epilogue != G_GELU) || (epilogue == G_GELU && residual))
     return -hipErrorInvalidValue;
   G256 p{};
@@ -717,7 +708,6 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
   p.gm = 4;
   p.stamps = (u32x4*)stamps;
   p.stamp_tiles = stamp_tiles;
-  p.stagger = stagger;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = ((M + 255) / 256) * (N / 256);
@@ -746,11 +736,6 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
   const int rc = hipGetLastError();
   return rc ? -rc : nwg;
 }
-
-// Cache policy of the epilogue's C stores (A/B in benchmarks/gemm_bench.py --store-aux): 0 default,
-// 2 non-temporal, 18 sc1 + non-temporal
-static int g_store_aux = 0;
-void gemm256_set_store_aux(int aux) { g_store_aux = aux; }
 
 // Eligible shapes: N % 256 == 0, K % 128 == 0, 16-B aligned rows, 32-bit buffer offsets.
 int gemm256_ok(int M, int N, int K, long lda, long ldb) {
@@ -794,11 +779,15 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
     if (b_shuf) hipLaunchKernelGGL((gemm256_kernel<E, B, R, true, false, AX>), dim3(nwg), dim3(512), 0, s, p); \
     else hipLaunchKernelGGL((gemm256_kernel<E, B, R, false, false, AX>), dim3(nwg), dim3(512), 0, s, p);       \
   } while (0)
-#define G256_LAUNCH(E, B, R)                                  \
-  do {                                                        \
-    if (g_store_aux == 2) G256_LAUNCH_AUX(E, B, R, 2);        \
-    else if (g_store_aux == 18) G256_LAUNCH_AUX(E, B, R, 18); \
-    else G256_LAUNCH_AUX(E, B, R, 0);                         \
+  // C stores: write-through + non-temporal (sc1 nt) for the short-K bias / GELU projections of the
+  // encoder -- their epilogue burst then retires before the next tile's third K-tile is waited for
+  // (bge qkv 217 -> 203 us, up 338 -> 326 us); the default policy everywhere else, where it measured
+  // faster (residual epilogues, Llama prefill: profiles/gemm_tile_stamps.md)
+  const bool nt_out = K <= 1024 && !residual && !b_shuf;
+#define G256_LAUNCH(E, B, R)                         \
+  do {                                               \
+    if (nt_out) G256_LAUNCH_AUX(E, B, R, 18);        \
+    else G256_LAUNCH_AUX(E, B, R, 0);                \
   } while (0)
   switch (epilogue) {
     case G_NONE:

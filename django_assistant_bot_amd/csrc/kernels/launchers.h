@@ -63,9 +63,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 // 8-row [gate | up] groups
 // diagnostic per-tile s_memtime stamps (benchmarks/gemm_stamps.py); returns the grid or -error
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
-                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux,
-                    int stagger);
-void gemm256_set_store_aux(int aux);  // epilogue store cache policy A/B (gemm_bench --store-aux)
+                    int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux);
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
             const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
 
