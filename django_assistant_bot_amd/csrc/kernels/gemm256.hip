@@ -306,11 +306,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // Every piece is restaged >= 2 phases after its last read.  In the last iteration of a tile the
   // phase 3-8 pieces are the NEXT tile's K-tiles 0 / 1 (same buffers as e+2 / o+2), so the next
   // tile starts without a prologue; after the last tile nothing is staged and the phase-4 wait
-  // drains everything (one vmcnt(0) per workgroup).  The epilogue stages the next tile's K-tile 1
-  // B1 / A1 (phases 1-2's pieces; buffer 1's last reads were in phases 6-7) BEFORE its stores: vmcnt
-  // retires in issue order, so the first wait of the next tile that can depend on the stores is
-  // phase 8's (K-tile 2) instead of phase 5's -- three more phases for the chip-wide store burst
-  // to drain (profiles/gemm_tile_stamps.md).  One copy of the body: the variants differ
+  // drains everything (one vmcnt(0) per workgroup).  One copy of the body: the variants differ
   // only in uniform (SGPR) values, which keeps hipcc's register allocation of the loop intact.
   bool after_epi = false;
   int tile_no = 0;
@@ -330,26 +326,20 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       const int e = 2 * it, o = e + 1;
       const int ke = last ? 0 : e + 2, ko = last ? 1 : o + 2;
       const __amdgpu_buffer_rsrc_t sa = last ? nA : rA, sb = last ? nB : rB;
-      // phase 1 (after an epilogue, K-tile 1's B1 / A1 were staged by it, ahead of its stores)
+      // phase 1
       G256_READ_A(0, 0)
       G256_READ_B(0, 0)
-      if (fe) {
-        wait_vm<10 + kEpi>();
-      } else {
-        stage(1, 3, o, rA, rB);
-        wait_vm<8>();
-      }
+      stage(1, 3, o, rA, rB);
+      if (fe) wait_vm<8 + kEpi>();
+      else wait_vm<8>();
       bar();
       G256_MFMA(0, 0)
       bar();
       // phase 2
       G256_READ_B(0, 1)
-      if (fe) {
-        wait_vm<8 + kEpi>();
-      } else {
-        stage(1, 1, o, rA, rB);
-        wait_vm<8>();
-      }
+      stage(1, 1, o, rA, rB);
+      if (fe) wait_vm<8 + kEpi>();
+      else wait_vm<8>();
       bar();
       G256_MFMA(0, 1)
       bar();
@@ -375,8 +365,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       G256_READ_B(1, 0)
       if (st) {
         stage(0, 3, ke, sa, sb);
-        if (fe) wait_vm<8 + kEpi>();  // K-tile 1's B1 is older than the epilogue stores
-        else wait_vm<8>();
+        wait_vm<8>();
       }
       bar();
       G256_MFMA(0, 0)
@@ -385,8 +374,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       G256_READ_B(1, 1)
       if (st) {
         stage(0, 1, ke, sa, sb);
-        if (fe) wait_vm<8 + kEpi>();  // ... and its A1
-        else wait_vm<8>();
+        wait_vm<8>();
       }
       bar();
       G256_MFMA(0, 1)
@@ -418,16 +406,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
     const long c_rows = min(256, p.M - m0);
     const __amdgpu_buffer_rsrc_t rC = make_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
-    // the next tile's K-tile 1 B1 / A1 (see the schedule note): issued after this epilogue's own
-    // waits (bias / residual loads) and before its first store
-    auto stage_next_k1 = [&]() {
-      if (more) {
-        stage(1, 3, 1, nA, nB);
-        stage(1, 1, 1, nA, nB);
-      }
-    };
     if constexpr (EPI == G_CAND) {
-      stage_next_k1();
       // acc[ih][jh][i][jn][r] = score of query m0 + 128 ih + 64 wr + 16 i + li against index row
       // n0 + 128 jh + 32 wc + 16 jn + 4 g + r.  M <= kCandMaxM: the thresholds sit in LDS and a hit
       // (rare: ~26 per 256x256 tile at k = 250) goes to this wave's LDS list; the group filters and
@@ -528,7 +507,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      stage_next_k1();
 #pragma unroll
       for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
@@ -632,9 +610,8 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
             u32x4 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) v[q] = pack2bf(o[2 * q], o[2 * q + 1]);
-            if (i == 0 && jh == 0 && ih == 0) {
-              if constexpr (BIAS || RES) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-              stage_next_k1();
+            if constexpr (BIAS || RES) {
+              if (i == 0 && jh == 0 && ih == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, SAUX);
           }
