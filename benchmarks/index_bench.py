@@ -42,8 +42,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sample-stride", type=int, default=0,
                     help="A/B: the threshold search's row-sample stride (0 = VectorIndex default)")
-    ap.add_argument("--scan-ring", type=int, nargs="*", default=[],
-                    help="A/B: also time each batch with the persistent scan's ring at these depths (8 / 12)")
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
                     help="ranks; from a plain process the script starts them itself (parallel/launch.py)")
     args = ap.parse_args()
@@ -85,20 +83,7 @@ def main():
         pdist.barrier(info)
         el = pdist.max_over_ranks(time.perf_counter() - t0, dev)
         per_call = el / args.iters
-        ring = {}
-        for depth in args.scan_ring:
-            from django_assistant_bot_amd.ops.kernels import native
-
-            native().index_scan_set_deep(int(depth == 12))
-            index.search(q, args.k)
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            for _ in range(args.iters):
-                index.search(q, args.k)
-            torch.cuda.synchronize(dev)
-            ring[f"ring{depth}_ms"] = round(1000 * (time.perf_counter() - t1) / args.iters, 3)
-            native().index_scan_set_deep(1)
-        results.append({"queries_per_rank": B, "ms_per_search": round(1000 * per_call, 3), **ring,
+        results.append({"queries_per_rank": B, "ms_per_search": round(1000 * per_call, 3),
                         "queries_per_s": round(W * B / per_call, 1),
                         "scan_TBps": round(args.rows * args.dim * 2 / per_call / 1e12, 2)})
         assert ids.shape == (B, args.k)

@@ -177,7 +177,6 @@ PYBIND11_MODULE(_native, m) {
   });
   // candidates over a shuffle_weights copy of the rows (b_rows of them): 1..16 queries on the
   // persistent scan, 17..128 on the weight-streaming kernel, more on the 8-phase GEMM
-  m.def("index_scan_set_deep", &dab::index_scan_set_deep);
   m.def("score_candidates_shuf", [](u A, long lda, u Wshuf, int M, int N, int K, u row_group, u q_group, u thr,
                                     u cnt, u cand_val, u cand_idx, int cap, u s, int b_rows) {
     auto* rg = reinterpret_cast<const int*>(row_group);

@@ -54,9 +54,9 @@ constexpr int kScanListW = 160;  // candidate list entries per wave (12 B each)
 
 }  // namespace
 
-template <bool SHUF, int MT, int NW, int NWIN = kScanNWIN>
+template <bool SHUF, int MT, int NW>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void index_scan_kernel(ScanParams p) {
-  constexpr int RT = kScanRT, TR = 32 * NW;  // rows per workgroup tile
+  constexpr int RT = kScanRT, NWIN = kScanNWIN, TR = 32 * NW;  // rows per workgroup tile
   constexpr int XS = 16 * MT * scan_kmax(MT) * 2;
   __shared__ __attribute__((aligned(16))) char xs[XS + 64 + NW * kScanListW * 12];
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, g = lane >> 4;
@@ -201,10 +201,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void index_scan_kernel(ScanParams 
   cand_flush();
 }
 
-// A/B switch of the 12-chunk ring (benchmarks/index_bench.py --scan-ring)
-static int g_scan_deep = 1;
-void index_scan_set_deep(int on) { g_scan_deep = on != 0; }
-
 static int index_scan_launch(bool shuf, const void* X, long ldx, const void* W, long ldw, int M, int N, int K,
                              const int* row_group, const int* q_group, const float* thr, int* cnt, float* cand_val,
                              int* cand_idx, int cap, hipStream_t s) {
@@ -229,17 +225,10 @@ static int index_scan_launch(bool shuf, const void* X, long ldx, const void* W, 
   const int nw = mt <= 2 ? 4 : 8, per_cu = 8 / nw;
   const long tiles = (N + 32L * nw - 1) / (32L * nw);
   const int grid = (int)(tiles < (long)per_cu * cus ? tiles : (long)per_cu * cus);
-  // ring depth: 12 chunks in flight per wave where the chunks per tile allow it (K = 768), else 8
-  const bool deep = g_scan_deep && (K / 32) % 12 == 0;
-#define SCAN_LAUNCH_R(MT_, NW_, R_)                                                                          \
-  do {                                                                                                       \
-    if (shuf) hipLaunchKernelGGL((index_scan_kernel<true, MT_, NW_, R_>), dim3(grid), dim3(64 * NW_), 0, s, p); \
-    else hipLaunchKernelGGL((index_scan_kernel<false, MT_, NW_, R_>), dim3(grid), dim3(64 * NW_), 0, s, p);     \
-  } while (0)
-#define SCAN_LAUNCH(MT_, NW_)                     \
-  do {                                            \
-    if (deep) SCAN_LAUNCH_R(MT_, NW_, 12);        \
-    else SCAN_LAUNCH_R(MT_, NW_, kScanNWIN);      \
+#define SCAN_LAUNCH(MT_, NW_)                                                                        \
+  do {                                                                                               \
+    if (shuf) hipLaunchKernelGGL((index_scan_kernel<true, MT_, NW_>), dim3(grid), dim3(64 * NW_), 0, s, p); \
+    else hipLaunchKernelGGL((index_scan_kernel<false, MT_, NW_>), dim3(grid), dim3(64 * NW_), 0, s, p);     \
   } while (0)
   switch (mt) {
     case 1: SCAN_LAUNCH(1, 4); break;
@@ -250,7 +239,6 @@ static int index_scan_launch(bool shuf, const void* X, long ldx, const void* W, 
     default: SCAN_LAUNCH(6, 8); break;
   }
 #undef SCAN_LAUNCH
-#undef SCAN_LAUNCH_R
   return hipGetLastError();
 }
 

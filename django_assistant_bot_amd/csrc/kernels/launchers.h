@@ -77,7 +77,6 @@ int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, co
                 hipStream_t s);
 // index_scan.hip: persistent scan for 1..64 queries at K <= 1024, 65..96 at K <= 768 (queries staged in
 // LDS once), K % 256 == 0
-void index_scan_set_deep(int on);  // A/B of the 12-chunk ring (index_bench --scan-ring)
 int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,
                           const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                           hipStream_t s);
