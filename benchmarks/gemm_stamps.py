@@ -7,7 +7,10 @@ clock cycles): K-loop cycles per tile and per 64-deep K-tile, epilogue cycles, t
 between one tile's epilogue end and the next tile's start, and the first tile's K-loop (which
 includes the workgroup's prologue wait).  The stamps cost wave 0 one vector store per tile.
 
-    python benchmarks/gemm_stamps.py [--shapes bge-qkv,llama-o]
+    python benchmarks/gemm_stamps.py [--shapes bge-qkv,llama-o] [--cand 0.0016 0.0004]
+
+--cand runs the index search's candidate GEMM (thresholds set for the given hit fraction) instead
+of / besides the plain shapes; its epilogue cycles include the candidate-list flushes.
 """
 import argparse
 import json
@@ -61,8 +64,56 @@ def run(name, M, N, K, kind, shuf, reps, aux=0):
                             stream(a), aux)
     ev[1].record()
     torch.cuda.synchronize()
-    us = ev[0].elapsed_time(ev[1]) * 100.0
-    s = out[-1]
+    res = {"shape": name, "M": M, "N": N, "K": K, "epilogue": kind, "store_aux": aux,
+           "us": round(ev[0].elapsed_time(ev[1]) * 100.0, 1)}
+    res.update(summarize(out[-1], K, tiles))
+    return res
+
+
+def run_cand(M, N, K, hit_frac, reps, flush_mode=1):
+    """The index search's candidate GEMM (shuffled index copy, thresholds from a 64k-row slice at the
+    given hit fraction: 0.0016 = the 1/64 sample's k = 250 bound over 10M rows)."""
+    a, w = rand((M, K)), rand((N, K))
+    a = a / a.float().norm(dim=1, keepdim=True).to(a.dtype)
+    w = w / w.float().norm(dim=1, keepdim=True).to(w.dtype)
+    wb = ops.shuffle_weights(w)
+    del w
+    sc = a.float() @ rand((65536, K)).float().T
+    kk = max(1, int(round(65536 * hit_frac)))
+    thr = sc.topk(kk, dim=1).values[:, -1].contiguous()
+    del sc
+    cap = max(64, int(N * hit_frac * 4))
+    cnt = torch.zeros(M, dtype=torch.int32, device="cuda")
+    cv = torch.empty(M * cap, dtype=torch.float32, device="cuda")
+    ci = torch.empty(M * cap, dtype=torch.int32, device="cuda")
+    tiles = (M + 255) // 256 * ((N + 255) // 256)
+    per_wg = -(-tiles // 256) + 1
+    st = torch.zeros((256, per_wg, 4), dtype=torch.int32, device="cuda")
+    nat = native()
+
+    def launch():
+        cnt.zero_()
+        return nat.gemm256_candidates_stamped(ptr(a), K, ptr(wb), M, N, K, wb.shape[0], ptr(thr), ptr(cnt), ptr(cv),
+                                              ptr(ci), cap, ptr(st), per_wg, stream(a), flush_mode)
+    out = []
+    for _ in range(reps):
+        st.zero_()
+        grid = launch()
+        torch.cuda.synchronize()
+        out.append(st[:grid].cpu().numpy().astype(np.uint32))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(10):
+        launch()
+    ev[1].record()
+    torch.cuda.synchronize()
+    res = summarize(out[-1], K, tiles)
+    res.update({"shape": "cand", "flush_mode": flush_mode, "M": M, "N": N, "K": K, "hit_frac": hit_frac,
+                "hits_per_tile": round(float(cnt.sum()) / tiles, 1), "us": round(ev[0].elapsed_time(ev[1]) * 100.0, 1)})
+    return res
+
+
+def summarize(s, K, tiles):
     t0 = s[:, :, 0].astype(np.uint64) | (s[:, :, 1].astype(np.uint64) << np.uint64(32))
     loop, epi_c = s[:, :, 2].astype(np.int64), s[:, :, 3].astype(np.int64)
     valid = t0 > 0
@@ -76,12 +127,13 @@ def run(name, M, N, K, kind, shuf, reps, aux=0):
     span = [int(t0[g, int(valid[g].sum()) - 1]) + int(loop[g, int(valid[g].sum()) - 1]) +
             int(epi_c[g, int(valid[g].sum()) - 1]) - int(t0[g, 0]) for g in range(s.shape[0]) if valid[g, 0]]
     kt = K // 64
-    return {"shape": name, "M": M, "N": N, "K": K, "epilogue": kind, "store_aux": aux, "us": round(us, 1),
-            "tiles_per_wg": round(tiles / s.shape[0], 2),
+    ev = epi_c[valid]
+    return {"tiles_per_wg": round(tiles / s.shape[0], 2),
             "loop_cyc_median": int(np.median(later)) if later.size else None,
             "loop_cyc_per_ktile": round(float(np.median(later)) / kt, 1) if later.size else None,
             "first_tile_loop_cyc": int(np.median(first)),
-            "epilogue_cyc_median": int(np.median(epi_c[valid])),
+            "epilogue_cyc_median": int(np.median(ev)), "epilogue_cyc_mean": int(np.mean(ev)),
+            "epilogue_cyc_p95": int(np.percentile(ev, 95)),
             "transition_cyc_median": int(np.median(trans)) if trans else None,
             "wg_span_cyc_median": int(np.median(span)),
             "loop_share": round(float(loop[valid].sum()) / float(np.sum(span)), 3)}
@@ -93,9 +145,18 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--aux", type=int, nargs="+", default=[0],
                     help="epilogue store cache policies to compare (0, 2 = nt, 16 = sc1, 18 = sc1 + nt)")
+    ap.add_argument("--cand", type=float, nargs="*", default=[],
+                    help="hit fractions for the candidate-GEMM stamps (0.0016 = the 1/64 sample's bound)")
+    ap.add_argument("--cand-m", type=int, default=512)
+    ap.add_argument("--flush-mode", type=int, nargs="+", default=[1])
+    ap.add_argument("--cand-n", type=int, default=1 << 20)
     args = ap.parse_args()
     torch.manual_seed(0)
-    for name in args.shapes.split(","):
+    for frac in args.cand:
+        for fm in args.flush_mode:
+            print(json.dumps(run_cand(args.cand_m, args.cand_n, 768, frac, args.reps, fm)), flush=True)
+        torch.cuda.empty_cache()
+    for name in (args.shapes.split(",") if args.shapes else []):
         for aux in args.aux:
             print(json.dumps(run(name, *SHAPES[name], args.reps, aux)), flush=True)
         torch.cuda.empty_cache()

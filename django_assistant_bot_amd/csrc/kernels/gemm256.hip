@@ -66,6 +66,7 @@ struct G256 {
   // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
   u32x4* stamps;
   int stamp_tiles;
+  int flush_mode;  // A/B (pending measurement): 0 = one global round trip per 64 entries, 1 = pipelined
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -184,7 +185,39 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   };
   auto cand_flush = [&]() {  // wave-uniform call (rare: the list's high-water mark, and the kernel end)
     const int c = min(cand_count(), kCandW);
-    for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
+    if (p.flush_mode == 0) {
+      for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
+    } else {
+      // every entry's group loads, then every slot claim, then the stores: one round trip of each
+      // kind per flush instead of one per 64 entries
+      constexpr int R = (kCandW + 63) / 64;
+      int fm[R], fn[R], fs[R], rg[R], qg[R];
+      float fv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int e = lane + 64 * r;
+        const bool ok = e < c;
+        fm[r] = ok ? c_m[e] : 0;
+        fn[r] = ok ? c_n[e] : 0;
+        fv[r] = ok ? c_v[e] : 0.f;
+        fs[r] = p.cap;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bool ok = lane + 64 * r < c;
+        rg[r] = !ok ? -1 : p.row_group ? p.row_group[fn[r]] : 0;
+        qg[r] = ok && p.q_group ? p.q_group[fm[r]] : -1;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (rg[r] >= 0 && (qg[r] < 0 || rg[r] == qg[r])) fs[r] = atomicAdd(p.cnt + fm[r], 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        if (fs[r] < p.cap) {
+          p.cand_val[(size_t)fm[r] * p.cap + fs[r]] = fv[r];
+          p.cand_idx[(size_t)fm[r] * p.cap + fs[r]] = fn[r];
+        }
+    }
     if (lane == 0) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a_cnt), "v"(0) : "memory");
     // retire the flush's memory ops here (the paths the compiler merges after it inherit nothing to
     // wait for); a flush is rare and drains the prefetch queue anyway
@@ -652,6 +685,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 // Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
 // index rows B [N, K], any N; K % 128 == 0.
 // b_rows > 0: B is a shuffle_weights copy of b_rows >= N rows (b_rows % 16 == 0, ldb == K).
+static int g_cand_flush = 1;
+void gemm256_set_flush_mode(int m) { g_cand_flush = m; }
+
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                        const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                        hipStream_t s, int b_rows) {
@@ -676,6 +712,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   p.cand_idx = cand_idx;
   p.cap = cap;
   p.rows_b = b_rows;
+  p.flush_mode = g_cand_flush;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
@@ -683,6 +720,40 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   if (b_rows > 0) hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false, true>), dim3(nwg), dim3(512), 0, s, p);
   else hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false>), dim3(nwg), dim3(512), 0, s, p);
   return hipGetLastError();
+}
+
+// Diagnostic: the candidate GEMM over a shuffled index copy (b_rows >= N rows) with per-tile stamps
+// (layout as gemm256_stamped).  No group filters.  Returns the grid.
+int gemm256_candidates_stamped(const void* A, long lda, const void* B, int M, int N, int K, int b_rows,
+                               const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap, void* stamps,
+                               int stamp_tiles, hipStream_t s, int flush_mode) {
+  if (M <= 0 || N <= 0 || M > kCandMaxM || K % 128 || lda % 8 || cap <= 0 || b_rows < N || b_rows % 16)
+    return -hipErrorInvalidValue;
+  G256 p{};
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldb = K;
+  p.gm = 4;
+  p.thr = thr;
+  p.cnt = cnt;
+  p.cand_val = cand_val;
+  p.cand_idx = cand_idx;
+  p.cap = cap;
+  p.rows_b = b_rows;
+  p.stamps = (u32x4*)stamps;
+  p.stamp_tiles = stamp_tiles;
+  p.flush_mode = flush_mode;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
+  const int nwg = tiles > cus ? cus : (int)tiles;
+  hipLaunchKernelGGL((gemm256_kernel<G_CAND, false, false, true, true>), dim3(nwg), dim3(512), 0, s, p);
+  const int rc = hipGetLastError();
+  return rc ? -rc : nwg;
 }
 
 // Diagnostic: gemm256 with per-tile s_memtime stamps (epilogues 0 / 1 with optional bias / residual).
