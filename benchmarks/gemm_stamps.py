@@ -70,7 +70,7 @@ def run(name, M, N, K, kind, shuf, reps, aux=0):
     return res
 
 
-def run_cand(M, N, K, hit_frac, reps, flush_mode=1):
+def run_cand(M, N, K, hit_frac, reps):
     """The index search's candidate GEMM (shuffled index copy, thresholds from a 64k-row slice at the
     given hit fraction: 0.0016 = the 1/64 sample's k = 250 bound over 10M rows)."""
     a, w = rand((M, K)), rand((N, K))
@@ -78,10 +78,11 @@ def run_cand(M, N, K, hit_frac, reps, flush_mode=1):
     w = w / w.float().norm(dim=1, keepdim=True).to(w.dtype)
     wb = ops.shuffle_weights(w)
     del w
-    sc = a.float() @ rand((65536, K)).float().T
+    sl = rand((65536, K)).float()
+    sc = a.float() @ (sl / sl.norm(dim=1, keepdim=True)).T
     kk = max(1, int(round(65536 * hit_frac)))
     thr = sc.topk(kk, dim=1).values[:, -1].contiguous()
-    del sc
+    del sc, sl
     cap = max(64, int(N * hit_frac * 4))
     cnt = torch.zeros(M, dtype=torch.int32, device="cuda")
     cv = torch.empty(M * cap, dtype=torch.float32, device="cuda")
@@ -94,7 +95,7 @@ def run_cand(M, N, K, hit_frac, reps, flush_mode=1):
     def launch():
         cnt.zero_()
         return nat.gemm256_candidates_stamped(ptr(a), K, ptr(wb), M, N, K, wb.shape[0], ptr(thr), ptr(cnt), ptr(cv),
-                                              ptr(ci), cap, ptr(st), per_wg, stream(a), flush_mode)
+                                              ptr(ci), cap, ptr(st), per_wg, stream(a))
     out = []
     for _ in range(reps):
         st.zero_()
@@ -108,7 +109,7 @@ def run_cand(M, N, K, hit_frac, reps, flush_mode=1):
     ev[1].record()
     torch.cuda.synchronize()
     res = summarize(out[-1], K, tiles)
-    res.update({"shape": "cand", "flush_mode": flush_mode, "M": M, "N": N, "K": K, "hit_frac": hit_frac,
+    res.update({"shape": "cand", "M": M, "N": N, "K": K, "hit_frac": hit_frac,
                 "hits_per_tile": round(float(cnt.sum()) / tiles, 1), "us": round(ev[0].elapsed_time(ev[1]) * 100.0, 1)})
     return res
 
@@ -148,13 +149,11 @@ def main():
     ap.add_argument("--cand", type=float, nargs="*", default=[],
                     help="hit fractions for the candidate-GEMM stamps (0.0016 = the 1/64 sample's bound)")
     ap.add_argument("--cand-m", type=int, default=512)
-    ap.add_argument("--flush-mode", type=int, nargs="+", default=[1])
     ap.add_argument("--cand-n", type=int, default=1 << 20)
     args = ap.parse_args()
     torch.manual_seed(0)
     for frac in args.cand:
-        for fm in args.flush_mode:
-            print(json.dumps(run_cand(args.cand_m, args.cand_n, 768, frac, args.reps, fm)), flush=True)
+        print(json.dumps(run_cand(args.cand_m, args.cand_n, 768, frac, args.reps)), flush=True)
         torch.cuda.empty_cache()
     for name in (args.shapes.split(",") if args.shapes else []):
         for aux in args.aux:

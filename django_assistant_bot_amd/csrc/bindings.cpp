@@ -150,7 +150,6 @@ PYBIND11_MODULE(_native, m) {
      py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
-  m.def("gemm256_set_flush_mode", &dab::gemm256_set_flush_mode);
   m.def("gemm256_stamped", [](u A, long lda, u B, u C, u bias, u residual, int M, int N, int K, int epilogue,
                               int b_shuf, u stamps, int stamp_tiles, u s, int store_aux) {
     const int r = dab::gemm256_stamped(CVP(A), lda, CVP(B), VP(C), CVP(bias), CVP(residual), M, N, K, epilogue, b_shuf,
@@ -161,10 +160,9 @@ PYBIND11_MODULE(_native, m) {
      py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("b_shuf"), py::arg("stamps"), py::arg("stamp_tiles"),
      py::arg("s"), py::arg("store_aux") = 0);
   m.def("gemm256_candidates_stamped", [](u A, long lda, u B, int M, int N, int K, int b_rows, u thr, u cnt, u cand_val,
-                                          u cand_idx, int cap, u stamps, int stamp_tiles, u s, int flush_mode) {
+                                          u cand_idx, int cap, u stamps, int stamp_tiles, u s) {
     const int r = dab::gemm256_candidates_stamped(CVP(A), lda, CVP(B), M, N, K, b_rows, (const float*)thr, (int*)cnt,
-                                                  (float*)cand_val, (int*)cand_idx, cap, VP(stamps), stamp_tiles, ST(s),
-                                                  flush_mode);
+                                                  (float*)cand_val, (int*)cand_idx, cap, VP(stamps), stamp_tiles, ST(s));
     if (r < 0) check(-r, "gemm256_candidates_stamped");
     return r;
   });

@@ -66,7 +66,6 @@ struct G256 {
   // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
   u32x4* stamps;
   int stamp_tiles;
-  int flush_mode;  // A/B (pending measurement): 0 = one global round trip per 64 entries, 1 = pipelined
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -185,39 +184,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   };
   auto cand_flush = [&]() {  // wave-uniform call (rare: the list's high-water mark, and the kernel end)
     const int c = min(cand_count(), kCandW);
-    if (p.flush_mode == 0) {
-      for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
-    } else {
-      // every entry's group loads, then every slot claim, then the stores: one round trip of each
-      // kind per flush instead of one per 64 entries
-      constexpr int R = (kCandW + 63) / 64;
-      int fm[R], fn[R], fs[R], rg[R], qg[R];
-      float fv[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int e = lane + 64 * r;
-        const bool ok = e < c;
-        fm[r] = ok ? c_m[e] : 0;
-        fn[r] = ok ? c_n[e] : 0;
-        fv[r] = ok ? c_v[e] : 0.f;
-        fs[r] = p.cap;
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const bool ok = lane + 64 * r < c;
-        rg[r] = !ok ? -1 : p.row_group ? p.row_group[fn[r]] : 0;
-        qg[r] = ok && p.q_group ? p.q_group[fm[r]] : -1;
-      }
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (rg[r] >= 0 && (qg[r] < 0 || rg[r] == qg[r])) fs[r] = atomicAdd(p.cnt + fm[r], 1);
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-        if (fs[r] < p.cap) {
-          p.cand_val[(size_t)fm[r] * p.cap + fs[r]] = fv[r];
-          p.cand_idx[(size_t)fm[r] * p.cap + fs[r]] = fn[r];
-        }
-    }
+    for (int e = lane; e < c; e += 64) cand_global(c_m[e], c_n[e], c_v[e]);
     if (lane == 0) asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(a_cnt), "v"(0) : "memory");
     // retire the flush's memory ops here (the paths the compiler merges after it inherit nothing to
     // wait for); a flush is rare and drains the prefetch queue anyway
@@ -448,6 +415,13 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       // every tile).  Larger M: per-tile threshold / group loads, waited here.
       if (p.M <= kCandMaxM) {
         const float* thr_s = reinterpret_cast<const float*>(smem + 2 * kBuf);
+        // Pass 1, branch-free: bit b = 64 ih + 16 i + 8 jh + 4 jn + r of hb[b / 32] marks a score >= the
+        // query's threshold.  Pass 2, a runtime loop over the wave's hits (as many trips as the
+        // busiest lane has hits, ~1-2): the lowest set bit is decoded, its score picked out of the
+        // accumulators by a select tree, and appended.  One copy of the append code instead of 128
+        // inlined ones: the unrolled form was ~60 KB of epilogue code whose fetch evicted the K-loop
+        // from the instruction cache (the next tile's K-loop ran ~8k cycles slower, with no hits).
+        unsigned hb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih)
 #pragma unroll
@@ -460,10 +434,46 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
               for (int jn = 0; jn < 2; ++jn)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                  const int n = n0 + 128 * jh + 32 * e_wc + 16 * jn + 4 * e_g + r;
-                  if (acc[ih][jh][i][jn][r] >= t && n < p.N) cand_push(m, n, acc[ih][jh][i][jn][r]);
+                  const int b = 64 * ih + 16 * i + 8 * jh + 4 * jn + r;
+                  hb[b >> 5] |= acc[ih][jh][i][jn][r] >= t ? 1u << (b & 31) : 0u;
                 }
           }
+        for (;;) {
+          const bool has = (hb[0] | hb[1] | hb[2] | hb[3]) != 0u;
+          if (__builtin_amdgcn_ballot_w64(has) == 0) break;  // wave-uniform
+          if (has) {
+            const int wd = hb[0] ? 0 : hb[1] ? 1 : hb[2] ? 2 : 3;
+            const unsigned wb = wd == 0 ? hb[0] : wd == 1 ? hb[1] : wd == 2 ? hb[2] : hb[3];
+            const int b = 32 * wd + __builtin_ctz(wb);
+            const unsigned clr = wb & (wb - 1u);
+            hb[0] = wd == 0 ? clr : hb[0];
+            hb[1] = wd == 1 ? clr : hb[1];
+            hb[2] = wd == 2 ? clr : hb[2];
+            hb[3] = wd == 3 ? clr : hb[3];
+            // score: for each of the 16 (jh, jn, r) positions pick the (ih, i) row by bits 4-6, then
+            // the position by bits 0-3
+            float col[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+              const int jh = q >> 3, jn = (q >> 2) & 1, r = q & 3;
+              float x[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) x[u] = acc[u >> 2][jh][u & 3][jn][r];
+#pragma unroll
+              for (int L = 0; L < 3; ++L)
+#pragma unroll
+                for (int u = 0; u < (4 >> L); ++u) x[u] = (b >> (4 + L)) & 1 ? x[2 * u + 1] : x[2 * u];
+              col[q] = x[0];
+            }
+#pragma unroll
+            for (int L = 0; L < 4; ++L)
+#pragma unroll
+              for (int u = 0; u < (8 >> L); ++u) col[u] = (b >> L) & 1 ? col[2 * u + 1] : col[2 * u];
+            const int m = m0 + 128 * (b >> 6) + 64 * wr + 16 * ((b >> 4) & 3) + e_li;
+            const int n = n0 + 128 * ((b >> 3) & 1) + 32 * e_wc + 16 * ((b >> 2) & 1) + 4 * e_g + (b & 3);
+            if (n < p.N) cand_push(m, n, col[0]);
+          }
+        }
         // (a per-step capacity check inside this fully unrolled loop made hipcc keep the loop and
         // move the accumulators to scratch: the list is checked once per tile, and a step that
         // finds it full appends directly)
@@ -685,9 +695,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 // Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
 // index rows B [N, K], any N; K % 128 == 0.
 // b_rows > 0: B is a shuffle_weights copy of b_rows >= N rows (b_rows % 16 == 0, ldb == K).
-static int g_cand_flush = 1;
-void gemm256_set_flush_mode(int m) { g_cand_flush = m; }
-
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                        const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                        hipStream_t s, int b_rows) {
@@ -712,7 +719,6 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   p.cand_idx = cand_idx;
   p.cap = cap;
   p.rows_b = b_rows;
-  p.flush_mode = g_cand_flush;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
@@ -726,7 +732,7 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 // (layout as gemm256_stamped).  No group filters.  Returns the grid.
 int gemm256_candidates_stamped(const void* A, long lda, const void* B, int M, int N, int K, int b_rows,
                                const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap, void* stamps,
-                               int stamp_tiles, hipStream_t s, int flush_mode) {
+                               int stamp_tiles, hipStream_t s) {
   if (M <= 0 || N <= 0 || M > kCandMaxM || K % 128 || lda % 8 || cap <= 0 || b_rows < N || b_rows % 16)
     return -hipErrorInvalidValue;
   G256 p{};
@@ -746,7 +752,6 @@ int gemm256_candidates_stamped(const void* A, long lda, const void* B, int M, in
   p.rows_b = b_rows;
   p.stamps = (u32x4*)stamps;
   p.stamp_tiles = stamp_tiles;
-  p.flush_mode = flush_mode;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);
