@@ -291,7 +291,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   stage(1, 2, 1, rA, rB);
   wait_vm<8>();
   bar();
-  if (wr == 1) bar();  // stagger group 1 by one barrier (ping-pong with group 0)
 
   // One iteration = 8 phases = K-tiles e = 2it (buffer 0) and o = 2it + 1 (buffer 1).
   // phase : quadrant reads  stage (buffer, slot, K-tile)  wait (for the next phase's reads)
@@ -313,6 +312,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   unsigned long long st_t0 = 0, st_t1 = 0;
   for (;;) {
     if constexpr (STAMP) st_t0 = __builtin_amdgcn_s_memtime();
+    // group 1 runs one barrier behind group 0 through the K-loop (ping-pong: one group's MFMAs beside
+    // the other's LDS reads and DMA issue); the pairing is re-made for every tile and undone before
+    // the epilogue (below), so the two groups' epilogues run side by side.  Kept across the tile
+    // boundary instead, each group's epilogue paired with one MFMA phase of the other and the
+    // epilogues ran one after the other.
+    if (wr == 1) bar();
     const int nsid = sid + nper;
     const bool more = nsid < cend;
     int nm0 = m0, nn0 = n0;
@@ -396,6 +401,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     }
 
     if constexpr (STAMP) st_t1 = __builtin_amdgcn_s_memtime();
+    if (wr == 0) bar();  // pairs with group 1's last K-loop barrier
     // ---- epilogue: acc[ih][jh][i][jn][r] = C[m0 + 128 ih + 64 wr + 16 i + li][n0 + 128 jh + 32 wc + 16 jn + 4 g + r]
     // The next tile's first K-tiles are already in flight; the stores overlap them.  Exactly
     // kEpiStores buffer stores per wave, unconditional (rows >= M fall outside the descriptor and
@@ -683,7 +689,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     rB = nB;
     zero_acc();
   }
-  if (wr == 0) bar();  // balance the stagger barrier
   if constexpr (EPI == G_CAND) {
     if (p.M <= kCandMaxM) cand_flush();
   }
