@@ -271,42 +271,48 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     bfr[JH][j][0] = *reinterpret_cast<const bf16x8*>(base + rdB0);                               \
     bfr[JH][j][1] = *reinterpret_cast<const bf16x8*>(base + rdB1);                               \
   }
-#define G256_MFMA(IH, JH)                                                                        \
+#define G256_MFMA2(IH, JH1, JH2)                                                                 \
   __builtin_amdgcn_s_setprio(1);                                                                 \
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                               \
   _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
   _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
-    acc[IH][JH][i][j] = mfma16(bfr[JH][j][ks], af[i][ks], acc[IH][JH][i][j]);                    \
+    acc[IH][JH1][i][j] = mfma16(bfr[JH1][j][ks], af[i][ks], acc[IH][JH1][i][j]);                 \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                               \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                  \
+  _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                  \
+    acc[IH][JH2][i][j] = mfma16(bfr[JH2][j][ks], af[i][ks], acc[IH][JH2][i][j]);                 \
   __builtin_amdgcn_s_setprio(0);
 
   const int T = p.K >> 6;  // K-tiles (even, >= 2)
   const int iters = T >> 1;
 
-  // prologue (first tile only): K-tile 0 complete, K-tile 1's A0 / B0 in flight
+  // prologue (first tile only): K-tile 0 complete, K-tile 1's A0 / B0 / B1 in flight
   stage(0, 0, 0, rA, rB);
   stage(0, 2, 0, rA, rB);
   stage(0, 3, 0, rA, rB);
   stage(0, 1, 0, rA, rB);
   stage(1, 0, 1, rA, rB);
   stage(1, 2, 1, rA, rB);
+  stage(1, 3, 1, rA, rB);
   wait_vm<8>();
   bar();
 
-  // One iteration = 8 phases = K-tiles e = 2it (buffer 0) and o = 2it + 1 (buffer 1).
-  // phase : quadrant reads  stage (buffer, slot, K-tile)  wait (for the next phase's reads)
-  //   1   : (0,0) A0 B0     (1, B1, o)                   vmcnt(8)  -> B1 e
-  //   2   : (0,1) B1        (1, A1, o)                   vmcnt(8)  -> A1 e
-  //   3   : (1,1) A1        (0, A0, e+2)                 -
-  //   4   : (1,0) -         (0, B0, e+2)                 vmcnt(8)  -> A0 B0 o
-  //   5   : (0,0) A0 B0     (0, B1, e+2)                 vmcnt(8)  -> B1 o
-  //   6   : (0,1) B1        (0, A1, e+2)                 vmcnt(8)  -> A1 o
-  //   7   : (1,1) A1        (1, A0, o+2)                 -
-  //   8   : (1,0) -         (1, B0, o+2)                 vmcnt(8)  -> A0 B0 e+2
-  // Every piece is restaged >= 2 phases after its last read.  In the last iteration of a tile the
-  // phase 3-8 pieces are the NEXT tile's K-tiles 0 / 1 (same buffers as e+2 / o+2), so the next
-  // tile starts without a prologue; after the last tile nothing is staged and the phase-4 wait
-  // drains everything (one vmcnt(0) per workgroup).  One copy of the body: the variants differ
-  // only in uniform (SGPR) values, which keeps hipcc's register allocation of the loop intact.
+  // One iteration = 4 phases = K-tiles e = 2it (buffer 0) and o = 2it + 1 (buffer 1); a phase is
+  // [LDS reads, DMA issue, counted wait] barrier [32 MFMAs: two quadrants] barrier, and the two wave
+  // groups run one barrier apart (one group's MFMAs beside the other's reads).
+  // phase : reads (quadrants)        stage (buffer, slots, K-tile)   wait (for the next phase's reads)
+  //   1   : A0 B0 B1 e ((0,0) (0,1))  (1, A1, o)                     vmcnt(8) -> A1 e
+  //   2   : A1 e       ((1,1) (1,0))  (0, A0 B0 B1, e+2)             vmcnt(8) -> A0 B0 B1 o
+  //   3   : A0 B0 B1 o ((0,0) (0,1))  (0, A1, e+2)                   vmcnt(8) -> A1 o
+  //   4   : A1 o       ((1,1) (1,0))  (1, A0 B0 B1, o+2)             vmcnt(8) -> A0 B0 B1 e+2
+  // Every piece is restaged one phase after its last read (a phase is 2 x 32 MFMAs, ~1k cycles:
+  // the reads of the other group's previous phase have long returned when the DMA lands) and read
+  // three phases later.  In the last iteration of a tile the phase 2-4 pieces are the NEXT tile's
+  // K-tiles 0 / 1 (same buffers as e+2 / o+2), so the next tile starts without a prologue; after
+  // the last tile nothing is staged and the phase-2 wait drains everything.  Half the barriers of
+  // the 8-phase form (one quadrant per phase), same registers (the B fragments of both halves
+  // stay live across a phase pair as before).  One copy of the body: the variants differ only in
+  // uniform (SGPR) values, which keeps hipcc's register allocation of the loop intact.
   bool after_epi = false;
   int tile_no = 0;
   unsigned long long st_t0 = 0, st_t1 = 0;
@@ -334,69 +340,48 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       // phase 1
       G256_READ_A(0, 0)
       G256_READ_B(0, 0)
-      stage(1, 3, o, rA, rB);
-      if (fe) wait_vm<8 + kEpi>();
-      else wait_vm<8>();
-      bar();
-      G256_MFMA(0, 0)
-      bar();
-      // phase 2
       G256_READ_B(0, 1)
       stage(1, 1, o, rA, rB);
       if (fe) wait_vm<8 + kEpi>();
       else wait_vm<8>();
       bar();
-      G256_MFMA(0, 1)
+      G256_MFMA2(0, 0, 1)
       bar();
-      // phase 3
+      // phase 2
       G256_READ_A(0, 1)
-      if (st) stage(0, 0, ke, sa, sb);
-      bar();
-      G256_MFMA(1, 1)
-      bar();
-      // phase 4
       if (st) {
+        stage(0, 0, ke, sa, sb);
         stage(0, 2, ke, sa, sb);
+        stage(0, 3, ke, sa, sb);
         if (fe) wait_vm<8 + kEpi>();
         else wait_vm<8>();
       } else {
         wait_vm<0>();
       }
       bar();
-      G256_MFMA(1, 0)
+      G256_MFMA2(1, 1, 0)
       bar();
-      // phase 5
+      // phase 3
       G256_READ_A(1, 0)
       G256_READ_B(1, 0)
-      if (st) {
-        stage(0, 3, ke, sa, sb);
-        wait_vm<8>();
-      }
-      bar();
-      G256_MFMA(0, 0)
-      bar();
-      // phase 6
       G256_READ_B(1, 1)
       if (st) {
         stage(0, 1, ke, sa, sb);
         wait_vm<8>();
       }
       bar();
-      G256_MFMA(0, 1)
+      G256_MFMA2(0, 0, 1)
       bar();
-      // phase 7
+      // phase 4
       G256_READ_A(1, 1)
-      if (st) stage(1, 0, ko, sa, sb);
-      bar();
-      G256_MFMA(1, 1)
-      bar();
-      // phase 8
       if (st) {
+        stage(1, 0, ko, sa, sb);
         stage(1, 2, ko, sa, sb);
+        stage(1, 3, ko, sa, sb);
         wait_vm<8>();
       }
       bar();
-      G256_MFMA(1, 0)
+      G256_MFMA2(1, 1, 0)
       bar();
     }
 
@@ -694,7 +679,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   }
 #undef G256_READ_A
 #undef G256_READ_B
-#undef G256_MFMA
+#undef G256_MFMA2
 }
 
 // Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
