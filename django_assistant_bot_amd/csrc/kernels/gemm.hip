@@ -327,7 +327,7 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   if (K % 64 || N % 4 || lda % 8 || ldb % 8 || cap <= 0 || !thr || !cnt || !cand_val || !cand_idx)
     return hipErrorInvalidValue;
   if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
-  // query batches that fill 256-row tiles: the persistent 8-phase kernel (a 10M-row scan at K 768 is
+  // query batches that fill 256-row tiles: the persistent gemm256 kernel (a 10M-row scan at K 768 is
   // 39k short-K tiles per 256 queries; the one-tile-per-workgroup kernel below pays its prologue and
   // epilogue on every one of them)
   if (M >= 128 && K % 128 == 0)

@@ -3,22 +3,27 @@
 // bge qkv / o / up / down at M = 64k).  Replaces HF Linear in the reference
 // (ai/providers/transformers.py:57-66 generate, ai/embedders/transformers.py:18-22 encoder forward).
 //
-// Structure: the 256x256 "8-phase" schedule of cdna_hip_programming.md section 5 (T1-T5):
+// Structure: the 256x256 phased schedule of cdna_hip_programming.md section 5 (T1-T5), with two
+// quadrants per phase:
 //   * 512 threads = 8 waves; per K-tile (BK = 64) the block tile is cut into 2x2 quadrants of
-//     128x128 and every wave owns a 64x32 piece of EACH quadrant (waves 2 (M) x 4 (N) per quadrant),
-//     so one phase = one quadrant = 16 x v_mfma_f32_16x16x32_bf16 per wave, 4 phases per K-tile;
+//     128x128 and every wave owns a 64x32 piece of EACH quadrant (waves 2 (M) x 4 (N) per quadrant);
+//     one phase = two quadrants = 32 x v_mfma_f32_16x16x32_bf16 per wave, 2 phases per K-tile (the
+//     8-phase form's one quadrant per phase spent ~350 of every 2,400 cycles per K-tile at its
+//     16 barriers; with 8 barriers per 2 K-tiles a K-tile takes ~2,200 cycles, but the chip then
+//     holds a lower clock: profiles/gemm_tile_stamps.md);
 //   * the A/B tiles are staged by LDS-DMA (buffer_load ... lds, 16 B per lane) in HALF-TILE pieces
-//     (128 rows x 64 k = 16 KB, two instructions per wave), one piece per phase, so the load stream
-//     is spread evenly under the MFMAs; 2 K-tile buffers = 128 KB of LDS (1 block per CU);
+//     (128 rows x 64 k = 16 KB, two instructions per wave), 1 or 3 pieces per phase;
+//     2 K-tile buffers = 128 KB of LDS (1 block per CU);
 //   * counted waits only: every phase waits `vmcnt(8)` (4 pieces stay in flight ACROSS barriers,
-//     each piece has 4 phases ~ 2k cycles to land), raw s_barrier (never __syncthreads, whose
+//     each piece has 3 phases ~ 3k cycles to land), raw s_barrier (never __syncthreads, whose
 //     fence would drain the DMA), all LDS in ONE __shared__ array;
 //   * the two wave groups (wr = 0 / 1, one wave of each per SIMD) are staggered by one barrier so one
-//     group's MFMA cluster overlaps the other group's LDS reads + DMA issue (ping-pong);
+//     group's MFMA cluster overlaps the other group's LDS reads + DMA issue (ping-pong), re-made on
+//     every tile so the two groups' epilogues overlap;
 //     s_setprio(1) around each MFMA cluster keeps hipcc from moving MFMAs across the barriers (T5);
 //   * fragment registers: the A rows of the current quadrant row (32 VGPR) and BOTH B halves
-//     (2 x 16 VGPR), so a K-tile reads A0+B0 / B1 / A1 / - in its 4 phases (24 ds_read_b128, the
-//     minimum), and every staged piece is rewritten >= 2 phases after its last read (WAR rule with
+//     (2 x 16 VGPR), so a K-tile reads A0+B0+B1 / A1 in its 2 phases (24 ds_read_b128, the
+//     minimum), and every staged piece is rewritten one phase after its last read (WAR rule with
 //     staggered groups) and waited >= 1 phase before its first read (RAW rule);
 //   * LDS rows are 128 B; the 16-B chunk c of row r lives at chunk c ^ ((r >> 1) & 7): conflict-free
 //     for the 4 x 16-lane groups of ds_read_b128 (MI355X_MICROARCH.md section LDS).  LDS-DMA writes
@@ -331,7 +336,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     const __amdgpu_buffer_rsrc_t nA = rsrc_a(nm0), nB = rsrc_b(nn0);
     for (int it = 0; it < iters; ++it) {
       const bool last = it == iters - 1;
-      const bool st = !last || more;  // stage phases 3-8
+      const bool st = !last || more;  // stage phases 2-4
       // first iteration after an epilogue: kEpi younger stores sit in the VM queue
       const bool fe = after_epi && it == 0;
       const int e = 2 * it, o = e + 1;

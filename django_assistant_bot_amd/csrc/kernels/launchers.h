@@ -53,7 +53,7 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
             const uint32_t* allow, int allow_words, hipStream_t s, int b_rows = 0);
 
-// gemm256.hip (large-M prefill / encoder GEMM, 256x256 8-phase schedule; epilogue 0 none, 1 GELU,
+// gemm256.hip (large-M prefill / encoder GEMM, 256x256 phased schedule; epilogue 0 none, 1 GELU,
 // 2 SwiGLU on [gate 16 | up 16]-interleaved weight rows; bias / residual optional)
 int gemm256_ok(int M, int N, int K, long lda, long ldb);
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
