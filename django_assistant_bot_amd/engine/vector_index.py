@@ -14,7 +14,7 @@ compaction), growth, and safetensors snapshots for warm starts.
 
 On the GPU (bf16, dim % 128 == 0) the rows are held ONCE, in the ``ops.shuffle_weights`` fragment
 layout: every 16-row x 32-k block is one coalesced 1 KB load for the 1..128-query scans
-(index_scan.hip / the streaming GEMM's candidate epilogue) and one LDS-DMA piece for the 8-phase
+(index_scan.hip / the streaming GEMM's candidate epilogue) and one LDS-DMA piece for the phased
 GEMM at >= 128 queries and the generic-filter score GEMM.  (Round 2 kept a row-major copy beside
 it: 2x the index HBM.)  Only the 1/64 row sample of the threshold search is gathered row-major, and
 cached until the next update.

@@ -90,7 +90,7 @@ class LlamaModel:
         # disabled the streaming decode for 70B at TP 1).  The LM head too; a tied embedding table
         # keeps its row-major copy for the gather.
         # (``fragment_layout=False``: row-major weights on the GPU too, every projection on the
-        # 128x128 / 8-phase GEMMs -- the comparison path of tests/test_models_gpu.py)
+        # 128x128 / phased 256x256 GEMMs -- the comparison path of tests/test_models_gpu.py)
         self.frag = fragment_layout and self.device.type == "cuda" and self._fragment_ok(weights)
         take = weights.pop if consume else weights.__getitem__
 

@@ -328,11 +328,11 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
 # GEMM
 
 
-GEMM256_MIN_M = 1024  # the 8-phase 256x256 kernel from here on; the 128x128 kernel below
+GEMM256_MIN_M = 1024  # the phased 256x256 kernel from here on; the 128x128 kernel below
 
 
 def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    """Large-M shapes go to the 256x256 8-phase kernel (gemm256.hip)."""
+    """Large-M shapes go to the phased 256x256 kernel (gemm256.hip)."""
     return M >= GEMM256_MIN_M and bool(native().gemm256_ok(M, N, K, lda, ldb))
 
 
@@ -407,7 +407,7 @@ def _gemm256_into(A, B, out, bias, residual, epilogue, shuffled):
 
 
 def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
-    """The 8-phase 256x256 kernel directly, for any M (``gemm_bt`` takes it from M >= 1024):
+    """The phased 256x256 kernel directly, for any M (``gemm_bt`` takes it from M >= 1024):
     tests and benchmarks.  N % 256 == 0, K % 128 == 0."""
     M, K = A.shape
     N = B.shape[0]
@@ -447,9 +447,9 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
 def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=None):
     """``score_candidates`` over a copy of the rows in the ``shuffle_weights`` layout (``B_shuf``
     [R, K], R >= round_up(N, 128), R % 16 == 0): every 16-row x 32-k fragment is one coalesced 1 KB
-    load (1..16 queries: the persistent scan of index_scan.hip; 17..128: the weight-streaming
-    kernel's candidate epilogue; more: the 8-phase GEMM's candidate epilogue, 128x128 kernel when
-    K % 128)."""
+    load (1..96 queries at K <= 768, 1..64 at K <= 1024: the persistent scan of index_scan.hip;
+    up to 127: the weight-streaming kernel's candidate epilogue; more: gemm256's candidate epilogue,
+    the 128x128 kernel when K % 128)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
     M, K = A.shape
     expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "queries need K % 128 == 0")
@@ -690,7 +690,7 @@ def topk_rows(scores, k, index_base=0, want_global=False):
 
 
 def linear(x, w, b=None, residual=None, act=None):
-    """y = x W^T (+b) (+act) (+residual) on the native MFMA GEMMs (``gemm_bt``: the 256x256 8-phase
+    """y = x W^T (+b) (+act) (+residual) on the native MFMA GEMMs (``gemm_bt``: the phased 256x256
     kernel for large token counts, the 128x128 kernel otherwise), epilogues fused.  Shapes the
     kernels cannot take (K % 64, N % 4) fall back to torch with a one-time warning."""
     epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]

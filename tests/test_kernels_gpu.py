@@ -290,7 +290,7 @@ def test_gemm_big_tiles(M, N, K):
                                    (1100, 512, 4096), (600, 256, 14336), (2000, 768, 3072)])
 @pytest.mark.parametrize("shuffled", [False, True])
 def test_gemm256(M, N, K, shuffled):
-    """8-phase 256x256 kernel (gemm256.hip) for every eligible shape: ragged M, every epilogue, grids
+    """Phased 256x256 kernel (gemm256.hip) for every eligible shape: ragged M, every epilogue, grids
     of more tiles than CUs (persistent workgroups, next-tile prefetch, counted waits past the
     epilogue stores); B row-major or in the fragment layout the model keeps (one weight copy)."""
     assert ops.native().gemm256_ok(M, N, K, K, K)
@@ -337,6 +337,41 @@ def test_gemm256_stamped_matches_and_stamps(aux):
     s = st[:grid].cpu()
     ran = s[:, :, 0] != 0
     assert int(ran.sum()) == tiles and bool((s[:, :, 2][ran] > 0).all()) and bool((s[:, :, 3][ran] > 0).all())
+
+
+def test_gemm256_candidates_stamped_matches_production():
+    """The stamped candidate-GEMM launcher (benchmarks/gemm_stamps.py --cand) appends the same
+    candidate set as the production search path over the same shuffled copy, and stamps every tile."""
+    from django_assistant_bot_amd.ops.kernels import native, ptr, stream
+
+    M, N, K = 300, 20_000, 768
+    A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
+    B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
+    full = ops.gemm_bt(A, B, epilogue=ops.EPI_SCORES, out_f32=True)
+    thr = torch.quantile(full, 0.99, dim=1).contiguous()
+    Bp = torch.zeros((-(-N // 128) * 128, K), dtype=torch.bfloat16, device=DEV)
+    Bp[:N] = B
+    Ws = ops.shuffle_weights(Bp)
+    cap = 2048
+    cv0, ci0, cnt0 = ops.score_candidates_shuffled(A, Ws, N, thr, cap, None, None)
+    cnt = torch.zeros(M, dtype=torch.int32, device=DEV)
+    cv = torch.empty(M * cap, dtype=torch.float32, device=DEV)
+    ci = torch.empty(M * cap, dtype=torch.int32, device=DEV)
+    tiles = (M + 255) // 256 * ((N + 255) // 256)
+    per_wg = -(-tiles // 256) + 1
+    st = torch.zeros((256, per_wg, 4), dtype=torch.int32, device=DEV)
+    grid = native().gemm256_candidates_stamped(ptr(A), K, ptr(Ws), M, N, K, Ws.shape[0], ptr(thr), ptr(cnt), ptr(cv),
+                                               ptr(ci), cap, ptr(st), per_wg, stream(A))
+    torch.cuda.synchronize()
+    assert torch.equal(cnt, cnt0) and int(cnt.max()) <= cap
+    ci, cv = ci.view(M, cap), cv.view(M, cap)
+    for m in range(0, M, 13):
+        k = int(cnt[m])
+        assert set(ci[m, :k].tolist()) == set(ci0[m, :k].tolist())
+        torch.testing.assert_close(cv[m, :k].sort().values, cv0[m, :k].sort().values, atol=0, rtol=0)
+    s = st[:grid].cpu()
+    ran = s[:, :, 0] != 0
+    assert int(ran.sum()) == tiles and bool((s[:, :, 2][ran] > 0).all())
 
 
 @pytest.mark.parametrize("shuffled", [False, True])
