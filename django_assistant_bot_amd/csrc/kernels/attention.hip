@@ -75,14 +75,10 @@ struct FlashParams {
 // most tiles; decided before the tile's P is exponentiated (nothing is scaled twice).
 constexpr float kDeferLog2 = 8.f;
 
-template <int D, bool CAUSAL, bool PAGED, int NW, int QT, bool ONE = false>
+template <int D, bool CAUSAL, bool PAGED, int NW, int QT>
 // (QT = 2 with 4 waves is held to 256 registers -- 2 waves per SIMD, no spills -- by the
 // launch bound; unbounded it took 294 and ran at 1 wave per SIMD.)
-// ONE: every sequence fits one 64-key tile (encoder chunks of <= 64 tokens): no next-tile prefetch
-// registers, so the bound holds the kernel to 64 VGPRs and 8 workgroups per CU (the 4-wave form took
-// 112 registers and 4 per CU, and a workgroup's life at these lengths is one load latency, so the
-// number resident sets the rate).
-__global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : ONE ? 8 : 1) void flash_fwd_kernel(FlashParams p) {
+__global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_fwd_kernel(FlashParams p) {
   constexpr int KT = 64;
   constexpr int NT = 64 * NW;
   constexpr int QB = 16 * QT * NW;
@@ -145,7 +141,7 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : ONE ? 8 : 1) vo
     const int last_q = min(q0 + QB - 1, seqlen_q - 1);
     n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
   }
-  const int n_tiles = ONE ? min(div_up(n_keys, KT), 1) : div_up(n_keys, KT);
+  const int n_tiles = div_up(n_keys, KT);
 
   u32x4 kreg[CH], vreg[CH];
   // Branch-free staging: rows past the end are clamped to the last valid key (finite data, masked
@@ -198,7 +194,7 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : ONE ? 8 : 1) vo
   }
   for (int kt = 0; kt < n_tiles; ++kt) {
     __syncthreads();
-    if (!ONE && kt + 1 < n_tiles) load_tile(kt + 1);
+    if (kt + 1 < n_tiles) load_tile(kt + 1);
     // S^T = K Q^T: each K fragment feeds QT MFMAs
     f32x4 s[QT][4];
 #pragma unroll
@@ -277,7 +273,6 @@ __global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : ONE ? 8 : 1) vo
         for (int qt = 0; qt < QT; ++qt) o[qt][t] = mfma16(a, pb[qt][ss], o[qt][t]);
       }
     }
-    if (ONE) break;
     __syncthreads();
     if (kt + 1 < n_tiles) store_tile();
   }
@@ -1026,16 +1021,12 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // waves (8 waves measured 5 % slower there; a 4-wave x 2-sub-tile form was no faster either)
   const bool wide = D == 128 && max_seqlen_q > 64;
   const int qb = wide ? 128 : 64;
-  // encoder batches of short chunks (no cache, keys = queries, all <= 64): the single-tile form
-  const bool one = !wide && !paged && !causal && D <= 64 && max_seqlen_q <= 64 && cu_k == cu_q;
   dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
 #define DAB_FLASH(DD, C, P)                                                                          \
   do {                                                                                              \
     if (wide)                                                                                       \
       hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD == 128 ? 8 : 4), 1>), grid,              \
                          dim3(DD == 128 ? 512 : 256), 0, s, prm);                                   \
-    else if (one)                                                                                   \
-      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1, true>), grid, dim3(256), 0, s, prm);     \
     else                                                                                            \
       hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1>), grid, dim3(256), 0, s, prm);           \
   } while (0)
