@@ -149,8 +149,10 @@ def test_rope_kv_write():
 
 @pytest.mark.parametrize("D", [32, 64, 128])
 @pytest.mark.parametrize("causal", [False, True])
-def test_flash_packed(D, causal):
-    lens = [5, 70, 130, 1]
+@pytest.mark.parametrize("lens", [[5, 70, 130, 1], [5, 64, 33, 1, 50, 17, 64, 2]])
+def test_flash_packed(D, causal, lens):
+    """Packed varlen attention against the fp32 reference (long and short, encoder-chunk-like
+    batches)."""
     Hq, Hkv = (8, 2) if causal else (4, 4)
     T = sum(lens)
     cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
