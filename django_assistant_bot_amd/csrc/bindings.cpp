@@ -195,9 +195,10 @@ PYBIND11_MODULE(_native, m) {
     int rc = hipErrorInvalidValue;
     if (K % 256 == 0 && ((M <= 64 && K <= 1024) || (M <= 96 && K <= 768)))
       rc = dab::index_scan_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
-    else if (M < 128)  // 128+ queries fill the persistent 256x256 kernel's tiles (gemm256 G_CAND)
+    else if (M <= 64 || K % 128)
       rc = dab::stream_score_candidates_shuf(CVP(A), lda, CVP(Wshuf), M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s));
-    else
+    else  // 65+ queries past the scan's limits: the persistent 256x256 kernel (gemm256 G_CAND); at
+          // 97-127 queries of 768 the streaming kernel took 5.6-6.0 ms on 10M rows, gemm256 ~3.9
       rc = dab::gemm_score_candidates(CVP(A), lda, CVP(Wshuf), K, M, N, K, rg, qg, th, ct, cv, ci, cap, ST(s), b_rows);
     check(rc, "score_candidates_shuf");
   }, py::arg("A"), py::arg("lda"), py::arg("Wshuf"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("row_group"),

@@ -327,16 +327,17 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   if (K % 64 || N % 4 || lda % 8 || ldb % 8 || cap <= 0 || !thr || !cnt || !cand_val || !cand_idx)
     return hipErrorInvalidValue;
   if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
-  // query batches that fill 256-row tiles: the persistent gemm256 kernel (a 10M-row scan at K 768 is
-  // 39k short-K tiles per 256 queries; the one-tile-per-workgroup kernel below pays its prologue and
-  // epilogue on every one of them)
-  if (M >= 128 && K % 128 == 0)
+  // 65+ query batches past the scan's limits (and every batch of 128+): the persistent gemm256 kernel
+  // (a 10M-row scan at K 768 is 39k short-K tiles per 256 queries; the one-tile-per-workgroup kernel
+  // below pays its prologue and epilogue on every one of them)
+  const bool scan_ok = b_rows == 0 && K % 256 == 0 && ((M <= 64 && K <= 1024) || (M <= 96 && K <= 768));
+  if (K % 128 == 0 && (M >= 128 || (M > 64 && !scan_ok)))
     return gemm256_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s,
                               b_rows);
   // 1..64 queries (K <= 1024) or 65..96 (K <= 768): the persistent scan with the queries in LDS once
   // per workgroup (K % 256 == 0); 32..64 at other widths: the index streams through the decode GEMM's weight ring.
   // Row-major copies only here; shuffled copies go through score_candidates_shuf (VectorIndex picks).
-  if (b_rows == 0 && K % 256 == 0 && ((M <= 64 && K <= 1024) || (M <= 96 && K <= 768)))
+  if (scan_ok)
     return index_scan_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   if (b_rows == 0 && M >= 32 && M <= 64 && K % 128 == 0)
     return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);

@@ -448,8 +448,8 @@ def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=No
     """``score_candidates`` over a copy of the rows in the ``shuffle_weights`` layout (``B_shuf``
     [R, K], R >= round_up(N, 128), R % 16 == 0): every 16-row x 32-k fragment is one coalesced 1 KB
     load (1..96 queries at K <= 768, 1..64 at K <= 1024: the persistent scan of index_scan.hip;
-    up to 127: the weight-streaming kernel's candidate epilogue; more: gemm256's candidate epilogue,
-    the 128x128 kernel when K % 128)."""
+    more (K % 128 == 0): gemm256's candidate epilogue; the weight-streaming kernel's candidate
+    epilogue otherwise)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B_shuf.dtype == torch.bfloat16, "bf16 CUDA operands required")
     M, K = A.shape
     expect(shuffled_scan_ok(M, K) and A.stride(-1) == 1 and A.stride(0) % 8 == 0, "queries need K % 128 == 0")

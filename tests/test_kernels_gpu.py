@@ -635,13 +635,14 @@ def test_score_candidates_gemm256_lds_lists(q):
         torch.testing.assert_close(cv[m, :k], full[m, ci[m, :k].long()], atol=1e-5, rtol=1e-5)
 
 
-@pytest.mark.parametrize("M", [1, 5, 16, 17, 37, 64, 65, 96, 97, 127, 128, 300])
-def test_score_candidates_shuffled_exact_set(M):
-    """The scans over a shuffle_weights copy of the rows (1..96 queries: index_scan.hip SHUF with
-    1-6 16-query tiles in LDS; 97..127: the streaming kernel's cfg 10; 128+: gemm256 G_CAND reading
-    the fragment layout) append exactly the filtered scores >=
-    thr[m] (N not a multiple of 128: the copy is zero-padded)."""
-    N, K = 100_004, 768
+@pytest.mark.parametrize("M,K", [(m, 768) for m in (1, 5, 16, 17, 37, 64, 65, 96, 97, 127, 128, 300)] +
+                         [(20, 896), (40, 1280), (80, 1280)])
+def test_score_candidates_shuffled_exact_set(M, K):
+    """The scans over a shuffle_weights copy of the rows (1..96 queries at K 768: index_scan.hip SHUF
+    with 1-6 16-query tiles in LDS; 97+: gemm256 G_CAND reading the fragment layout; widths the scan
+    does not take: the streaming kernel at <= 64 queries, gemm256 above) append exactly the filtered
+    scores >= thr[m] (N not a multiple of 128: the copy is zero-padded)."""
+    N = 100_004
     A = torch.nn.functional.normalize(torch.randn(M, K, device=DEV), dim=-1).to(torch.bfloat16)
     B = torch.nn.functional.normalize(torch.randn(N, K, device=DEV), dim=-1).to(torch.bfloat16)
     rg = torch.randint(-1, 3, (N,), device=DEV, dtype=torch.int32)
