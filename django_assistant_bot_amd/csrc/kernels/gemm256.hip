@@ -334,6 +334,10 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     int nm0 = m0, nn0 = n0;
     if (more) tile_of(nsid, tiles_m, tiles_n, p.gm, nm0, nn0);
     const __amdgpu_buffer_rsrc_t nA = rsrc_a(nm0), nB = rsrc_b(nn0);
+    // G_CAND: a tile whose rows 128-255 are all past M (97-128 queries, or the last row tile of a
+    // larger batch) skips their MFMAs (the accumulators stay zero; their thresholds are +inf).
+    // Uniform per tile; the LDS reads, barriers and DMA schedule are unchanged.
+    const bool h2 = EPI != G_CAND || m0 + 128 < p.M;
     for (int it = 0; it < iters; ++it) {
       const bool last = it == iters - 1;
       const bool st = !last || more;  // stage phases 2-4
@@ -364,7 +368,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         wait_vm<0>();
       }
       bar();
-      G256_MFMA2(1, 1, 0)
+      if (h2) {
+        G256_MFMA2(1, 1, 0)
+      }
       bar();
       // phase 3
       G256_READ_A(1, 0)
@@ -386,7 +392,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         wait_vm<8>();
       }
       bar();
-      G256_MFMA2(1, 1, 0)
+      if (h2) {
+        G256_MFMA2(1, 1, 0)
+      }
       bar();
     }
 
