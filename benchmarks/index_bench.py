@@ -42,7 +42,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sample-stride", type=int, default=0,
                     help="A/B: the threshold search's row-sample stride (0 = VectorIndex default)")
-    ap.add_argument("--skip-ab", action="store_true")
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", 1)),
                     help="ranks; from a plain process the script starts them itself (parallel/launch.py)")
     args = ap.parse_args()
@@ -87,21 +86,6 @@ def main():
         res = {"queries_per_rank": B, "ms_per_search": round(1000 * per_call, 3),
                "queries_per_s": round(W * B / per_call, 1),
                "scan_TBps": round(args.rows * args.dim * 2 / per_call / 1e12, 2)}
-        if args.skip_ab and dev.type == "cuda":  # A/B (temporary): skip the empty lower half's MFMAs
-            from django_assistant_bot_amd.ops.kernels import native
-            arms = {0: [], 1: []}
-            for _ in range(2):
-                for mode in (0, 1):
-                    native().gemm256_set_skip_half(mode)
-                    index.search(q, args.k)
-                    torch.cuda.synchronize(dev)
-                    t1 = time.perf_counter()
-                    for _ in range(args.iters):
-                        index.search(q, args.k)
-                    torch.cuda.synchronize(dev)
-                    arms[mode].append(1000 * (time.perf_counter() - t1) / args.iters)
-            native().gemm256_set_skip_half(1)
-            res.update({f"skip{m}_ms": round(min(v), 3) for m, v in arms.items()})
         results.append(res)
         assert ids.shape == (B, args.k)
     if R == 0:

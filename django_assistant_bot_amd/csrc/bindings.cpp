@@ -150,7 +150,6 @@ PYBIND11_MODULE(_native, m) {
      py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
-  m.def("gemm256_set_skip_half", &dab::gemm256_set_skip_half);
   m.def("gemm256_stamped", [](u A, long lda, u B, u C, u bias, u residual, int M, int N, int K, int epilogue,
                               int b_shuf, u stamps, int stamp_tiles, u s, int store_aux) {
     const int r = dab::gemm256_stamped(CVP(A), lda, CVP(B), VP(C), CVP(bias), CVP(residual), M, N, K, epilogue, b_shuf,

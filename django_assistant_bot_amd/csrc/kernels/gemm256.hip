@@ -71,7 +71,6 @@ struct G256 {
   // of the epilogue} as one 16-B vector store; stamp_tiles entries per workgroup
   u32x4* stamps;
   int stamp_tiles;
-  int skip_half;  // A/B (pending measurement)
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -338,7 +337,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     // G_CAND: a tile whose rows 128-255 are all past M (97-128 queries, or the last row tile of a
     // larger batch) skips their MFMAs (the accumulators stay zero; their thresholds are +inf).
     // Uniform per tile; the LDS reads, barriers and DMA schedule are unchanged.
-    const bool h2 = EPI != G_CAND || !p.skip_half || m0 + 128 < p.M;
+    const bool h2 = EPI != G_CAND || m0 + 128 < p.M;
     for (int it = 0; it < iters; ++it) {
       const bool last = it == iters - 1;
       const bool st = !last || more;  // stage phases 2-4
@@ -699,9 +698,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
 // Threshold candidates of the index search (see gemm.hip gemm_score_candidates): queries A [M, K] x
 // index rows B [N, K], any N; K % 128 == 0.
 // b_rows > 0: B is a shuffle_weights copy of b_rows >= N rows (b_rows % 16 == 0, ldb == K).
-static int g_skip_half = 1;
-void gemm256_set_skip_half(int on) { g_skip_half = on; }
-
 int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, int N, int K, const int* row_group,
                        const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap,
                        hipStream_t s, int b_rows) {
@@ -726,7 +722,6 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
   p.cand_idx = cand_idx;
   p.cap = cap;
   p.rows_b = b_rows;
-  p.skip_half = g_skip_half;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const long tiles = (long)((M + 255) / 256) * ((N + 255) / 256);

@@ -65,7 +65,6 @@ int gemm256_candidates(const void* A, long lda, const void* B, long ldb, int M, 
 int gemm256_candidates_stamped(const void* A, long lda, const void* B, int M, int N, int K, int b_rows,
                                const float* thr, int* cnt, float* cand_val, int* cand_idx, int cap, void* stamps,
                                int stamp_tiles, hipStream_t s);
-void gemm256_set_skip_half(int on);
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
                     int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux);
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
