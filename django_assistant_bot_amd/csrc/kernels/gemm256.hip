@@ -413,8 +413,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
     if constexpr (EPI == G_CAND) {
       // acc[ih][jh][i][jn][r] = score of query m0 + 128 ih + 64 wr + 16 i + li against index row
       // n0 + 128 jh + 32 wc + 16 jn + 4 g + r.  M <= kCandMaxM: the thresholds sit in LDS and a hit
-      // (rare: ~26 per 256x256 tile at k = 250) goes to this wave's LDS list; the group filters and
-      // the global appends run when the list is flushed.  The epilogue then issues no vector-memory
+      // (rare: ~105 per 256x256 tile at k = 250 under the 1/64 sample's bound) goes to this wave's
+      // LDS list; the group filters and the global appends run when the list is flushed.  The
+      // epilogue then issues no vector-memory
       // op, so the next tile's prefetched K-tiles stay in flight (a vmcnt(0) here drained them on
       // every tile).  Larger M: per-tile threshold / group loads, waited here.
       if (p.M <= kCandMaxM) {
