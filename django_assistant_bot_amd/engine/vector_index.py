@@ -292,11 +292,15 @@ class VectorIndex:
             cand_val, cand_idx, cnt = ops.score_candidates_shuffled(q, self.vecs, n4, thr, cap, self.row_group[:n4], qg)
         else:
             cand_val, cand_idx, cnt = ops.score_candidates(q, self.vecs[:n4], thr, cap, self.row_group[:n4], qg)
-        if int(cnt.max()) > cap:
+        cmax = int(cnt.max())
+        if cmax > cap:
             self.stats["threshold_overflows"] += 1
             return None
         self.stats["threshold_searches"] += 1
-        vals, pos = ops.topk_rows(cand_val, min(k, cap))
+        # only the filled prefix of the lists (the longest one, ~16k of the 64k-entry capacity on
+        # unstructured data) is ranked; shorter lists are -inf past their count
+        n_use = min(cap, max(k, -(-cmax // 64) * 64))
+        vals, pos = ops.topk_rows(cand_val[:, :n_use], min(k, n_use))
         rows = torch.gather(cand_idx, 1, pos.long())
         return vals, rows.masked_fill(torch.isinf(vals), 0)
 
