@@ -421,8 +421,9 @@ def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
 
 def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
     """Filtered cosine scores of A [M, K] against B [N, K] that are >= thr[m], appended per query
-    (no [M, N] score matrix).  -> (cand_val fp32 [M, cap] (-inf padded), cand_idx int32 [M, cap],
-    count int32 [M]; count > cap means the list overflowed)."""
+    (no [M, N] score matrix).  -> (cand_val fp32 [M, cap] (-inf padded), cand_idx int32 [M, cap]
+    (defined for the first count entries of a row only), count int32 [M]; count > cap means the
+    list overflowed)."""
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 CUDA operands required")
     expect(A.stride(-1) == 1 and B.stride(-1) == 1 and A.stride(0) % 8 == 0 and B.stride(0) % 8 == 0,
            "operands must be K-contiguous with row strides % 8 == 0")
@@ -437,7 +438,7 @@ def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
         _i32(q_group)
         expect(q_group.numel() >= M, "q_group shorter than M")
     cand_val = torch.full((M, cap), float("-inf"), dtype=torch.float32, device=A.device)
-    cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
+    cand_idx = torch.empty((M, cap), dtype=torch.int32, device=A.device)
     cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
     native().gemm_score_candidates(ptr(A), A.stride(0), ptr(B), B.stride(0), M, N, K, ptr(row_group), ptr(q_group),
                                    ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A))
@@ -463,7 +464,7 @@ def score_candidates_shuffled(A, B_shuf, N, thr, cap, row_group=None, q_group=No
         _i32(q_group)
         expect(q_group.numel() >= M, "q_group shorter than M")
     cand_val = torch.full((M, cap), float("-inf"), dtype=torch.float32, device=A.device)
-    cand_idx = torch.zeros((M, cap), dtype=torch.int32, device=A.device)
+    cand_idx = torch.empty((M, cap), dtype=torch.int32, device=A.device)
     cnt = torch.zeros(M, dtype=torch.int32, device=A.device)
     native().score_candidates_shuf(ptr(A), A.stride(0), ptr(B_shuf), M, int(N), K, ptr(row_group), ptr(q_group),
                                    ptr(thr), ptr(cnt), ptr(cand_val), ptr(cand_idx), int(cap), stream(A),
