@@ -1,4 +1,9 @@
-"""Django admin for bots, dialogs, instances and messages (reference bot/admin.py)."""
+"""Django admin for bots, dialogs, instances and messages (reference bot/admin.py).
+
+The classes are not registered here: as in the reference (whose ``@admin.register`` lines are
+commented out, reference bot/admin.py:19,37,63,104), the host project registers them
+(reference example/bot/admin.py:6-9 ``admin.site.register(Bot, BotAdmin)`` ...); registering them
+here too would make the host's registration raise ``AlreadyRegistered``."""
 from django import forms
 from django.contrib import admin
 from django.db import models
@@ -16,7 +21,6 @@ class BotAdminForm(forms.ModelForm):
         fields = "__all__"
 
 
-@admin.register(Bot)
 class BotAdmin(admin.ModelAdmin):
     form = BotAdminForm
     list_display = ["codename", "is_whitelist_enabled"]
@@ -29,7 +33,6 @@ class BotAdmin(admin.ModelAdmin):
         return obj.callback_url
 
 
-@admin.register(Dialog)
 class DialogAdmin(admin.ModelAdmin):
     list_display = ("id", "bot_link", "instance_link", "is_completed", "messages_link")
     list_filter = ["is_completed", "instance__bot__codename"]
@@ -52,7 +55,6 @@ class DialogAdmin(admin.ModelAdmin):
         return format_html('<a href="{}?dialog__id__exact={}">View messages ({})</a>', url, obj.id, n)
 
 
-@admin.register(Instance)
 class InstanceAdmin(admin.ModelAdmin):
     list_display = ("username_display", "bot_link", "created_at", "is_unavailable", "total_cost")
     search_fields = ["user__username", "bot__codename"]
@@ -77,7 +79,6 @@ class InstanceAdmin(admin.ModelAdmin):
         return obj._total_cost
 
 
-@admin.register(Message)
 class MessageAdmin(admin.ModelAdmin):
     list_display = ["timestamp", "dialog_link", "role", "short_text", "io_tokens"]
     search_fields = ["text", "role__name"]

@@ -1,7 +1,8 @@
 """Campaign admin with a "send test message" widget (reference broadcasting/admin.py:25-267).
 
 Both test paths send the campaign text as a plain {'text': ...} answer (the reference json-parsed the
-text in one path and wrapped it in the other)."""
+text in one path and wrapped it in the other).  Registration is the host's, as in the reference
+(``admin.site.register(BroadcastCampaign, BroadcastCampaignAdmin)`` in a host app's admin.py)."""
 import json
 import logging
 
@@ -35,7 +36,6 @@ def send_test(bot_codename: str, platform_code: str, text: str, username: str) -
     return f"Test message sent to {username}."
 
 
-@admin.register(BroadcastCampaign)
 class BroadcastCampaignAdmin(admin.ModelAdmin):
     list_display = ("__str__", "bot", "platform", "status", "total_recipients", "successful_sents", "failed_sents",
                     "created_at")

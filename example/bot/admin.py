@@ -1,13 +1,11 @@
-"""Admin registrations of the example project (reference example/bot/admin.py): the library's model
-admins are registered by the apps themselves; here only the token admin is added."""
+"""Admin registrations of the example host (reference example/bot/admin.py:6-9): the library ships
+the model admins, the host decides what its admin site shows."""
 from django.contrib import admin
 
-from assistant.admin.admin import TokenAdmin
+from assistant.bot.admin import BotAdmin, DialogAdmin, InstanceAdmin, MessageAdmin
+from assistant.bot.models import Bot, Dialog, Instance, Message
 
-try:
-    from rest_framework.authtoken.models import TokenProxy
-
-    admin.site.unregister(TokenProxy)
-    admin.site.register(TokenProxy, TokenAdmin)
-except Exception:  # authtoken not installed / not registered
-    pass
+admin.site.register(Bot, BotAdmin)
+admin.site.register(Instance, InstanceAdmin)
+admin.site.register(Dialog, DialogAdmin)
+admin.site.register(Message, MessageAdmin)

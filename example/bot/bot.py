@@ -4,8 +4,9 @@ Shows the extension points of ``AssistantBot``:
   * ``get_answer_to_messages`` replaced by intent routing (fast-model classification into
     #create_task / #list_tasks / #other) instead of the RAG pipeline;
   * a small state machine kept in ``instance.state`` (title -> priority -> confirmation);
-  * ``@TaskManagerBot.command`` handlers for callback buttons and slash commands, including /start and
-    /help which override the built-ins.
+  * ``@AssistantBot.command`` handlers written as methods of the class, as the reference host does
+    (the library moves them into this class's own registry), including ``command_start`` /
+    ``command_help``, which replace the built-in /start and /help.
 
 Tasks live in the instance state (``state['tasks']``), so the demo needs no models of its own.
 """
@@ -37,7 +38,7 @@ def pick_intent(text: str) -> str:
 
 
 class TaskManagerBot(AssistantBot):
-    _command_handlers: list = []  # this bot's own command registry
+    """Creates and lists tasks kept in the instance state."""
 
     # -------------------------------------------------------------------------------- routing
     async def get_answer_to_messages(self, messages, debug_info, do_interrupt) -> Answer:
@@ -94,61 +95,54 @@ class TaskManagerBot(AssistantBot):
         return SingleAnswer(f"📋 Task list:\n\n{body}", buttons=[
             [Button("➕ New task", callback_data="/new_task")], [Button("🏠 Main menu", callback_data="/start")]])
 
+    # ------------------------------------------------------------------------------- commands
+    @AssistantBot.command(r"/priority (high|medium|low)$")
+    async def set_priority(self, match: re.Match, message_id: Optional[int] = None) -> Answer:
+        if self.instance.state.get("awaiting_input") != "task_priority":
+            return SingleAnswer("Nothing to set a priority for.", no_store=True)
+        task = dict(self.instance.state.get("new_task") or {}, priority=match.group(1))
+        await self.update_state({"awaiting_input": "confirming", "new_task": task})
+        return MultiPartAnswer([
+            SingleAnswer(f"Selected priority: {task['priority']}"),
+            SingleAnswer(f"Create task?\n{task['title']} ({task['priority']} priority)", buttons=[
+                [Button("✅ Confirm", callback_data="/confirm_task")],
+                [Button("❌ Cancel", callback_data="/cancel")]]),
+        ])
 
-@TaskManagerBot.command(r"/priority (high|medium|low)$")
-async def set_priority(bot: TaskManagerBot, match: re.Match, message_id: Optional[int] = None) -> Answer:
-    if bot.instance.state.get("awaiting_input") != "task_priority":
-        return SingleAnswer("Nothing to set a priority for.", no_store=True)
-    task = dict(bot.instance.state.get("new_task") or {}, priority=match.group(1))
-    await bot.update_state({"awaiting_input": "confirming", "new_task": task})
-    return MultiPartAnswer([
-        SingleAnswer(f"Selected priority: {task['priority']}"),
-        SingleAnswer(f"Create task?\n{task['title']} ({task['priority']} priority)", buttons=[
-            [Button("✅ Confirm", callback_data="/confirm_task")], [Button("❌ Cancel", callback_data="/cancel")]]),
-    ])
+    @AssistantBot.command(r"/confirm_task$")
+    async def confirm_task(self, match=None, message_id=None) -> Answer:
+        if self.instance.state.get("awaiting_input") != "confirming":
+            return SingleAnswer("Nothing to confirm.", no_store=True)
+        tasks = list(self.instance.state.get("tasks") or []) + [self.instance.state["new_task"]]
+        logger.info("task created: %s", tasks[-1])
+        await self.update_state({"tasks": tasks, "awaiting_input": None, "new_task": None})
+        return MultiPartAnswer([SingleAnswer("🎉 Task created!"), SingleAnswer("What's next?", buttons=[
+            [Button("➕ New task", callback_data="/new_task")], [Button("📋 Task list", callback_data="/list")]])])
 
+    @AssistantBot.command(r"/cancel$")
+    async def cancel(self, match=None, message_id=None) -> Answer:
+        tasks = self.instance.state.get("tasks") or []
+        await self.clear_state()
+        await self.update_state({"tasks": tasks})  # keep the task list, drop the pending operation
+        return SingleAnswer("❌ Operation cancelled", buttons=[[Button("Main menu", callback_data="/start")]])
 
-@TaskManagerBot.command(r"/confirm_task$")
-async def confirm_task(bot: TaskManagerBot, match=None, message_id=None) -> Answer:
-    if bot.instance.state.get("awaiting_input") != "confirming":
-        return SingleAnswer("Nothing to confirm.", no_store=True)
-    tasks = list(bot.instance.state.get("tasks") or []) + [bot.instance.state["new_task"]]
-    logger.info("task created: %s", tasks[-1])
-    await bot.update_state({"tasks": tasks, "awaiting_input": None, "new_task": None})
-    return MultiPartAnswer([SingleAnswer("🎉 Task created!"), SingleAnswer("What's next?", buttons=[
-        [Button("➕ New task", callback_data="/new_task")], [Button("📋 Task list", callback_data="/list")]])])
+    @AssistantBot.command(r"/list$")
+    async def list_tasks(self, match=None, message_id=None) -> Answer:
+        return self.task_list()
 
+    @AssistantBot.command(r"/new_task$")
+    async def new_task(self, match=None, message_id=None) -> Answer:
+        return await self.initiate_task_creation()
 
-@TaskManagerBot.command(r"/cancel$")
-async def cancel(bot: TaskManagerBot, match=None, message_id=None) -> Answer:
-    tasks = bot.instance.state.get("tasks") or []
-    await bot.clear_state()
-    await bot.update_state({"tasks": tasks})  # keep the task list, drop the pending operation
-    return SingleAnswer("❌ Operation cancelled", buttons=[[Button("Main menu", callback_data="/start")]])
+    @AssistantBot.command(r"/start")
+    async def command_start(self, *args, **kwargs) -> Answer:
+        return MultiPartAnswer([SingleAnswer("🖖 Welcome to TaskBot!"),
+                                SingleAnswer("Choose action:", buttons=MAIN_MENU)])
 
-
-@TaskManagerBot.command(r"/list$")
-async def list_tasks(bot: TaskManagerBot, match=None, message_id=None) -> Answer:
-    return bot.task_list()
-
-
-@TaskManagerBot.command(r"/new_task$")
-async def new_task(bot: TaskManagerBot, match=None, message_id=None) -> Answer:
-    return await bot.initiate_task_creation()
-
-
-async def _start(self, text: str = "") -> Answer:
-    return MultiPartAnswer([SingleAnswer("🖖 Welcome to TaskBot!"), SingleAnswer("Choose action:",
-                                                                                buttons=MAIN_MENU)])
-
-
-async def _help(self) -> Answer:
-    return SingleAnswer("🤖 *TaskBot - Task Management*\n\n📝 *Commands:*\n\n"
-                        "• /new_task - Create a task\n• /list - Task list\n• /cancel - Cancel operation\n"
-                        "• /start - Main menu",
-                        buttons=[[Button("🏠 Main menu", callback_data="/start")],
-                                 [Button("➕ New task", callback_data="/new_task")]])
-
-
-TaskManagerBot.command_start = _start  # the built-in /start and /help are replaced
-TaskManagerBot.command_help = _help
+    @AssistantBot.command(r"/help")
+    async def command_help(self, *args, **kwargs) -> Answer:
+        return SingleAnswer("🤖 *TaskBot - Task Management*\n\n📝 *Commands:*\n\n"
+                            "• /new_task - Create a task\n• /list - Task list\n• /cancel - Cancel operation\n"
+                            "• /start - Main menu",
+                            buttons=[[Button("🏠 Main menu", callback_data="/start")],
+                                     [Button("➕ New task", callback_data="/new_task")]])
