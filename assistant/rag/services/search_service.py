@@ -68,12 +68,13 @@ async def embedding_search_sentences(query_embedding, qs, n: int = 10):
 async def _objects_embedding_search(query_embedding, qs, n: int = 10, field: str = "embedding"):
     """The ``n`` rows of ``qs`` nearest to the query, ascending cosine distance, each annotated with
     ``.distance`` exactly like ``qs.annotate(distance=CosineDistance(field, q)).order_by('distance')[:n]``."""
-    from assistant.storage.index import get_index_service
+    from assistant.storage.index import MAX_SEARCH_K, get_index_service
 
     def run():
         svc = get_index_service()
-        want = n
-        for _ in range(_REFILL_ROUNDS):
+        want = min(n, MAX_SEARCH_K)
+        out = []
+        for _round in range(_REFILL_ROUNDS):
             hits = svc.search(qs, query_embedding, want, field)
             if not hits:
                 return []
@@ -88,11 +89,13 @@ async def _objects_embedding_search(query_embedding, qs, n: int = 10, field: str
             # LIMIT n semantics (reference search_service.py:191-195): n qualifying rows whenever
             # they exist.  Hits the QuerySet rejected mean stale mirrored metadata: re-mirror those
             # rows and search again, over-fetching by what was lost, until n rows qualify or the
-            # index has no more candidates under the filter.
+            # index has no more candidates under the filter.  The request never grows past the
+            # index's largest k (a bigger one fails on gpu_service); at that size every round still
+            # repairs the rows it dropped, up to _REFILL_ROUNDS searches.
             if len(out) >= n or not dropped or len(hits) < want:
                 break
             svc.refresh_rows(qs.model, dropped, field)
-            want = max(2 * want, n + len(dropped))
+            want = min(max(2 * want, n + len(dropped)), MAX_SEARCH_K)
         return out[:n]
 
     return await sync_to_async(run)()

@@ -28,6 +28,9 @@ from assistant.conf import settings
 
 logger = logging.getLogger(__name__)
 
+# Largest k one index search returns (the top-k kernels' bound; gpu_service rejects more with a 400)
+MAX_SEARCH_K = 1024
+
 SEARCHABLE = {
     "assistant_storage.question": "embedding",
     "assistant_storage.sentence": "embedding",
@@ -186,7 +189,7 @@ class _EngineBackend:
         idx = self._idx.get(name)
         if idx is None or len(idx) == 0:
             return [], []
-        sims, ids, _ = idx.search(np.asarray(q, dtype=np.float32)[None], min(n, 1024),
+        sims, ids, _ = idx.search(np.asarray(q, dtype=np.float32)[None], min(n, MAX_SEARCH_K),
                                   q_groups=None if group is None else [group],
                                   allowed=None if allowed is None else [allowed],
                                   doc_lt=None if doc_lt is None else [doc_lt])
@@ -221,7 +224,7 @@ class _GPUServiceBackend:
         self._post(f"/index/{name}/delete", {"ids": list(map(int, ids))})
 
     def search(self, name, q, n, allowed, group, doc_lt=None):
-        r = self._post(f"/index/{name}/search", {"queries": [list(map(float, q))], "k": int(n),
+        r = self._post(f"/index/{name}/search", {"queries": [list(map(float, q))], "k": min(int(n), MAX_SEARCH_K),
                                                  "groups": None if group is None else [int(group)],
                                                  "allowed": None if allowed is None else [list(map(int, allowed))],
                                                  "doc_lt": None if doc_lt is None else [int(doc_lt)]})

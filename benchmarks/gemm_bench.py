@@ -26,7 +26,16 @@ SHAPES = {
             ("bge-up", 65536, 3072, 768, "gelu"), ("bge-down", 65536, 768, 3072, "bias")],
     "square": [("sq4096", 4096, 4096, 4096, "none"), ("sq8192", 8192, 8192, 8192, "none")],
     "edge": [("edge-m1000", 1000, 1024, 512, "none"), ("edge-m300", 300, 512, 256, "bias")],
+    # mixed prefill + decode steps: M = 384 / 640 / 1024 tokens per step
+    "mid": [(f"mid{M}-{n}", M, N, K, kind) for M in (384, 640, 1024)
+            for n, N, K, kind in (("qkv", 6144, 4096, "none"), ("o", 4096, 4096, "none"),
+                                  ("gateup", 28672, 4096, "swiglu"), ("down", 4096, 14336, "none"))],
 }
+
+
+def roofline_us(M, N, K):
+    """max(weight bytes / 6 TB/s, FLOPs / 1.5 PF/s): the mid-M target of VERDICT r4 item 1."""
+    return max(2.0 * N * K / 6e12, 2.0 * M * N * K / 1.5e15) * 1e6
 
 
 def rand(shape, scale=1.0):
@@ -84,7 +93,7 @@ def main():
             b = rand((N,), 0.5)
             n_out = N // 2 if kind == "swiglu" else N
             out = torch.empty((M, n_out), dtype=torch.bfloat16, device="cuda")
-            frag = group == "llama"
+            frag = group in ("llama", "mid")
             ws = ops.shuffle_weights(w) if frag else w
             run_native(a, ws, b, kind, out, frag)
             torch.cuda.synchronize()
@@ -94,6 +103,8 @@ def main():
             arms = [("nat", lambda: run_native(a, ws, b, kind, out, frag)), ("lib", lambda: run_lib(a, w, b, kind))]
             if args.native_only:
                 arms = arms[:1]
+            if group == "mid" and frag and ops.native().gemm256_ok(M, N, K, K, K):
+                arms.append(("g256", lambda: ops.kernels.gemm256(a, ws, epilogue=EPI[kind], shuffled=True)))
             if args.ab_layout and frag:
                 arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
             extra = {}
@@ -119,6 +130,8 @@ def main():
                               "native_tflops": round(flop / tn / 1e6, 1), "lib_tflops": round(flop / tl / 1e6, 1),
                               "speedup": round(tl / tn, 3), "max_abs_err": round(err, 5),
                               "ref_max": round(scale, 3), "ok": err <= 0.02 * max(scale, 1.0),
+                              "roofline_us": round(roofline_us(M, N, K), 1),
+                              "vs_roofline": round(tn / roofline_us(M, N, K), 3),
                               **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()}}),
                   flush=True)
             del a, w, ws, b, out

@@ -97,6 +97,15 @@ __device__ __forceinline__ void bar() {
   asm volatile("" ::: "memory");
 }
 
+// The barrier after a phase's LDS reads: those reads are retired first (gfx950's s_barrier does not
+// wait for lgkmcnt), so the DMA the other wave group issues one phase later into a piece read here
+// is ordered after the reads by the barrier itself, not by load latency.  Nearly free:
+// the MFMAs behind the barrier need the data anyway.
+__device__ __forceinline__ void read_bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+}
+
 constexpr int kBuf = 65536;   // one K-tile: A0 | A1 | B0 | B1, 16 KB each
 constexpr int kHalf = 16384;  // 128 rows x 128 B
 // G_CAND, M <= kCandMaxM: after the two K-tile buffers, the thresholds [kCandMaxM] fp32, 8 per-wave
@@ -353,7 +362,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       stage(1, 1, o, rA, rB);
       if (fe) wait_vm<8 + kEpi>();
       else wait_vm<8>();
-      bar();
+      read_bar();
       G256_MFMA2(0, 0, 1)
       bar();
       // phase 2
@@ -367,7 +376,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
       } else {
         wait_vm<0>();
       }
-      bar();
+      read_bar();
       if (h2) {
         G256_MFMA2(1, 1, 0)
       }
@@ -380,7 +389,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         stage(0, 1, ke, sa, sb);
         wait_vm<8>();
       }
-      bar();
+      read_bar();
       G256_MFMA2(0, 0, 1)
       bar();
       // phase 4
@@ -391,7 +400,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
         stage(1, 3, ko, sa, sb);
         wait_vm<8>();
       }
-      bar();
+      read_bar();
       if (h2) {
         G256_MFMA2(1, 1, 0)
       }

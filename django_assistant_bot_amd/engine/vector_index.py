@@ -287,7 +287,24 @@ class VectorIndex:
         tv, _ = ops.topk_rows(s_scores, kk)
         del s_scores
         thr = tv[:, kk - 1].contiguous()
-        cap = max(4096, 64 * k * self.sample_stride // 16)
+        # about k * stride scores clear the sample's k-th best (its rank in the whole index); the
+        # lists hold twice that plus a fixed margin (the count's spread is ~sqrt(k) * stride).  Above
+        # a byte budget for the [q, cap] lists the queries go through in chunks (k = 1024
+        # at 512 queries asked for ~1 GB of candidate memory per search).
+        cap = 2 * k * self.sample_stride + 4096
+        per_chunk = max(1, self.CAND_BYTES // (8 * cap))
+        if q.shape[0] > per_chunk:
+            parts = [self._threshold_candidates(q[i:i + per_chunk], thr[i:i + per_chunk], k, cap, n4,
+                                                None if qg is None else qg[i:i + per_chunk])
+                     for i in range(0, q.shape[0], per_chunk)]
+            if any(p is None for p in parts):
+                return None
+            return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+        return self._threshold_candidates(q, thr, k, cap, n4, qg)
+
+    CAND_BYTES = 256 << 20  # candidate-list memory of one threshold search
+
+    def _threshold_candidates(self, q, thr, k: int, cap: int, n4: int, qg):
         if self.frag:
             cand_val, cand_idx, cnt = ops.score_candidates_shuffled(q, self.vecs, n4, thr, cap, self.row_group[:n4], qg)
         else:
@@ -297,8 +314,8 @@ class VectorIndex:
             self.stats["threshold_overflows"] += 1
             return None
         self.stats["threshold_searches"] += 1
-        # only the filled prefix of the lists (the longest one, ~16k of the 64k-entry capacity on
-        # unstructured data) is ranked; shorter lists are -inf past their count
+        # only the filled prefix of the lists (the longest one, ~16k of the 36k-entry capacity at
+        # k = 250 on unstructured data) is ranked; shorter lists are -inf past their count
         n_use = min(cap, max(k, -(-cmax // 64) * 64))
         vals, pos = ops.topk_rows(cand_val[:, :n_use], min(k, n_use))
         rows = torch.gather(cand_idx, 1, pos.long())

@@ -261,3 +261,55 @@ def test_stale_group_bits_refill_to_n(data, monkeypatch):
     # the mirror is repaired: the next search needs no refill
     hits = svc.search(qs, q, 5)
     assert [p for p, _ in hits] == order[3:8]
+
+
+def test_refill_never_asks_past_the_largest_k(data, monkeypatch):
+    """``embedding_search`` asks for n = 10 * 10 * 10 = 1000 rows; a stale hit used to double
+    the next request to >= 2000, which gpu_service rejects (k <= 1024, gpu_service/main.py) and the
+    whole RAG search failed.  A backend with gpu_service's bound: every request stays <= 1024 and the
+    search returns the qualifying rows."""
+    import asyncio
+
+    from assistant.rag.services import search_service
+
+    vecs, ids, docs, groups = data
+    g_hot = int(index_mod.row_group(2, 1))
+    q = np.random.default_rng(5).standard_normal(DIM).astype(np.float32)
+    # every row is filed under the hot group, in the mirror and the DB, except one stale row: the
+    # best match, which the DB has since moved to another bot
+    best = int(ids[np.argmax((vecs / np.linalg.norm(vecs, axis=1, keepdims=True)) @ q)])
+    db_groups = {int(i): g_hot for i in ids}
+    db_groups[best] = int(index_mod.row_group(3, 1))
+    members = {pk for pk, g in db_groups.items() if g == g_hot}
+
+    class BoundedBackend(index_mod._EngineBackend):
+        asked = []
+
+        def search(self, name, qv, n, allowed, group, doc_lt=None):
+            self.asked.append(int(n))
+            if not 1 <= int(n) <= index_mod.MAX_SEARCH_K:  # what gpu_service answers with a 400
+                raise ValueError("k must be in [1, 1024]")
+            return super().search(name, qv, n, allowed, group, doc_lt)
+
+    svc = index_mod.IndexService(backend="engine")
+    svc._be = BoundedBackend()
+    name = "assistant_storage.question.embedding"
+    svc._be.upsert(name, ids, vecs, docs, np.full(len(ids), g_hot, dtype=np.int32))
+    monkeypatch.setattr(svc, "ensure_loaded", lambda *a: None)
+    row_of = {int(i): r for r, i in enumerate(ids)}
+
+    def meta(model, field, rows):
+        pks = np.asarray([o.pk for o in rows], dtype=np.int64)
+        r = np.asarray([row_of[int(p)] for p in pks], dtype=np.int64)
+        return pks, docs[r], np.asarray([db_groups[int(p)] for p in pks], dtype=np.int32), vecs[r]
+
+    monkeypatch.setattr(index_mod, "_meta_values", meta)
+    qs = index_mod.with_index_filter(StubQS([]), bot=2, completed=True)
+    fqs = _FilterQS(members)
+    qs.filter, qs.model = fqs.filter, types.SimpleNamespace(_meta=_Meta("assistant_storage.question"), objects=fqs)
+    monkeypatch.setattr(index_mod, "get_index_service", lambda: svc)
+    got = asyncio.run(search_service.embedding_search_questions(q, qs, n=1000))
+    assert BoundedBackend.asked == [1000, index_mod.MAX_SEARCH_K]  # the old loop asked for 2000 next
+    assert len(got) == 1000
+    assert all(o.pk in members for o in got)
+    assert all(a.distance <= b.distance + 1e-6 for a, b in zip(got, got[1:]))
