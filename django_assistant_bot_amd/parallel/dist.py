@@ -35,8 +35,30 @@ def env_world() -> tuple[int, int, int]:
             int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", 0))))
 
 
+def force_group() -> bool:
+    """``DAB_FORCE_GROUP=1``: form the process group even for a world of one rank, so every
+    collective branch (RCCL device-tensor all_gather / all_to_all / gather / barrier, the node's
+    control broadcasts) runs on a single GPU exactly as it does at 8."""
+    return os.environ.get("DAB_FORCE_GROUP", "") not in ("", "0")
+
+
+def grouped() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
 def init(backend: str | None = None, device_type: str | None = None, timeout_s: int = 600) -> DistInfo:
-    """Initialise the default group when WORLD_SIZE > 1 (idempotent).  GPU ranks bind cuda:LOCAL_RANK."""
+    """Initialise the default group when WORLD_SIZE > 1, or at any world size under
+    ``DAB_FORCE_GROUP`` (idempotent).  GPU ranks bind cuda:LOCAL_RANK."""
     rank, world, local = env_world()
     if device_type is None:
         device_type = "cuda" if torch.cuda.is_available() else "cpu"
@@ -50,8 +72,10 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
         device = torch.device("cpu")
     if backend is None:
         backend = os.environ.get("DAB_DIST_BACKEND") or ("nccl" if device_type == "cuda" else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or force_group()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1 and "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(_free_port())
         kw = {}
         if backend == "nccl":
             kw["device_id"] = device
@@ -65,7 +89,7 @@ def init(backend: str | None = None, device_type: str | None = None, timeout_s: 
             kw["store"] = dist.PrefixStore(f"dab/attempt_{attempt}", base)
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
-    return DistInfo(rank, world, local, device, backend if world > 1 else "none")
+    return DistInfo(rank, world, local, device, backend if dist.is_initialized() else "none")
 
 
 def barrier(info: DistInfo | None = None) -> None:

@@ -59,7 +59,7 @@ def embed_corpus(engine, text_of: Callable[[int], str], n: int, rank: int = 0, w
         pool.shutdown()
     local = torch.cat(out_vecs) if out_vecs else None
     total = len(ids)
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():  # (also a world-1 group under DAB_FORCE_GROUP)
         dev = engine.device if dist.get_backend() == "nccl" else torch.device("cpu")
         t = torch.tensor([total], dtype=torch.int64, device=dev)
         dist.all_reduce(t)

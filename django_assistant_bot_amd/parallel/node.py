@@ -132,10 +132,13 @@ class Node:
 
         self.info, self.plan = info, plan
         self.rank, self.world = info.rank, info.world_size
+        # commands go through the control group whenever one exists: W > 1, or a world-1 group
+        # formed on purpose (DAB_FORCE_GROUP) so the broadcast paths run on one GPU too
+        self.grouped = pdist.grouped()
         self.device = info.device
         assert plan.world == self.world, "plan built for another world size"
         W, T, R = self.world, plan.gen_tp, plan.gen_replicas
-        if ctrl is None and W > 1:
+        if ctrl is None and self.grouped:
             ctrl = control_group(list(range(W)))
         self.ctrl = ctrl
         self.tp_group, self.tp_rank, self.replica = pdist.tp_groups(T)
@@ -223,7 +226,7 @@ class Node:
         hdr = torch.zeros(wire.HDR, dtype=torch.int64)
         hdr[0] = _CODE[op]
         hdr[1:1 + len(words)] = torch.tensor(words, dtype=torch.int64)
-        if self.world > 1:
+        if self.grouped:
             dist.broadcast(hdr, src=0, group=self.ctrl)
         self.commands += 1
         with self._side_stream():
@@ -262,7 +265,7 @@ class Node:
         if self.rank == 0 and not self._stopped:
             self._stop_llm_links()
             with self._cmd_lock:
-                if self.world > 1 and self.healthy:
+                if self.grouped and self.healthy:
                     try:
                         self._run("stop", None)
                     except Exception:
@@ -270,7 +273,7 @@ class Node:
                 self._stopped = True
 
     def _bcast(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world > 1:
+        if self.grouped:
             dist.broadcast(t, src=0, group=self.ctrl)
         return t
 
@@ -294,7 +297,7 @@ class Node:
         return [int(rank)]
 
     def _cdev(self, group):
-        if self.world == 1:
+        if not self.grouped:
             return self.device
         return self.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
 
@@ -310,7 +313,7 @@ class Node:
 
     def _index_total(self, local: int) -> int:
         t = torch.tensor([local], dtype=torch.int64, device=self._cdev(self.index_group))
-        if self.plan.index_shards > 1:
+        if self.grouped:
             dist.all_reduce(t, group=self.index_group)
         return int(t.item())
 
@@ -456,7 +459,7 @@ class Node:
             mine = _words_texts(offs.numpy(), flat.numpy())
         eng = self.embeds[name]
         v = eng.embed(mine, normalize=norm, out_dtype=torch.float32)
-        if D == 1:
+        if D == 1 and not self.grouped:
             return v
         cdev = self._cdev(self.embed_group)
         rows = math.ceil(n / D)
@@ -596,7 +599,7 @@ class Node:
         t = torch.tensor([self.stats["ctrl_s"], self.stats["llm_steps"], self.stats["upsert_bytes_recv"],
                           self.stats["embed_bytes_recv"], self.stats["ingest_bytes_recv"],
                           self.stats["ingest_vec_bytes_recv"]], dtype=torch.float64)
-        if self.world == 1:
+        if not self.grouped:
             return t[None]
         parts = [torch.zeros_like(t) for _ in range(self.world)] if self.rank == 0 else None
         dist.gather(t, parts, dst=0, group=self.ctrl)

@@ -158,7 +158,7 @@ class ShardedIndex:
         q = torch.as_tensor(queries).to(self.device, torch.float32)
         if q.ndim == 1:
             q = q[None]
-        if not self.distributed or self.world == 1:
+        if not self.distributed:  # (a world-1 group, DAB_FORCE_GROUP, runs the collectives)
             return self.local.search(q, k, q_groups)
         cdev = self._comm_device()
         nq = q.shape[0]
@@ -219,7 +219,7 @@ class ShardedIndex:
         q = torch.as_tensor(queries).to(self.device, torch.float32)
         if q.ndim == 1:
             q = q[None]
-        if not self.distributed or self.world == 1:
+        if not self.distributed:  # (a world-1 group, DAB_FORCE_GROUP, runs the collectives)
             return self.local.search(q, k, q_groups, allowed=allowed, doc_lt=doc_lt)
         nq = q.shape[0]
         cdev = self._comm_device()
