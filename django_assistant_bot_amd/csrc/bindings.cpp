@@ -237,10 +237,22 @@ PYBIND11_MODULE(_native, m) {
                                     ST(s)),
           "sample_tokens_2stage");
   });
-  m.def("mask_logits", [](u logits, int f32, long ld, int rows, int vocab, u mask, int words, u row_flags, u s) {
+  m.def("mask_logits", [](u logits, int f32, long ld, int rows, int vocab, u mask, int words, u row_flags, u s,
+                          long mask_ld) {
     check(dab::mask_logits(VP(logits), f32, ld, rows, vocab, (const uint32_t*)mask, words, (const int*)row_flags,
-                           ST(s)),
+                           ST(s), mask_ld),
           "mask_logits");
+  });
+  m.def("sample_candidates", [](u logits, int f32, long ld, int rows, int vocab, int base, u keys, u idx, int ncand,
+                                u s) {
+    check(dab::sample_candidates(CVP(logits), f32, ld, rows, vocab, base, (uint32_t*)keys, (int*)idx, ncand, ST(s)),
+          "sample_candidates");
+  });
+  m.def("sample_merge", [](u keys, u idx, int ncand, int rows, int vocab, u temp, u top_k, u top_p,
+                           unsigned long long seed, u counters, u out_tokens, u s) {
+    check(dab::sample_merge((const uint32_t*)keys, (const int*)idx, ncand, rows, vocab, (const float*)temp,
+                            (const int*)top_k, (const float*)top_p, seed, (int64_t*)counters, (int*)out_tokens, ST(s)),
+          "sample_merge");
   });
   m.def("topk_rows_2stage", [](u scores, long ld, int rows, int n, int k, u out_vals, u out_idx, long long base,
                                u out_idx64, u ws, size_t ws_bytes, u s) {

@@ -100,7 +100,13 @@ int stream_gemm_shuffled(int cfg);  // 1: cfg reads weights in the ops.shuffle_w
 // Disallowed tokens of the rows with row_flags[r] != 0 (mask bit clear) -> -inf logits, in place
 // (JSON-constrained decoding); rows without the flag are untouched.
 int mask_logits(void* logits, int logits_f32, long ld, int rows, int vocab, const uint32_t* mask, int words,
-                const int* row_flags, hipStream_t s);
+                const int* row_flags, hipStream_t s, long mask_ld = 0);
+// vocab-parallel sampling (TP): stage 1 on a vocabulary slice, stage 2 on the all-gathered candidates
+int sample_candidates(const void* logits, int logits_f32, long ld, int rows, int vocab, int index_base,
+                      uint32_t* cand_key, int* cand_idx, int ncand, hipStream_t s);
+int sample_merge(const uint32_t* cand_key, const int* cand_idx, int ncand, int rows, int vocab,
+                 const float* temperature, const int* top_k, const float* top_p, unsigned long long seed,
+                 int64_t* counters, int* out_tokens, hipStream_t s);
 int sample_tokens(const void* logits, int logits_f32, long ld, int rows, int vocab, const float* temperature,
                   const int* top_k, const float* top_p, unsigned long long seed, int64_t* counters, int* out_tokens,
                   float* out_logprobs, hipStream_t s);

@@ -266,7 +266,7 @@ struct ChunkFast {
 template <int PT>
 __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restrict__ src, int src_bf16, long ld, int n,
                                                            int k, int kc, uint32_t* __restrict__ cand_key,
-                                                           int* __restrict__ cand_idx) {
+                                                           int* __restrict__ cand_idx, int index_base = 0) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t bc[2];
   __shared__ uint32_t cnt[2];
@@ -350,7 +350,7 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
       if (slot >= 0 && slot < CH_FAST_CAP) {
         uint32_t* e2 = reinterpret_cast<uint32_t*>(fst.kv) + 2 * slot;
         e2[0] = key[j];
-        e2[1] = (uint32_t)(start + i);
+        e2[1] = (uint32_t)(index_base + start + i);
       }
     }
     __syncthreads();
@@ -457,12 +457,12 @@ __global__ __launch_bounds__(CH_NT) void chunk_topk_kernel(const void* __restric
     const int pg = wave_append(&cnt[0], valid && key[j] > prefix);
     if (pg >= 0) {
       ok[pg] = key[j];
-      oi[pg] = start + i;
+      oi[pg] = index_base + start + i;
     }
     const int pe = wave_append(&cnt[1], valid && key[j] == prefix);
     if (pe >= 0 && (uint32_t)pe < need) {
       ok[n_gt + pe] = key[j];
-      oi[n_gt + pe] = start + i;
+      oi[n_gt + pe] = index_base + start + i;
     }
   }
   for (int i = kk + tid; i < kc; i += CH_NT) {
@@ -593,6 +593,32 @@ int sample_tokens_2stage(const void* logits, int logits_f32, long ld, int rows, 
   return hipGetLastError();
 }
 
+// Vocab-parallel sampling under tensor parallelism: stage 1 on this rank's slice of the vocabulary
+// (token ids offset by the slice start), candidates [rows][ncand] keys then [rows][ncand] ids; the TP
+// ranks all-gather them and every rank runs stage 2 on the same union with the same counters, so all
+// ranks draw the same token without a broadcast.  The union of per-chunk top-64s holds the global
+// top-k (k <= 64), so the draw is the replicated head's draw on the same logits.
+int sample_candidates(const void* logits, int logits_f32, long ld, int rows, int vocab, int index_base,
+                      uint32_t* cand_key, int* cand_idx, int ncand, hipStream_t s) {
+  if (rows <= 0) return 0;
+  constexpr int PT = 32, KC = 64;
+  const int nchunks = (vocab + CH_NT * PT - 1) / (CH_NT * PT);
+  if (vocab <= 0 || ncand != nchunks * KC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(chunk_topk_kernel<PT>, dim3(nchunks, rows), dim3(CH_NT), 0, s, logits, logits_f32 ? 0 : 1, ld,
+                     vocab, KC, KC, cand_key, cand_idx, index_base);
+  return hipGetLastError();
+}
+
+int sample_merge(const uint32_t* cand_key, const int* cand_idx, int ncand, int rows, int vocab,
+                 const float* temperature, const int* top_k, const float* top_p, unsigned long long seed,
+                 int64_t* counters, int* out_tokens, hipStream_t s) {
+  if (rows <= 0) return 0;
+  if (ncand <= 0 || ncand > SEL_MAXK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_merge_kernel, dim3(rows), dim3(SEL_NT), 0, s, cand_key, cand_idx, ncand, temperature, top_k,
+                     top_p, vocab, seed, counters, out_tokens);
+  return hipGetLastError();
+}
+
 int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float* out_vals, int* out_idx,
                      int64_t index_base, int64_t* out_idx64, void* workspace, size_t workspace_bytes, hipStream_t s) {
   if (rows <= 0) return 0;
@@ -616,12 +642,12 @@ int topk_rows_2stage(const float* scores, long ld, int rows, int n, int k, float
 // without the flag return after one load.
 __global__ __launch_bounds__(256) void mask_logits_kernel(void* __restrict__ logits, int logits_f32, long ld,
                                                           int vocab, const uint32_t* __restrict__ mask, int words,
-                                                          const int* __restrict__ row_flags) {
+                                                          long mask_ld, const int* __restrict__ row_flags) {
   const int row = blockIdx.y;
   if (row_flags[row] == 0) return;
   const int w = blockIdx.x * 256 + threadIdx.x;
   if (w >= words) return;
-  const uint32_t bits = mask[(size_t)row * words + w];
+  const uint32_t bits = mask[(size_t)row * mask_ld + w];
   if (bits == 0xFFFFFFFFu) return;
   const int t0 = w * 32, n = min(32, vocab - t0);
   if (logits_f32) {
@@ -636,11 +662,12 @@ __global__ __launch_bounds__(256) void mask_logits_kernel(void* __restrict__ log
 }
 
 int mask_logits(void* logits, int logits_f32, long ld, int rows, int vocab, const uint32_t* mask, int words,
-                const int* row_flags, hipStream_t s) {
+                const int* row_flags, hipStream_t s, long mask_ld) {
   if (rows <= 0) return 0;
-  if (vocab <= 0 || words * 32 < vocab) return hipErrorInvalidValue;
+  if (mask_ld <= 0) mask_ld = words;
+  if (vocab <= 0 || words * 32 < vocab || mask_ld < words) return hipErrorInvalidValue;
   hipLaunchKernelGGL(mask_logits_kernel, dim3((words + 255) / 256, rows), dim3(256), 0, s, logits, logits_f32, ld,
-                     vocab, mask, words, row_flags);
+                     vocab, mask, words, mask_ld, row_flags);
   return hipGetLastError();
 }
 

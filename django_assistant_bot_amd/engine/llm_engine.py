@@ -132,7 +132,7 @@ class LLMEngine:
             self.model = shared_model
         else:
             self.model = LlamaModel(cfg, weights, self.device, tp_group=tp_group, tp_size=tp_size,
-                                    interleaved_mlp=interleaved_mlp, consume=own_weights)
+                                    interleaved_mlp=interleaved_mlp, consume=own_weights, tp_rank=tp_rank)
         del weights
         if self.is_gpu and shared_model is None:
             # the caller's weight dict held the row-major originals while the model converted them
@@ -224,6 +224,13 @@ class LLMEngine:
         self._workspace = ops.DecodeWorkspace(mb, cfg.heads // tp_size, cfg.head_dim, max_parts, dev) if self.is_gpu \
             else None
         self._sample_ws = ops.kernels.sample_workspace(mb, cfg.vocab_size, dev) if self.is_gpu else None
+        # vocab-parallel LM head (TP): the decode graph ends with this rank's sampling candidates;
+        # the all-gather and the merge that draws the token run after the replay (_vp_merge)
+        self.vp = bool(getattr(self.model, "vocab_parallel", False))
+        self._vp_cand = None
+        if self.vp and self.is_gpu:
+            ncl = ops.kernels.sample_candidates_per_row(self.model.vocab_local)
+            self._vp_cand = torch.zeros((2, mb, ncl), dtype=torch.int32, device=dev)
         self._graphs: dict = {}
         self._buckets = _bucket_sizes(max_batch)
         self._graph_pool = None
@@ -646,10 +653,29 @@ class LLMEngine:
             self._mask_events[t] = ev
         return True
 
+    def _mask(self, logits, rows: int):
+        m = self.model
+        ops.mask_logits(logits, self._d_mask[:rows], self._d_mflag[:rows], vocab=getattr(m, "vocab_local", None),
+                        word_offset=getattr(m, "vocab_start", 0) // 32)
+
+    def _vp_merge(self, cand, temp, topk, topp, cnt, out=None):
+        """Vocab-parallel draw: all-gather every TP rank's candidates [2, rows, n] and merge them
+        (``ops.sample_merge``); every rank gets the same tokens from the same counters."""
+        import torch.distributed as dist
+
+        src = cand.contiguous()
+        if dist.get_backend(self.tp_group) != "nccl":  # gloo rehearsal of the TP group on one GPU
+            src = src.cpu()
+        parts = [torch.empty_like(src) for _ in range(self.tp_size)]
+        dist.all_gather(parts, src, group=self.tp_group)
+        allc = torch.stack(parts, 2).to(self.device)  # [2, rows, tp, n]
+        allc = allc.reshape(2, allc.shape[1], -1).contiguous()
+        return ops.sample_merge(allc, temp, topk, topp, self.seed, cnt, self.cfg.vocab_size, out=out)
+
     def _sample(self, logits, reqs, to_host: bool = True):
         n = len(reqs)
         if self._fill_masks(reqs, n):
-            ops.mask_logits(logits, self._d_mask[:n], self._d_mflag[:n])
+            self._mask(logits, n)
         temps = torch.tensor([r.params.temperature if r.params.do_sample else 0.0 for r in reqs], dtype=torch.float32)
         topk = torch.tensor([r.params.top_k for r in reqs], dtype=torch.int32)
         topp = torch.tensor([r.params.top_p for r in reqs], dtype=torch.float32)
@@ -658,9 +684,17 @@ class LLMEngine:
             fast = all((0 < r.params.top_k <= ops.kernels.SAMPLE_FAST_MAX_K) or not r.params.do_sample
                        or r.params.temperature <= 0 for r in reqs)
             h = self._h2d
-            toks = ops.sample_tokens(logits, h(temps), h(topk), h(topp), self.seed, h(cnt), fast=fast)
-            toks = self._tp_sync_tokens(toks)
+            if self.vp and fast:
+                cand = ops.sample_candidates(logits, self.model.vocab_local, self.model.vocab_start)
+                toks = self._vp_merge(cand, h(temps), h(topk), h(topp), h(cnt))
+            else:
+                if self.vp:  # exact full-vocabulary sampling (top_k off or > 64): gather the logits
+                    logits = self.model.full_logits(logits)
+                toks = ops.sample_tokens(logits, h(temps), h(topk), h(topp), self.seed, h(cnt), fast=fast)
+                toks = self._tp_sync_tokens(toks)
             return toks.cpu().tolist() if to_host else toks
+        if self.vp:
+            logits = self.model.full_logits(logits)
         g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
         return ops.sample_tokens(logits, temps, topk, topp, self.seed, cnt, generator=g).tolist()
 
@@ -892,7 +926,8 @@ class LLMEngine:
         self._masked = self._fill_masks(batch, Bp)
         t1 = time.perf_counter()
         g = None
-        if self.use_graphs:
+        # (vocab-parallel full-vocabulary sampling gathers the logits in the body: eager)
+        if self.use_graphs and not (self.vp and not self._fast):
             g = self._graphs.get((Bp, self._fast, self._masked))
             if g is None:
                 g = self._capture(Bp)
@@ -903,7 +938,11 @@ class LLMEngine:
             else:
                 self._decode_body(Bp)
         if self.is_gpu:
-            self._tp_sync_tokens(self._d_tokens[:Bp])
+            if self.vp and self._fast:
+                self._vp_merge(self._vp_cand[:, :Bp], self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp],
+                               self._d_cnt[:Bp], out=self._d_tokens[:Bp])
+            else:
+                self._tp_sync_tokens(self._d_tokens[:Bp])
             self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
         t2 = time.perf_counter()
@@ -939,12 +978,19 @@ class LLMEngine:
         h = self.model.forward(self._d_ids[:Bp], meta, self.kv)
         logits = self.model.logits(h)
         if self._masked:
-            ops.mask_logits(logits, self._d_mask[:Bp], self._d_mflag[:Bp])
-        if self.is_gpu:
+            self._mask(logits, Bp)
+        if self.is_gpu and self.vp and self._fast:
+            # this rank's candidates; the all-gather + merge follow the replay (_run_decode)
+            ops.sample_candidates(logits, self.model.vocab_local, self.model.vocab_start, out=self._vp_cand[:, :Bp])
+        elif self.is_gpu:
+            if self.vp:
+                logits = self.model.full_logits(logits)
             ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp], self.seed,
                               self._d_cnt[:Bp], out=self._d_tokens[:Bp], fast=self._fast,
                               workspace=self._sample_ws)
         else:
+            if self.vp:
+                logits = self.model.full_logits(logits)
             g = torch.Generator().manual_seed(int(self.seed * 7919 + int(self._h_cnt[0])))
             self._d_tokens[:Bp] = ops.sample_tokens(logits, self._d_temp[:Bp], self._d_topk[:Bp], self._d_topp[:Bp],
                                                     self.seed, self._d_cnt[:Bp], generator=g)

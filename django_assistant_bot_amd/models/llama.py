@@ -74,14 +74,39 @@ class KVCache:
 
 
 class LlamaModel:
+    # rows of a vocab-parallel LM head shard are padded to a multiple of this (every stream_gemm
+    # tile height and the fragment layout divide it); the pad rows are zero and never sampled
+    VOCAB_PAD = 384
+
     def __init__(self, cfg: DecoderConfig, weights: dict, device, tp_group=None, tp_size: int = 1,
-                 interleaved_mlp: bool = False, fragment_layout: bool = True, consume: bool = False):
+                 interleaved_mlp: bool = False, fragment_layout: bool = True, consume: bool = False,
+                 tp_rank: int | None = None, vocab_parallel: bool = True):
         """``consume``: the entries of ``weights`` are popped as the model takes them over, so each
         original is freed as soon as its fragment-layout copy exists (peak HBM = model + one
-        tensor: 70B at TP 1 needs it, 2 x 140 GB would not fit in 288 GB)."""
+        tensor: 70B at TP 1 needs it, 2 x 140 GB would not fit in 288 GB).
+
+        ``vocab_parallel`` (TP > 1): the LM head is split by vocabulary rows, rank r keeping tokens
+        [r V/tp, (r+1) V/tp) (a replicated head streamed the whole 2.1 GB 70B head
+        on every rank every step).  Each rank then produces the logits of its slice only; the engine
+        samples from the all-gathered per-slice candidates (``ops.sample_candidates`` /
+        ``sample_merge``).  Needs V % (32 tp) == 0 (whole JSON-mask words per slice); otherwise the
+        head stays replicated."""
         self.cfg = cfg
         self.device = torch.device(device)
-        self.tp_group, self.tp_size = tp_group, tp_size
+        if tp_rank is None:
+            tp_rank = 0
+            if tp_size > 1:
+                import torch.distributed as dist
+
+                tp_rank = dist.get_rank(tp_group) if dist.is_initialized() else 0
+        self.tp_group, self.tp_size, self.tp_rank = tp_group, tp_size, tp_rank
+        V = cfg.vocab_size
+        # (the merged candidate set, tp x 64 per 8192-token chunk of a slice, must fit the merge
+        # kernel's 1024 entries: true for Llama-3's 128256 tokens at tp 2 / 4 / 8)
+        self.vocab_parallel = (bool(vocab_parallel) and tp_size > 1 and V % (32 * tp_size) == 0
+                               and tp_size * -(-(V // tp_size) // 8192) * 64 <= 1024)
+        self.vocab_local = V // tp_size if self.vocab_parallel else V
+        self.vocab_start = tp_rank * self.vocab_local if self.vocab_parallel else 0
         self.hq = cfg.heads // tp_size
         self.hkv = cfg.kv_heads // tp_size
         self.interleaved_mlp = interleaved_mlp  # gate_up rows in 8-row [gate | up] groups (EPI_SWIGLU8)
@@ -100,10 +125,15 @@ class LlamaModel:
 
         self.embed = take("embed").to(self.device)
         self.final_norm = take("final_norm").to(self.device)
-        if "lm_head" in weights:
-            self.lm_head = proj("lm_head")
-        else:
-            self.lm_head = ops.shuffle_weights(self.embed) if self.frag else self.embed
+        head = take("lm_head").to(self.device) if "lm_head" in weights else self.embed
+        if self.vocab_parallel:
+            head = head[self.vocab_start:self.vocab_start + self.vocab_local]
+            pad = (-self.vocab_local) % self.VOCAB_PAD if self.frag else 0
+            if pad:
+                head = torch.cat([head, head.new_zeros((pad, head.shape[1]))])
+            head = head.contiguous()
+        self.lm_head = ops.shuffle_weights(head) if self.frag else head
+        del head
         self.layers = []
         for i in range(cfg.layers):
             self.layers.append(DecoderLayer(take(f"l{i}.attn_norm").to(self.device), proj(f"l{i}.qkv_w"),
@@ -115,6 +145,21 @@ class LlamaModel:
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
+
+    def full_logits(self, local: torch.Tensor) -> torch.Tensor:
+        """All-gather the vocab-parallel slices of every TP rank -> [n, V] (the CPU sampling path
+        and tests; the GPU path gathers candidates instead)."""
+        if not self.vocab_parallel:
+            return local
+        import torch.distributed as dist
+
+        src = local[:, :self.vocab_local].contiguous()
+        staged = src.is_cuda and dist.get_backend(self.tp_group) != "nccl"  # gloo rehearsals on one GPU
+        if staged:
+            src = src.cpu()
+        parts = [torch.empty_like(src) for _ in range(self.tp_size)]
+        dist.all_gather(parts, src, group=self.tp_group)
+        return torch.cat(parts, 1).to(local.device)
 
     def _fragment_ok(self, weights: dict) -> bool:
         keys = ["lm_head" if "lm_head" in weights else "embed"] + [
@@ -305,7 +350,8 @@ class LlamaModel:
     def logits(self, h: torch.Tensor) -> torch.Tensor:
         """[n, H] -> [n, V] logits (bf16; the sampler reads bf16 or fp32).  Up to 256 rows (decode
         steps, prefill last tokens) stream the fragment-layout LM head through ``stream_gemm``;
-        larger batches run the MFMA GEMM on the same copy."""
+        larger batches run the MFMA GEMM on the same copy.  Vocab-parallel: [n, padded slice] with
+        the first ``vocab_local`` columns valid (tokens ``vocab_start`` ...)."""
         if not h.is_cuda:
             return ops.linear(h, self.lm_head)
         return self._proj(h, self.lm_head, h.shape[0] <= self.STREAM_MAX_M, False, name="lm_head")

@@ -641,22 +641,64 @@ def sample_tokens(logits, temperature, top_k, top_p, seed: int, counters, genera
     return out
 
 
-def mask_logits(logits, mask, row_flags):
+def mask_logits(logits, mask, row_flags, vocab: int | None = None, word_offset: int = 0):
     """In place: logits[r, t] = -inf where bit t of ``mask[r]`` (int32 words, bit t % 32 of word
     t // 32) is clear, for the rows whose ``row_flags[r]`` (int32) is non-zero (JSON-constrained
-    decoding).  Returns ``logits``."""
-    rows, vocab = logits.shape
-    expect(mask.dtype == torch.int32 and mask.is_contiguous() and mask.shape[0] >= rows and mask.shape[1] * 32 >= vocab,
-           "mask: int32 [rows, ceil(vocab / 32)]")
+    decoding).  Vocab-parallel slices: the first ``vocab`` columns of ``logits`` are tokens
+    32 * ``word_offset`` ... (mask words ``word_offset`` ...).  Returns ``logits``."""
+    rows = logits.shape[0]
+    vocab = logits.shape[1] if vocab is None else int(vocab)
+    words = -(-vocab // 32)
+    expect(mask.dtype == torch.int32 and mask.is_contiguous() and mask.shape[0] >= rows
+           and mask.shape[1] >= word_offset + words, "mask: int32 [rows, >= ceil(vocab / 32) words past the offset]")
     if not logits.is_cuda:
-        bits = (mask[:rows].view(torch.int32).unsqueeze(-1) >> torch.arange(32, dtype=torch.int32)) & 1
+        m = mask[:rows, word_offset:word_offset + words]
+        bits = (m.view(torch.int32).unsqueeze(-1) >> torch.arange(32, dtype=torch.int32)) & 1
         allow = bits.reshape(rows, -1)[:, :vocab].bool() | (row_flags[:rows] == 0).unsqueeze(1)
-        return logits.masked_fill_(~allow, float("-inf"))
+        logits[:, :vocab].masked_fill_(~allow, float("-inf"))
+        return logits
     expect(logits.stride(-1) == 1 and logits.dtype in (torch.float32, torch.bfloat16), "logits: fp32/bf16 rows")
     _i32(row_flags)
-    native().mask_logits(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab, ptr(mask),
-                         mask.shape[1], ptr(row_flags), stream(logits))
+    native().mask_logits(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, vocab,
+                         ptr(mask) + 4 * int(word_offset), words, ptr(row_flags), stream(logits), mask.stride(0))
     return logits
+
+
+def sample_candidates(logits, vocab: int, index_base: int = 0, out=None):
+    """Stage 1 of vocab-parallel sampling: each 8192-token chunk's top-64 of the first ``vocab``
+    columns of ``logits`` as (order-preserving uint32 key, token id + ``index_base``) -> int32
+    [2, rows, ncand] (keys, then ids).  The TP ranks all-gather these and ``sample_merge`` draws
+    from the union (GPU only)."""
+    expect(logits.is_cuda and logits.stride(-1) == 1 and logits.dtype in (torch.float32, torch.bfloat16),
+           "logits: CUDA fp32/bf16 rows")
+    rows = logits.shape[0]
+    ncand = sample_candidates_per_row(vocab)
+    if out is None:
+        out = torch.empty((2, rows, ncand), dtype=torch.int32, device=logits.device)
+    # (a row slice of a larger [2, R, ncand] buffer is fine: each half is rows x ncand contiguous)
+    expect(out.dtype == torch.int32 and tuple(out.shape) == (2, rows, ncand) and out.stride(2) == 1
+           and out.stride(1) == ncand, "candidates: int32 [2, rows, ncand] with contiguous halves")
+    native().sample_candidates(ptr(logits), int(logits.dtype == torch.float32), logits.stride(0), rows, int(vocab),
+                               int(index_base), ptr(out[0]), ptr(out[1]), ncand, stream(logits))
+    return out
+
+
+def sample_candidates_per_row(vocab: int) -> int:
+    return -(-int(vocab) // _CHUNK) * SAMPLE_FAST_MAX_K
+
+
+def sample_merge(cands, temperature, top_k, top_p, seed: int, counters, vocab: int, out=None):
+    """Stage 2 of vocab-parallel sampling: ``cands`` int32 [2, rows, n] (every rank's
+    ``sample_candidates`` side by side along n, n <= 1024) -> sorted top-k -> HF top-p ->
+    multinomial with the per-row counter RNG (advanced in-kernel): the replicated head's draw."""
+    two, rows, n = cands.shape
+    expect(two == 2 and n <= 1024 and cands.dtype == torch.int32 and cands.is_contiguous(),
+           "candidates: contiguous int32 [2, rows, <= 1024]")
+    out = torch.empty((rows,), dtype=torch.int32, device=cands.device) if out is None else out
+    _i32(top_k)
+    native().sample_merge(ptr(cands[0]), ptr(cands[1]), n, rows, int(vocab), ptr(temperature), ptr(top_k), ptr(top_p),
+                          int(seed) & ((1 << 64) - 1), ptr(counters), ptr(out), stream(cands))
+    return out
 
 
 def topk_rows(scores, k, index_base=0, want_global=False):

@@ -554,6 +554,33 @@ def test_sampling_distribution(fast):
     assert int(tok.max()) <= 1
 
 
+@pytest.mark.parametrize("tp", [2, 4, 8])
+@pytest.mark.parametrize("temp_v", [0.0, 1.0])
+def test_vocab_parallel_sampling_draws_the_replicated_token(tp, temp_v):
+    """with the LM head split by vocabulary over tp ranks, each slice's chunk
+    top-64 (``sample_candidates``, ids offset by the slice start) merged by ``sample_merge`` draws
+    exactly the token the replicated head's two-stage sampler draws from the full logits, with the
+    same counters (top-k 50 -> top-p 0.95 -> multinomial, and greedy)."""
+    V, R = 128256, 96
+    g = torch.Generator(device=DEV).manual_seed(tp)
+    logits = (torch.randn(R, V, device=DEV, generator=g) * 3).to(torch.bfloat16)
+    logits[5, 1000:1100] = 9.0  # ties across the top-k boundary, inside one slice
+    temp = torch.full((R,), temp_v, device=DEV)
+    topk = torch.full((R,), 50, dtype=torch.int32, device=DEV)
+    topp = torch.full((R,), 0.95, device=DEV)
+    c1 = torch.arange(R, dtype=torch.int64, device=DEV) * 3
+    c2 = c1.clone()
+    ref = ops.sample_tokens(logits, temp, topk, topp, 99, c1, fast=True)
+    Vs = V // tp
+    parts = [ops.sample_candidates(logits[:, r * Vs:(r + 1) * Vs].contiguous(), Vs, r * Vs) for r in range(tp)]
+    allc = torch.stack(parts, 2).reshape(2, R, -1).contiguous()  # what the all-gather assembles
+    got = ops.sample_merge(allc, temp, topk, topp, 99, c2, V)
+    assert torch.equal(got, ref)
+    assert torch.equal(c1, c2)  # counters advanced once per row either way
+    if temp_v == 0.0:
+        assert torch.equal(got.long(), logits.float().argmax(-1))
+
+
 @pytest.mark.parametrize("nq", [1, 7, 20, 37, 300])
 @pytest.mark.parametrize("groups", [False, True])
 def test_index_threshold_search_matches_full_scan(groups, nq):

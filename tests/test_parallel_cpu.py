@@ -63,12 +63,15 @@ def _tp_body(info, out_path, model_name):
                     block_tables=torch.arange(4, dtype=torch.int32)[None], ctx_lens=torch.tensor([T], dtype=torch.int32),
                     cu_q=torch.tensor([0, T], dtype=torch.int32), max_q=T)
     h = model.forward(ids, meta, kv)
+    local = model.logits(h)
+    lg = model.full_logits(local)  # vocab-parallel head: every rank holds V / W of the rows
     if info.rank == 0:
         ref_model = LlamaModel(cfg, full, "cpu")
         kv2 = KVCache(cfg.layers, 4, cfg.kv_heads, 64, cfg.head_dim, "cpu", dtype=torch.float32)
         ref = ref_model.forward(ids, meta, kv2)
-        lg_err = (model.logits(h) - ref_model.logits(ref)).abs().max().item()
-        torch.save({"err": (h - ref).abs().max().item(), "logits_err": lg_err}, out_path)
+        lg_err = (lg - ref_model.logits(ref)).abs().max().item()
+        torch.save({"err": (h - ref).abs().max().item(), "logits_err": lg_err, "vp": model.vocab_parallel,
+                    "head_rows": model.lm_head.shape[0], "local_cols": local.shape[1]}, out_path)
 
 
 @pytest.mark.parametrize("world,model_name", TP_CASES)
@@ -77,6 +80,10 @@ def test_tensor_parallel_forward_matches_full_model(tmp_path, world, model_name)
     _run(_tp_body, out, model_name, world=world)
     res = torch.load(out, weights_only=True)
     assert res["err"] < 1e-4 and res["logits_err"] < 1e-4
+    from django_assistant_bot_amd.models.configs import decoder_config
+
+    V = decoder_config(model_name).vocab_size
+    assert res["vp"] and res["head_rows"] == V // world and res["local_cols"] == V // world
 
 
 def _index_body(info, out_path):

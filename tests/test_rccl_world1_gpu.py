@@ -136,7 +136,7 @@ def test_world1_rccl_group_runs_every_collective_branch(tmp_path):
     assert res["max"] == 3.5 and res["gather"] == [2.25] and res["bcast"] == 7
     assert res["comm_device"].startswith("cuda") and res["len"] == 30000
     assert res["collectives"] == 3  # query block + remainder all_gather, all_to_all of the partials
-    assert res["search_ids_equal"] and res["search_sims_err"] == 0.0
+    assert res["search_ids_equal"] and res["search_sims_err"] < 1e-4  # (scores of a 20-query vs a gathered batch)
     assert res["replicated_ids_equal"] and res["merge_bytes"] > 0
     assert res["node_grouped"] and res["node_commands"] > 0
     assert res["node_embed_err"] < 1e-3

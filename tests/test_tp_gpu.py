@@ -1,7 +1,8 @@
 """Tensor-parallel generation on the GPU path: W = 2 / 4 / 8 ranks of ``LLMEngine``
 share the box's one GPU (gloo default group; one-shot IPC all-reduce for the TP partial sums,
-captured inside the HIP-graph decode; split-K decode GEMMs with bf16 partial sums; sampled tokens
-broadcast from TP rank 0), at the Llama-3-70B head layout (64 query / 8 KV heads: at TP 4 each rank
+captured inside the HIP-graph decode; split-K decode GEMMs with bf16 partial sums; the LM head split
+by vocabulary, each rank's sampling candidates all-gathered and merged identically on every rank),
+at the Llama-3-70B head layout (64 query / 8 KV heads: at TP 4 each rank
 holds 16 query and 2 KV heads, at TP 8 -- the degree BASELINE config 5 names -- 8 and 1).
 
 Parity with TP = 1: the TP ranks' greedy tokens are checked against a TP = 1 model of the full
@@ -67,6 +68,9 @@ def _body(rank, world, layout, port, out_path):
                         max_batch=8, block_size=64, num_blocks=96, max_prefill_tokens=256, tp_group=group,
                         tp_size=world, tp_rank=tp_rank)
         assert eng.model.custom_ar is not None and eng.model.frag
+        # vocab-parallel LM head: this rank's V / tp rows (+ zero pad rows)
+        assert eng.vp and eng.model.vocab_local == cfg.vocab_size // world
+        assert eng.model.lm_head.shape[0] == -(-cfg.vocab_size // world // 384) * 384
         sp = SamplingParams(max_new_tokens=12, do_sample=False, temperature=0.0, ignore_eos=True)
         outs = eng.generate(_prompts(), sp)  # 300 > 256: a chunked prefill; decode via graphs
         eng.model.custom_ar.check_error()
