@@ -57,7 +57,13 @@ def main():
     steps = [rows[starts[i]:starts[i + 1]] for i in range(len(starts) - 1)]
     lines = [f"# per-step kernel breakdown: {prefix}", ""]
     dec = [s for s in steps if any("paged_decode" in n for _, _, n in s) and not any(_is_prefill_attn(n) for _, _, n in s)]
-    pre = [s for s in steps if any(_is_prefill_attn(n) for _, _, n in s)]
+    mixed = [s for s in steps if any(_is_prefill_attn(n) for _, _, n in s) and any("paged_decode" in n for _, _, n in s)]
+    pre = [s for s in steps if any(_is_prefill_attn(n) for _, _, n in s) and s not in mixed]
+    if mixed:
+        spans = sorted((s[-1][1] - s[0][0]) / 1e6 for s in mixed)
+        med = min(mixed, key=lambda s: abs((s[-1][1] - s[0][0]) / 1e6 - spans[len(spans) // 2]))
+        lines += window_table(med, "median mixed step (prompt chunks + decode rows in one forward)")
+        lines += [f"mixed steps: {len(mixed)}, median span {spans[len(spans) // 2]:.3f} ms", ""]
     if pre:
         big = max(pre, key=lambda s: s[-1][1] - s[0][0])
         lines += window_table(big, "largest prefill step")
