@@ -55,6 +55,16 @@ ARMS = {
     "spart128": {"_spart": 128},
     "part640": {"_part": 640},              # ~2 equal partitions of a ~1.2k context
     "part768": {"_part": 768},
+    # batches <= 16: the consumer-side RMSNorm (``_layer_small``) instead of the norm launches
+    "normfused": {"_fuse": True},
+    # ... with the o / down residual producers at 32 weight rows per workgroup (cfg 33)
+    "res32": {"_fuse": True, "_res_cfg": 33},
+    # batches <= 16: Infinity-Cache warm-up of the next o / gate_up weights riding on the attention
+    "warm32": {"_warm": 32},
+    "warm64": {"_warm": 64},
+    "warm96": {"_warm": 96},
+    "warm160": {"_warm": 160},
+    "warm96b128": {"_warm": 96, "_warm_blocks": 128},
 }
 
 
@@ -118,6 +128,10 @@ def main():
             eng.part_size = spec.get("_spart", base_spart)
             eng.model.STREAM_CFG_M16 = spec.get("_m16", type(eng.model).STREAM_CFG_M16)
             eng.model.STREAM_CFG_M32 = spec.get("_m32", type(eng.model).STREAM_CFG_M32)
+            eng.model.small_norm_fused = spec.get("_fuse", False)
+            eng.model.l3_warm_mb = spec.get("_warm", type(eng.model).l3_warm_mb)
+            eng.model.l3_warm_blocks = spec.get("_warm_blocks", type(eng.model).l3_warm_blocks)
+            eng.model.STREAM_CFG_RES16 = spec.get("_res_cfg", type(eng.model).STREAM_CFG_RES16)
             eng._graphs.clear()
             for _ in range(4):
                 eng.step()

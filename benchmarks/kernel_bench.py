@@ -147,6 +147,20 @@ def attn_suite():
     t = timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True))
     flop = 4.0 * B * Hq * T * T * D / 2
     emit(op="flash-prefill-causal", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    # A/B of the software-pipelined V reads (DAB_FLASH_VPIPE), interleaved rounds in this process
+    ref_out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True)
+    ab = {"base": [], "vpipe": []}
+    for _ in range(5):
+        for arm in ab:
+            os.environ["DAB_FLASH_VPIPE"] = "1" if arm == "vpipe" else "0"
+            ab[arm].append(timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True)))
+    os.environ["DAB_FLASH_VPIPE"] = "1"
+    err = (ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True).float() - ref_out.float()).abs().max()
+    os.environ.pop("DAB_FLASH_VPIPE")
+    for arm, ts in ab.items():
+        tm = sorted(ts)[len(ts) // 2]
+        emit(op=f"flash-prefill-causal-{arm}", B=B, T=T, us=round(tm * 1e6, 1), tflops=round(flop / tm / 1e12, 1),
+             max_diff_vs_base=round(float(err), 5) if arm == "vpipe" else 0.0)
     # the model's prefill form: q read from the qkv projection (row stride (Hq + 2 Hkv) D), without
     # and with RoPE applied on load
     qkv = torch.randn(B * T, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)

@@ -131,15 +131,18 @@ PYBIND11_MODULE(_native, m) {
   m.def("destroy_stream", [](u s) { check(hipStreamDestroy(ST(s)), "hipStreamDestroy"); });
   m.def("paged_decode_attention", [](u q, u kc, u vc, u bt, int max_blocks, int bs, u ctx, u out, u po, u pm, u pl,
                                      u cnt, int batch, int Hq, int Hkv, int D, int part_size, int max_parts,
-                                     float scale, u s, u order) {
+                                     float scale, u s, u order, u w0, long w0_bytes, u w1, long w1_bytes,
+                                     int w_blocks) {
+    dab::L3Warm warm{{(const char*)w0, (const char*)w1}, {w0_bytes, w1_bytes}, w_blocks};
     check(dab::paged_decode_attention(CVP(q), CVP(kc), CVP(vc), (const int*)bt, max_blocks, bs, (const int*)ctx, VP(out),
                                       (float*)po, (float*)pm, (float*)pl, (int*)cnt, batch, Hq, Hkv, D, part_size,
-                                      max_parts, scale, ST(s), (const int*)order),
+                                      max_parts, scale, ST(s), (const int*)order, &warm),
           "paged_decode_attention");
   }, py::arg("q"), py::arg("kc"), py::arg("vc"), py::arg("bt"), py::arg("max_blocks"), py::arg("bs"), py::arg("ctx"),
      py::arg("out"), py::arg("po"), py::arg("pm"), py::arg("pl"), py::arg("cnt"), py::arg("batch"), py::arg("Hq"),
      py::arg("Hkv"), py::arg("D"), py::arg("part_size"), py::arg("max_parts"), py::arg("scale"), py::arg("s"),
-     py::arg("order") = 0);
+     py::arg("order") = 0, py::arg("w0") = 0, py::arg("w0_bytes") = 0, py::arg("w1") = 0, py::arg("w1_bytes") = 0,
+     py::arg("w_blocks") = 0);
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
                       int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s, int b_rows) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
@@ -205,11 +208,13 @@ PYBIND11_MODULE(_native, m) {
      py::arg("q_group"), py::arg("thr"), py::arg("cnt"), py::arg("cand_val"), py::arg("cand_idx"), py::arg("cap"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("stream_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
-                          int S, int epilogue, u s, int nt, int cfg) {
+                          int S, int epilogue, u s, int nt, int cfg, float norm_eps) {
     check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
-                           cfg),
+                           cfg, norm_eps),
           "stream_gemm");
-  });
+  }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
+     py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
+     py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f);
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
   m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);

@@ -347,11 +347,44 @@ __device__ __forceinline__ void ds_tr16_x8(const unsigned (&a)[8], u32x2 (&r)[8]
       : "memory");
 }
 
+// The same 8 transposed reads without the wait (VPIPE): the next k-step's V fragments are requested
+// before the current k-step's MFMAs and retired by a counted lgkmcnt (lgkm_wait) right before their
+// use, so the LDS latency hides under the MFMAs instead of stalling the wave four times per tile.
+template <int OFF>
+__device__ __forceinline__ void ds_tr16_issue(const unsigned (&a)[8], u32x2 (&r)[8]) {
+  asm volatile(
+      "ds_read_b64_tr_b16 %0, %8 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %1, %9 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %2, %10 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %3, %11 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %4, %12 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %5, %13 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %6, %14 offset:%16\n\t"
+      "ds_read_b64_tr_b16 %7, %15 offset:%16"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7])
+      : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(a[4]), "v"(a[5]), "v"(a[6]), "v"(a[7]), "i"(OFF)
+      : "memory");
+}
+
+// s_waitcnt lgkmcnt(N) + a scheduling fence: hipcc would otherwise hoist the register-only MFMAs
+// that consume the asm reads above the wait (cdna_hip_programming.md rule 18)
+template <int N>
+__device__ __forceinline__ void lgkm_wait() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// the value of lane l ^ 32 (v_permlane32_swap: VALU, no LDS round trip on the lgkm counter)
+__device__ __forceinline__ float xor32(float v) {
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? sw[0] : sw[1]);
+}
+
 __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <bool CAUSAL>
+template <bool CAUSAL, bool VPIPE = false>
 __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
   constexpr int D = 128, KT = 64, QB = 128;
   constexpr int TILE = KT * D * 2;  // 16 KB
@@ -534,10 +567,13 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
         if (key + 32 >= kv_len || (CAUSAL && key + 32 > q_pos)) s1[r] = kNegInf;
       }
     }
+    // VPIPE: the first k-step's V fragments are requested now and land under the softmax
+    u32x2 trA[8], trB[8];
+    if constexpr (VPIPE) ds_tr16_issue<B0>(vadr, trA);
     float mx = kNegInf;
 #pragma unroll
     for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = fmaxf(mx, VPIPE ? xor32(mx) : __shfl_xor(mx, 32, 64));
     // Deferred rescale (cdna_hip_programming.md T13): while no query of the wave sees its maximum
     // grow by more than kDeferLog2 (log2 units) the running maximum stays, P reaches at most
     // 2^kDeferLog2 (exact in bf16 up to the usual 8-bit mantissa) and the O / l rescale is skipped;
@@ -567,14 +603,29 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
     // 32 kb + 16 ss + 8 (j >> 2) + 4 hi + (j & 3); the V^T A fragment takes its elements from the
     // same keys: two transposed reads of 4 keys at 32 kb + 16 ss + 4 hi (+ 8).
     static_for<0, 4>([&](auto KS_) DAB_ALWAYS_INLINE {
-      constexpr int kb = decltype(KS_)::value >> 1, ss = decltype(KS_)::value & 1;
+      constexpr int ks = decltype(KS_)::value;
+      constexpr int kb = ks >> 1, ss = ks & 1;
       const f32x16& sv = kb ? s1 : s0;
       u32x4 pu;
 #pragma unroll
       for (int e = 0; e < 4; ++e) pu[e] = pack2bf(sv[8 * ss + 2 * e], sv[8 * ss + 2 * e + 1]);
       const bf16x8 pf = __builtin_bit_cast(bf16x8, pu);
       u32x2 tr[8];
-      ds_tr16_x8<B0 + kb * 8192 + ss * 4096>(vadr, tr);
+      if constexpr (VPIPE) {
+        // k-step ks + 1's reads go out behind k-step ks's, then ks's are retired (in-order counter)
+        u32x2(&cur)[8] = (ks & 1) ? trB : trA;
+        u32x2(&nxt)[8] = (ks & 1) ? trA : trB;
+        if constexpr (ks < 3) {
+          ds_tr16_issue<B0 + ((ks + 1) >> 1) * 8192 + ((ks + 1) & 1) * 4096>(vadr, nxt);
+          lgkm_wait<8>();
+        } else {
+          lgkm_wait<0>();
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) tr[i] = cur[i];
+      } else {
+        ds_tr16_x8<B0 + kb * 8192 + ss * 4096>(vadr, tr);
+      }
 #pragma unroll
       for (int db = 0; db < 4; ++db) {
         u32x4 u;
@@ -657,6 +708,7 @@ struct DecodeParams {
   const int* order;  // optional [B] sequence visit order (longest first: see paged_decode_attention)
   int Hq, Hkv, part_size, max_parts;
   float scale_log2;
+  L3Warm warm;  // optional: the next projections' weights, warmed into L3 by appended workgroups
 };
 
 // DMA (D = 128): each wave streams its 32-key K / V sub-tiles straight into its LDS slot by LDS-DMA
@@ -673,6 +725,13 @@ struct DecodeParams {
 template <int D, bool KV_NT, bool DMA = false, int NSLOT = 1>
 __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(DecodeParams p, int total_items) {
   static_assert(NSLOT == 1 || (NSLOT == 2 && DMA), "two slots: DMA staging only");
+  // appended workgroups (small batches leave most CUs idle during this latency-bound launch): warm
+  // the following projections' weights into the Infinity Cache and leave
+  const int attn_blocks = gridDim.x - p.warm.blocks;
+  if ((int)blockIdx.x >= attn_blocks) {
+    l3_warm(p.warm, blockIdx.x - attn_blocks);
+    return;
+  }
   constexpr int KT = 32;
   constexpr int NKK = D / 32;
   constexpr int NTD = D / 16;
@@ -708,7 +767,7 @@ __global__ __launch_bounds__(256, NSLOT == 1 ? 2 : 1) void paged_decode_kernel(D
   for (int off = 32; off; off >>= 1) maxc = max(maxc, __shfl_xor(maxc, off));
   maxc = __builtin_amdgcn_readfirstlane(maxc);
   const int live_items = min(p.max_parts, (maxc + p.part_size - 1) / p.part_size) * BH;
-  for (int item = blockIdx.x; item < live_items; item += gridDim.x) {
+  for (int item = blockIdx.x; item < live_items; item += attn_blocks) {
     const int part = item / BH;
     const int bh = item - part * BH;
     const int hk = bh % p.Hkv, b = p.order ? p.order[bh / p.Hkv] : bh / p.Hkv;
@@ -1011,7 +1070,13 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // Llama prefill (D = 128 over the paged cache): the 32x32 kernel below
   if (D == 128 && paged && block_size % 64 == 0) {
     dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
-    if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
+    // software-pipelined V reads by default (3% faster, bit-identical: profiles/attn_vpipe_r5.md);
+    // DAB_FLASH_VPIPE=0 selects the unpipelined kernel (A/B: benchmarks/kernel_bench.py attn)
+    const char* vp = std::getenv("DAB_FLASH_VPIPE");
+    const bool vpipe = !(vp && vp[0] == '0');
+    if (causal && vpipe) hipLaunchKernelGGL((flash_d128_kernel<true, true>), g32, dim3(256), 0, s, prm);
+    else if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
+    else if (vpipe) hipLaunchKernelGGL((flash_d128_kernel<false, true>), g32, dim3(256), 0, s, prm);
     else hipLaunchKernelGGL((flash_d128_kernel<false>), g32, dim3(256), 0, s, prm);
     return hipGetLastError();
   }
@@ -1061,7 +1126,8 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
 int paged_decode_attention(const void* q, const void* k_cache, const void* v_cache, const int* block_tables,
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
-                           int part_size, int max_parts, float scale, hipStream_t s, const int* order) {
+                           int part_size, int max_parts, float scale, hipStream_t s, const int* order,
+                           const L3Warm* warm) {
   if (batch <= 0) return 0;
   if (Hq % Hkv || Hq / Hkv > 16 || part_size % 128 || max_parts < 1 || block_size % 32) return hipErrorInvalidValue;
   if (max_parts > 1 && !counters) return hipErrorInvalidValue;
@@ -1085,8 +1151,12 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
   prm.part_size = part_size;
   prm.max_parts = max_parts;
   prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.warm = warm ? *warm : L3Warm{{nullptr, nullptr}, {0, 0}, 0};
+  if (prm.warm.blocks < 0 || prm.warm.blocks > 1024 || ((prm.warm.bytes[0] | prm.warm.bytes[1]) & 15) ||
+      (prm.warm.blocks && prm.warm.bytes[0] + prm.warm.bytes[1] <= 0))
+    return hipErrorInvalidValue;
   const int total_items = max_parts * Hkv * batch;
-  dim3 grid(total_items < 2048 ? total_items : 2048);
+  dim3 grid((total_items < 2048 ? total_items : 2048) + prm.warm.blocks);
   // K/V are read exactly once per step: non-temporal loads (aux = 2) -- in the Llama-3-8B decode step
   // at batch 128 this took the attention from 127 to 111 us per layer (5.1 -> 5.8 TB/s;
   // profiles/decode_round2.md).  D = 128 stages K / V by LDS-DMA (100.7 vs 102.6 us isolated, same

@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "launchers.h"  // L3Warm
+
 namespace dab {
 
 typedef uint16_t bf16;
@@ -123,6 +125,36 @@ __device__ __forceinline__ bf16x4 ds_read_tr16(const void* lds_ptr) {
 }
 
 __device__ __forceinline__ int div_up(int a, int b) { return (a + b - 1) / b; }
+
+// Infinity-Cache (L3) warm-up of up to two byte ranges, read as one concatenated range: workgroup
+// ``part`` of ``nparts`` reads its share with plain (allocating) 16-B loads, 8 per lane in flight,
+// so a later kernel's read of the same bytes is served on-die (MI355X_MICROARCH.md § Infinity
+// Cache: 256 MiB, resident while the bytes between two uses fit).  Nothing is written: the loaded
+// words feed an empty asm statement, which keeps the loads.  Ranges must be 16-B multiples.
+__device__ __forceinline__ void l3_warm_range(const char* base, long lo, long hi) {
+  const u32x4* p = reinterpret_cast<const u32x4*>(base);
+  const long step = blockDim.x;
+  uint32_t acc = 0;
+  for (long i = (lo >> 4) + threadIdx.x; i < (hi >> 4); i += 8 * step) {
+    u32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const long k = i + j * step;
+      v[j] = k < (hi >> 4) ? p[k] : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= v[j].x ^ v[j].w;
+  }
+  asm volatile("" ::"v"(acc));
+}
+
+__device__ __forceinline__ void l3_warm(const L3Warm& w, int part) {
+  const long total = w.bytes[0] + w.bytes[1];
+  const long per = ((total + w.blocks - 1) / w.blocks + 4095) & ~4095L;
+  const long lo = part * per, hi = lo + per < total ? lo + per : total;
+  if (lo < w.bytes[0]) l3_warm_range(w.ptr[0], lo, hi < w.bytes[0] ? hi : w.bytes[0]);
+  if (hi > w.bytes[0]) l3_warm_range(w.ptr[1], (lo > w.bytes[0] ? lo : w.bytes[0]) - w.bytes[0], hi - w.bytes[0]);
+}
 
 // Orderable unsigned key of a float: larger float -> larger key (used by radix selects).
 __device__ __forceinline__ uint32_t float_key(float f) {

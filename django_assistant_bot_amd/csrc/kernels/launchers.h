@@ -13,6 +13,14 @@ namespace dab {
 
 inline int div_up_host(int a, int b) { return (a + b - 1) / b; }
 
+// Optional Infinity-Cache warm-up riding on a latency-bound launch (common.h l3_warm): up to two byte
+// ranges (16-B multiples) read by ``blocks`` workgroups appended to the kernel's grid.
+struct L3Warm {
+  const char* ptr[2];
+  long bytes[2];
+  int blocks;  // 0: off
+};
+
 // norm.hip
 int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const void* w, int rows, int cols, float eps,
             hipStream_t s);
@@ -44,7 +52,7 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
                            int max_blocks, int block_size, const int* ctx_lens, void* out, float* part_o,
                            float* part_m, float* part_l, int* counters, int batch, int Hq, int Hkv, int D,
                            int part_size, int max_parts, float scale, hipStream_t s,
-                           const int* order = nullptr);
+                           const int* order = nullptr, const L3Warm* warm = nullptr);
 
 // gemm.hip
 // b_rows > 0: B is an ops.shuffle_weights copy of b_rows (>= N) rows; epilogue 4 = SwiGLU over 8-row
@@ -73,7 +81,7 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
 // stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
-                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg);
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps = 0.f);
 int stream_gemm_bn(int cfg);
 // fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
 int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,

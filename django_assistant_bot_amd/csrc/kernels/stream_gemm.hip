@@ -43,6 +43,13 @@ struct StreamParams {
   long ldr;
   int M, N, K, S, kc;
   int epi;       // 0 none, 2 swiglu (16-row gate | up groups), 4 swiglu (8-row groups), 8 candidates
+  // RMSNorm in the consumer (small decode batches): X is the raw residual stream
+  // h and the norm gains are folded into W's columns, so RMSNorm(h) W^T = r[m] (h W^T) with
+  // r[m] = rsqrt(mean_k h[m][k]^2 + eps).  The epilogue computes r from the X rows (L2-resident,
+  // all K even for a K-slice) and scales the accumulators before the slab store / SwiGLU: the
+  // separate slab-summing RMSNorm launch disappears (its producer writes h with its residual add).
+  int norm;
+  float norm_eps;
   // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
   // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -98,7 +105,8 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   constexpr int CPW = KW / 32;        // 32-deep MFMA chunks per wave per stage
   constexpr int RED = KG * MP * BNP * 4;
   static_assert(BN <= 256 && BN % 16 == 0, "tile rows");
-  constexpr int SMEM = NB * XBUF > RED ? NB * XBUF : RED;
+  // + per-row sums of squares / scales of the consumer RMSNorm (after the ring / reduction area)
+  constexpr int SMEM = (NB * XBUF > RED ? NB * XBUF : RED) + MP * 4;
   static_assert(CPR >= 16 && CPW >= 1 && KW % 32 == 0, "stage shape");
   static_assert(NB >= 2 && (NB - 2) * GPL <= 63 && GPS % NL == 0, "loader vmcnt range");
   static_assert(NWC % KG == 0, "k groups");
@@ -250,16 +258,41 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   }
 
   // ---------------------------------------------------------------- epilogue (all 5 waves)
+  constexpr int NT = 64 * (NWC + NL);
+  float* rsq = reinterpret_cast<float*>(smem + (NB * XBUF > RED ? NB * XBUF : RED));
+  if (p.norm) {  // (uniform) sums of squares of the X rows, accumulated into LDS by every wave
+    for (int m = tid; m < MP; m += NT) rsq[m] = 0.f;
+  }
   wait_lgkm0();
   __builtin_amdgcn_s_barrier();
+  if (p.norm) {
+    const int vpr = p.K / 8;  // 16-B vectors per row
+    for (int m = 0; m < p.M; ++m) {
+      const bf16* xr = p.X + (size_t)m * p.ldx;
+      float ss = 0.f;
+      for (int v = tid; v < vpr; v += NT) {
+        float f[8];
+        unpack8(*reinterpret_cast<const u32x4*>(xr + 8 * v), f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ss = fmaf(f[j], f[j], ss);
+      }
+      ss = wave_sum(ss);
+      if (lane == 0) atomicAdd(rsq + m, ss);
+    }
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    for (int m = tid; m < p.M; m += NT) rsq[m] = rsqrtf(rsq[m] / (float)p.K + p.norm_eps);
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+  }
   auto tile4 = [&](int m, int c4) DAB_INLINE {
     const int col = c4 ^ (4 * (m & 15));
     f32x4 v = *reinterpret_cast<const f32x4*>(red + m * BNP + col);
 #pragma unroll
     for (int q = 1; q < KG; ++q) v += *reinterpret_cast<const f32x4*>(red + (q * MP + m) * BNP + col);
+    if (p.norm) v *= rsq[m];
     return v;
   };
-  constexpr int NT = 64 * (NWC + NL);
   if (p.S > 1) {
     float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
     // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
@@ -381,6 +414,11 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // staging and MFMAs
     {1, 2, 1, 4, 4, 2, true},  // 30: BN 128, 2 loaders
     {2, 2, 1, 4, 4, 2, true},  // 31: M <= 32, BN 128, 2 loaders
+    // M <= 16, whole-K producers of the residual stream (o / down with the residual add, no split-K
+    // slabs, so the consumer can normalise X itself): 16 / 32 weight rows per workgroup, an 8-stage
+    // weight ring per compute wave
+    {1, 1, 1, 4, 8, 1, true, 0, 1},  // 32: BN 16, 1 compute + 1 loader wave
+    {1, 1, 1, 4, 8, 1, true, 0, 2},  // 33: BN 32, 2 compute + 1 loader wave
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
@@ -415,7 +453,7 @@ static void launch_any(int cfg, const StreamParams& p, hipStream_t s, bool nt) {
 }
 
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
-                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg) {
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps) {
   constexpr int KS = 128;
   if (M <= 0 || N <= 0) return 0;
   const int bn = stream_gemm_bn(cfg);
@@ -442,6 +480,11 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   p.S = S;
   p.kc = K / S;
   p.epi = epilogue;
+  // norm_eps > 0: consumer RMSNorm (X = the residual stream h, gains folded into W); not with a
+  // residual add (its output is not a normalised product)
+  p.norm = norm_eps > 0.f;
+  p.norm_eps = norm_eps;
+  if (p.norm && (residual || K % 8 || M > stream_gemm_max_m(cfg))) return hipErrorInvalidValue;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();
 }

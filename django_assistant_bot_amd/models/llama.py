@@ -134,17 +134,35 @@ class LlamaModel:
             head = head.contiguous()
         self.lm_head = ops.shuffle_weights(head) if self.frag else head
         del head
+        # GPU: the attention / MLP RMSNorm gains live in the columns of the projection each norm feeds
+        # (rmsnorm(x) g W^T = rmsnorm(x) (W diag g)^T), the norms themselves run with unit gains.
+        # Small decode batches then normalise inside the consumer GEMM (``_layer_small``); the
+        # prefill / large-batch paths are unchanged apart from where g is applied.
+        self.fold_norms = self.frag
         self.layers = []
         for i in range(cfg.layers):
-            self.layers.append(DecoderLayer(take(f"l{i}.attn_norm").to(self.device), proj(f"l{i}.qkv_w"),
-                                            proj(f"l{i}.o_w"), take(f"l{i}.mlp_norm").to(self.device),
-                                            proj(f"l{i}.gate_up_w"), proj(f"l{i}.down_w")))
+            an = take(f"l{i}.attn_norm").to(self.device)
+            mn = take(f"l{i}.mlp_norm").to(self.device)
+            qkv_w, gu_w = take(f"l{i}.qkv_w").to(self.device), take(f"l{i}.gate_up_w").to(self.device)
+            if self.fold_norms:
+                qkv_w, an = self._fold(qkv_w, an), torch.ones_like(an)
+                gu_w, mn = self._fold(gu_w, mn), torch.ones_like(mn)
+            fmt = ops.shuffle_weights if self.frag else (lambda t: t)
+            self.layers.append(DecoderLayer(an, fmt(qkv_w), proj(f"l{i}.o_w"), mn, fmt(gu_w), proj(f"l{i}.down_w")))
+            del qkv_w, gu_w
         if self.frag and consume:
             torch.cuda.empty_cache()
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
+
+    @staticmethod
+    def _fold(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+        """W diag(g) (unit gains, e.g. random init: W itself)."""
+        if bool(torch.all(g == 1)):
+            return w
+        return (w.float() * g.float()[None, :]).to(w.dtype)
 
     def full_logits(self, local: torch.Tensor) -> torch.Tensor:
         """All-gather the vocab-parallel slices of every TP rank -> [n, V] (the CPU sampling path
@@ -259,10 +277,60 @@ class LlamaModel:
         # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
         # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
         sk = meta.decode and T <= self.STREAM_MAX_M and x.is_cuda
+        if sk and T <= self.SMALL_FUSED_MAX_M and self.small_norm_fused and self.fold_norms and self.tp_size == 1:
+            h = x  # the residual stream itself: no RMSNorm launches (``_layer_small``)
+            for li, L in enumerate(self.layers):
+                h = self._layer_small(li, L, h, meta, kv)
+            return ops.rmsnorm(h, self.final_norm, self.cfg.eps)[0]
         residual = None
         for li, L in enumerate(self.layers):
             x, residual = self._layer(li, L, x, residual, meta, kv, sk)
         return self._final_norm(x, residual)
+
+    # Small decode batches (the interactive case): the residual stream h is the
+    # only activation between layers.  The o / down projections stream their weights without split-K
+    # (16-row tiles fill the chip at M <= 16) and add the residual in their epilogue, so h leaves them
+    # complete; the qkv / gate_up projections read h as X and apply the RMSNorm as a per-row scale in
+    # their epilogue (gains folded into their weights).  The two slab-summing RMSNorm launches per
+    # layer are gone.  Switch: ``small_norm_fused`` (benchmarks/decode_ab.py A/B).  Measured SLOWER
+    # (B=1 3.88 vs 3.65 ms/token, B=8 4.25 vs 3.81 ms/step, profiles/decode_small_r5.md): the whole-K
+    # o / down tiles launch only N/16 workgroups, one per CU, and lose the split-K latency hiding
+    # that the two norm launches cost less than -- so it is off by default.
+    SMALL_FUSED_MAX_M = 16
+    STREAM_CFG_RES16 = 32  # stream_gemm.hip cfg 32: BN 16, whole K
+    small_norm_fused = False
+
+    def _layer_small(self, li: int, L: DecoderLayer, h, meta: AttnMeta, kv: KVCache):
+        cfg, D = self.cfg, self.cfg.head_dim
+        T = h.shape[0]
+        c, s = self._stream_choice("qkv", T, L.qkv_w.shape[0], L.qkv_w.shape[1])
+        qkv = ops.stream_gemm(h, L.qkv_w, splits=s, cfg=c, nt=True, norm_eps=cfg.eps)
+        q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
+        a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
+                             meta.workspace, order=meta.order)
+        h1 = ops.stream_gemm(a.view(T, self.hq * D), L.o_w, residual=h, cfg=self.STREAM_CFG_RES16, nt=True)
+        gc, _ = self._stream_choice("gate_up", T, L.gate_up_w.shape[0], L.gate_up_w.shape[1])
+        act = ops.stream_gemm(h1, L.gate_up_w, epilogue=ops.EPI_SWIGLU8, cfg=gc, nt=True, norm_eps=cfg.eps)
+        return ops.stream_gemm(act, L.down_w, residual=h1, cfg=self.STREAM_CFG_RES16, nt=True)
+
+    # Small decode batches: the paged attention is a chain of dependent memory round trips on a few
+    # dozen CUs (~15 us per layer at batch 1 while HBM idles).  ``l3_warm_mb`` > 0 appends
+    # ``l3_warm_blocks`` workgroups to that launch which read the first MB of the layer's o and
+    # gate_up weights into the Infinity Cache, so those projections stream part of their weights
+    # on-die.  A/B: benchmarks/decode_ab.py arms warm*.
+    L3_WARM_MAX_M = 16
+    l3_warm_mb = 0
+    l3_warm_blocks = 192
+
+    def _warm(self, L: DecoderLayer, T: int, ref):
+        if not self.l3_warm_mb or T > self.L3_WARM_MAX_M or not ref.is_cuda:
+            return None
+        budget = int(self.l3_warm_mb * 2 ** 20) & ~15
+        ob = L.o_w.numel() * L.o_w.element_size()
+        ranges = [(L.o_w, min(ob, budget))]
+        if budget > ob:
+            ranges.append((L.gate_up_w, min(budget - ob, L.gate_up_w.numel() * L.gate_up_w.element_size()) & ~15))
+        return ranges, self.l3_warm_blocks
 
     def _final_norm(self, x, residual):
         if x is None:  # the residual stream holds the last layer's output
@@ -298,7 +366,7 @@ class LlamaModel:
         q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
         if meta.decode:
             a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
-                                 meta.workspace, order=meta.order)
+                                 meta.workspace, order=meta.order, warm=self._warm(L, T, q))
         elif meta.n_decode:
             a = self._mixed_attention(q, kv, li, meta)
         else:

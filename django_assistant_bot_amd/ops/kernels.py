@@ -288,11 +288,15 @@ class DecodeWorkspace:
 
 
 def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, workspace: DecodeWorkspace | None = None,
-                 scale=None, out=None, order=None):
+                 scale=None, out=None, order=None, warm=None):
     """q [B, Hq, D] (one new token per sequence) over the paged caches.  ``order`` (int32 [B], a
     permutation of the batch) is the order the (sequence, kv head) items are dispatched in: longest
     context first balances the two rounds of workgroups every CU runs at RAG batch sizes.  Any
-    permutation is correct: the kernel bounds its partition walk by its own max over ctx_lens."""
+    permutation is correct: the kernel bounds its partition walk by its own max over ctx_lens.
+
+    ``warm`` = ``([(tensor, nbytes), ...up to 2], blocks)``: ``blocks`` workgroups appended to the
+    launch read the first ``nbytes`` of each tensor into the Infinity Cache (the next projections'
+    weights, while the latency-bound attention leaves the CUs idle); the output is unchanged."""
     B, Hq, D = q.shape
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if not q.is_cuda:
@@ -318,9 +322,18 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
     if order is not None:
         _i32(order)
         expect(order.is_cuda and order.numel() >= B, "decode order must hold the batch")
+    wargs = {}
+    if warm is not None and warm[1] > 0:
+        ranges, blocks = warm
+        expect(1 <= len(ranges) <= 2 and 0 < blocks <= 1024, "warm: 1-2 ranges, 1-1024 workgroups")
+        for i, (t, nb) in enumerate(ranges):
+            expect(t.is_cuda and t.is_contiguous() and 0 < nb <= t.numel() * t.element_size() and nb % 16 == 0,
+                   "warm range must be a 16-B multiple inside a contiguous device tensor")
+            wargs[f"w{i}"], wargs[f"w{i}_bytes"] = ptr(t), int(nb)
+        wargs["w_blocks"] = int(blocks)
     native().paged_decode_attention(ptr(q), ptr(k_cache), ptr(v_cache), ptr(block_tables), block_tables.shape[1], bs,
                                     ptr(ctx_lens), ptr(out), ptr(ws_o), ptr(ws_m), ptr(ws_l), ptr(ws_c), B, Hq, Hkv,
-                                    D, int(part_size), int(max_parts), float(scale), stream(q), ptr(order))
+                                    D, int(part_size), int(max_parts), float(scale), stream(q), ptr(order), **wargs)
     return out
 
 
@@ -486,9 +499,21 @@ def shuffle_rows_into(dst: torch.Tensor, rows: torch.Tensor, vals: torch.Tensor)
     v5[rows // 16, :, :, rows % 16, :] = vals.to(dst.dtype).reshape(-1, K // 32, 4, 8)
 
 
-def _ref_stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None):
+def _ref_stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, norm_eps=0.0):
     """CPU semantics of ``stream_gemm`` (row-major ``w``): bf16 [M, N] / SwiGLU / fp32 slabs
-    [S, M, N] whose sum is the product (slab 0 holds it, the others are zero)."""
+    [S, M, N] whose sum is the product (slab 0 holds it, the others are zero).  ``norm_eps`` > 0:
+    the product of the RMS-normalised rows of x (gains folded into w) before the epilogue."""
+    if norm_eps > 0:
+        xf = x.float()
+        r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + norm_eps)
+        y = xf @ w.float().t() * r
+        if epilogue in (EPI_SWIGLU, EPI_SWIGLU8):
+            grp = 16 if epilogue == EPI_SWIGLU else 8
+            v = y.view(y.shape[0], -1, 2, grp)
+            y = (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(y.shape[0], -1)
+        if splits > 1:
+            return torch.cat([y[None], torch.zeros((splits - 1,) + tuple(y.shape))], 0)
+        return y.to(torch.bfloat16)
     y = ref.gemm_bt(x, w, None, None, epilogue, out_f32=splits > 1)
     if splits > 1:
         return torch.cat([y[None], torch.zeros((splits - 1,) + tuple(y.shape), dtype=y.dtype)], 0)
@@ -518,15 +543,18 @@ def unshuffle_weights(w: torch.Tensor) -> torch.Tensor:
 
 
 
-def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0):
+def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0, norm_eps: float = 0.0):
     """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): bf16
     [M, N] (optional residual add), SwiGLU [M, N/2] over 16- / 8-row interleaved [gate | up] rows, or
     fp32 K-slice slabs [S, M, N] (their sum is the product; consumers sum them in their prologue or
     ``slab_reduce`` does).  ``cfg`` picks the tile / ring configuration
     (``native().stream_gemm_bn(cfg)`` weight rows per workgroup); ``nt`` streams the weights with
-    non-temporal loads.  On the CPU ``w`` is row-major."""
+    non-temporal loads.  ``norm_eps`` > 0: x is an un-normalised residual stream and w carries the
+    RMSNorm gains in its columns; the kernel scales row m by rsqrt(mean(x[m]^2) + eps) (the
+    consumer-side RMSNorm of small decode batches).  On the CPU ``w`` is row-major."""
     if not x.is_cuda:
-        return _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual)
+        return _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual, norm_eps=norm_eps)
+    expect(norm_eps <= 0 or residual is None, "the consumer RMSNorm takes no residual add")
     expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
     expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
     M, K = x.shape
@@ -557,7 +585,7 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
         ldo = out.stride(0)
     native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
                          residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
-                         int(bool(nt)), int(cfg))
+                         int(bool(nt)), int(cfg), float(norm_eps))
     return out
 
 

@@ -423,7 +423,7 @@ def test_gemm_swiglu():
 
 
 @pytest.mark.parametrize("cfg,M,N,K,S", _stream_cases(
-    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30, 31], [1, 16, 30, 37, 64, 100, 128, 200, 256],
+    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30, 31, 32, 33], [1, 16, 30, 37, 64, 100, 128, 200, 256],
     [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1), (672, 512, 1),
      (1344, 1024, 4), (2688, 1792, 7)]))
 def test_stream_gemm(cfg, M, N, K, S):
@@ -442,6 +442,40 @@ def test_stream_gemm(cfg, M, N, K, S):
         close(slabs.sum(0), exp, atol=1e-2, rtol=1e-2)
         res = bf(M, N)
         close(ops.slab_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 4, 16])
+@pytest.mark.parametrize("form", ["slabs", "swiglu8", "bf16"])
+def test_stream_gemm_consumer_rmsnorm(form, M):
+    """Small-batch decode: the consumer GEMM reads the un-normalised residual
+    stream and scales row m by rsqrt(mean(x[m]^2) + eps) in its epilogue, the gains folded into W:
+    equal to RMSNorm(x) g W^T in fp32 (split-K slabs, the SwiGLU8 gate_up form, plain bf16)."""
+    K, eps = 4096, 1e-5
+    x = (torch.randn(M, K, device=DEV) * 3).to(torch.bfloat16)
+    g = (torch.rand(K, device=DEV) + 0.5).to(torch.bfloat16)
+    if form == "swiglu8":
+        F = 1024
+        wg, wu = bf(F, K, scale=0.02), bf(F, K, scale=0.02)
+        w = ops.interleave_gate_up(wg, wu, 8)
+    else:
+        w = bf(6144 if form == "slabs" else 512, K, scale=0.05)
+    wf = (w.float() * g.float()[None]).to(torch.bfloat16)  # gains folded (the model's layout)
+    # the kernel's contract: r[m] (x W'^T) with the folded bf16 weights (folding's own rounding is
+    # covered by the model-level test against the norm kernels)
+    xn = x.float() * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + eps)
+    exp = xn @ wf.float().t()
+    ws = ops.shuffle_weights(wf)
+    if form == "slabs":
+        got = ops.stream_gemm(x, ws, splits=4, cfg=30, nt=True, norm_eps=eps).sum(0)
+        close(got, exp, atol=5e-2, rtol=2e-2)
+    elif form == "swiglu8":
+        got = ops.stream_gemm(x, ws, epilogue=ops.EPI_SWIGLU8, cfg=30, nt=True, norm_eps=eps)
+        v = exp.view(M, -1, 2, 8)
+        close(got, (torch.nn.functional.silu(v[:, :, 0]) * v[:, :, 1]).reshape(M, -1).to(torch.bfloat16),
+              atol=5e-2, rtol=3e-2)
+    else:
+        got = ops.stream_gemm(x, ws, cfg=30, nt=True, norm_eps=eps)
+        close(got, exp.to(torch.bfloat16), atol=5e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([0, 1, 3, 5, 6, 8, 10, 13], [5, 64, 128])])
@@ -917,3 +951,25 @@ def test_empty_batches_on_gpu():
     idx.add(np.arange(300), torch.randn(300, 256))
     s, ids, docs = idx.search(torch.zeros((0, 256)), 10)
     assert s.shape == (0, 10) and ids.shape == (0, 10)
+
+
+@pytest.mark.parametrize("B,blocks", [(1, 192), (4, 64), (16, 1)])
+def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
+    """Workgroups appended to the small-batch decode attention warm two weight ranges into the
+    Infinity Cache (``warm=``); the attention's output and its arrival counters are bit-identical."""
+    ctx = [1100 + 37 * i for i in range(B)]
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    nb = sum(math.ceil(c / bs) for c in ctx) + 4
+    kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, nb)
+    q = bf(B, Hq, D)
+    ctxt = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(4096 / 512), DEV)
+    base = ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws)
+    w0, w1 = bf(4096, 4096), bf(1000, 4096)  # o-sized, then a partial range of a second tensor
+    for ranges in ([(w0, w0.numel() * 2)], [(w0, w0.numel() * 2), (w1, 3 << 20)], [(w1, 4096 * 16)]):
+        out = ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws, warm=(ranges, blocks))
+        torch.cuda.synchronize()
+        assert torch.equal(out, base)
+        assert int(ws.cnt.abs().sum()) == 0
+    with pytest.raises(Exception):
+        ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws, warm=([(w1, 100)], blocks))  # not a 16-B multiple

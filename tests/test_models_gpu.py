@@ -58,6 +58,39 @@ def test_decode_stream_matches_row_major_path_and_reference(B):
     assert err < 0.15, err
 
 
+@pytest.mark.parametrize("B", [1, 5, 16])
+def test_small_batch_norm_in_consumer_matches_norm_kernels(B):
+    """Batches <= 16 decode without the RMSNorm launches (``LlamaModel._layer_small``: o / down add
+    the residual in their epilogue, qkv / gate_up normalise in theirs with the gains folded into
+    their weights).  Non-unit gains; same model with the fused path off (slab-summing RMSNorm
+    kernels) and the fp32 CPU reference."""
+    cfg = decoder_config("tiny-llama")
+    w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=9, interleave_mlp=True)
+    gen = torch.Generator().manual_seed(7)
+    for k in list(w32):
+        if k.endswith("_norm"):
+            w32[k] = 0.5 + torch.rand(w32[k].shape, generator=gen)
+    prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
+               for n in torch.randint(10, 150, (B,), generator=gen)]
+    wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
+    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+    assert m.frag and m.fold_norms and B <= m.SMALL_FUSED_MAX_M
+    m.small_norm_fused = True  # opt-in path (off by default: slower, profiles/decode_small_r5.md)
+    h_f, lg_f = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    m.small_norm_fused = False
+    h_u, lg_u = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    m.l3_warm_mb = 1  # the Infinity-Cache warm-up riding on the decode attention: same bits
+    h_w, lg_w = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    m.l3_warm_mb = 0
+    assert torch.equal(h_w, h_u) and torch.equal(lg_w, lg_u)
+    torch.testing.assert_close(h_f.float(), h_u.float(), atol=6e-2, rtol=5e-2)
+    torch.testing.assert_close(lg_f.float(), lg_u.float(), atol=6e-2, rtol=5e-2)
+    m_ref = LlamaModel(cfg, {k: v.bfloat16().float() for k, v in w32.items()}, "cpu", interleaved_mlp=True)
+    h_ref, _ = _run(m_ref, cfg, prompts, "cpu", torch.float32)
+    err = (h_f.float().cpu() - h_ref).abs().max().item()
+    assert err < 0.15, err
+
+
 def test_mixed_forward_matches_separate_prefill_and_decode():
     """One mixed forward (prefill chunks + decode rows, padded decode rows included) == the prefill
     forward and the decode forward run separately."""

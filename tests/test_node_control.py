@@ -166,5 +166,7 @@ def test_node_control_plane_world4(tmp_path):
         assert res["llm_steps"][r] >= 40
         per_step_ms = 1000 * res["ctrl_s"][r] / res["llm_steps"][r]
         # typically 0.06-0.16 ms on this CPU container; the bound leaves room for a loaded host and
-        # is still < 7 % of a 7.6 ms Llama-3-8B decode step
-        assert per_step_ms < 0.5, (r, per_step_ms)
+        # is still < 7 % of a 7.6 ms Llama-3-8B decode step (x3 when pytest-xdist workers share the 8
+        # CPUs with the 4 ranks: only the serial run prices the control plane)
+        bound = 1.5 if os.environ.get("PYTEST_XDIST_WORKER") else 0.5
+        assert per_step_ms < bound, (r, per_step_ms)
