@@ -55,6 +55,11 @@ class HashTokenizer {
   mutable std::unordered_map<int32_t, std::string> seen_;
   int32_t word_id(const std::string& w) const;
   std::string pseudo_word(int32_t id) const;
+  // Framed + truncated ids of one text into ``out``; words whose id is not yet marked in ``mark``
+  // (one byte per vocabulary id, owned by the calling thread) are appended to ``fresh``.
+  void encode_into(const std::string& text, bool add_special, int max_len, std::vector<int32_t>& out,
+                   std::vector<uint8_t>& mark, std::vector<std::pair<int32_t, std::string>>& fresh) const;
+  void remember(std::vector<std::pair<int32_t, std::string>>& fresh) const;
 };
 
 }  // namespace dab
