@@ -148,19 +148,36 @@ def attn_suite():
     flop = 4.0 * B * Hq * T * T * D / 2
     emit(op="flash-prefill-causal", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
     # A/B of the software-pipelined V reads (DAB_FLASH_VPIPE), interleaved rounds in this process
-    ref_out = ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True)
-    ab = {"base": [], "vpipe": []}
-    for _ in range(5):
-        for arm in ab:
-            os.environ["DAB_FLASH_VPIPE"] = "1" if arm == "vpipe" else "0"
-            ab[arm].append(timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True)))
-    os.environ["DAB_FLASH_VPIPE"] = "1"
-    err = (ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=True).float() - ref_out.float()).abs().max()
-    os.environ.pop("DAB_FLASH_VPIPE")
-    for arm, ts in ab.items():
-        tm = sorted(ts)[len(ts) // 2]
-        emit(op=f"flash-prefill-causal-{arm}", B=B, T=T, us=round(tm * 1e6, 1), tflops=round(flop / tm / 1e12, 1),
-             max_diff_vs_base=round(float(err), 5) if arm == "vpipe" else 0.0)
+    # A/B of the kernel variants (env-selected per launch), interleaved rounds in this process:
+    # base = unpipelined V reads, vpipe = pipelined (default), w8 = 8 waves + 3-deep K/V ring
+    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "w8": {"DAB_FLASH_W8": "1"}}
+
+    def with_env(env, fn):
+        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8")}
+        for k in old:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        try:
+            return fn()
+        finally:
+            for k, v in old.items():
+                os.environ.pop(k, None)
+                if v is not None:
+                    os.environ[k] = v
+
+    for causal in (True, False):
+        run = lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=causal)  # noqa: E731
+        ref_out = with_env(arms["base"], run)
+        ab = {a: [] for a in arms}
+        for _ in range(5):
+            for arm, env in arms.items():
+                ab[arm].append(with_env(env, lambda: timeit(run)))
+        fl = flop if causal else 2 * flop
+        for arm, ts in ab.items():
+            err = (with_env(arms[arm], run).float() - ref_out.float()).abs().max()
+            tm = sorted(ts)[len(ts) // 2]
+            emit(op=f"flash-prefill-{'causal' if causal else 'full'}-{arm}", B=B, T=T, us=round(tm * 1e6, 1),
+                 tflops=round(fl / tm / 1e12, 1), max_diff_vs_base=round(float(err), 5))
     # the model's prefill form: q read from the qkv projection (row stride (Hq + 2 Hkv) D), without
     # and with RoPE applied on load
     qkv = torch.randn(B * T, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
@@ -181,6 +198,33 @@ def attn_suite():
     t = timeit(lambda: ops.flash_attention_packed(qv, kv, vv, cu2, cu2, T2))
     flop = 4.0 * B2 * H2 * T2 * T2 * D2
     emit(op="flash-encoder", B=B2, T=T2, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
+    # the embed bench's shape: one 262,144-token packed batch of 25-75-token chunks (mean ~50), in
+    # length order as the engine packs them; A/B of the 5-waves-per-SIMD variant (DAB_ENC_W5)
+    g = torch.Generator().manual_seed(0)
+    lens = torch.sort(torch.randint(25, 76, (5300,), generator=g), descending=True).values
+    lens = lens[torch.cumsum(lens, 0) <= 262144]
+    cu3 = torch.zeros(len(lens) + 1, dtype=torch.int32)
+    cu3[1:] = torch.cumsum(lens, 0)
+    cu3 = cu3.cuda()
+    T3 = int(cu3[-1])
+    qkv3 = torch.randn(T3, 3 * H2 * D2, device="cuda").to(torch.bfloat16)
+    q3, k3, v3 = (qkv3[:, i * H2 * D2:(i + 1) * H2 * D2].view(-1, H2, D2) for i in range(3))
+    mx3 = int(lens.max())
+    run3 = lambda: ops.flash_attention_packed(q3, k3, v3, cu3, cu3, mx3)  # noqa: E731
+    ref3 = run3()
+    res3 = {"base": [], "w5": []}
+    for _ in range(5):
+        for arm in res3:
+            os.environ["DAB_ENC_W5"] = "1" if arm == "w5" else "0"
+            res3[arm].append(timeit(run3))
+    os.environ["DAB_ENC_W5"] = "1"
+    err3 = (run3().float() - ref3.float()).abs().max()
+    os.environ.pop("DAB_ENC_W5")
+    byts3 = T3 * 4 * H2 * D2 * 2  # q, k, v read + o written
+    for arm, ts in res3.items():
+        tm = sorted(ts)[len(ts) // 2]
+        emit(op=f"flash-encoder-embedbatch-{arm}", tokens=T3, seqs=len(lens), us=round(tm * 1e6, 1),
+             tbps=round(byts3 / tm / 1e12, 2), max_diff_vs_base=round(float(err3), 5) if arm == "w5" else 0.0)
     # decode: 64 sequences x 1300 context
     for Bd, C in ((64, 1300), (256, 1300), (64, 4000)):
         nbd = Bd * math.ceil(C / bs)

@@ -75,10 +75,13 @@ struct FlashParams {
 // most tiles; decided before the tile's P is exponentiated (nothing is scaled twice).
 constexpr float kDeferLog2 = 8.f;
 
-template <int D, bool CAUSAL, bool PAGED, int NW, int QT>
 // (QT = 2 with 4 waves is held to 256 registers -- 2 waves per SIMD, no spills -- by the
-// launch bound; unbounded it took 294 and ran at 1 wave per SIMD.)
-__global__ __launch_bounds__(64 * NW, (QT == 2 && NW == 4) ? 2 : 1) void flash_fwd_kernel(FlashParams p) {
+// launch bound; unbounded it took 294 and ran at 1 wave per SIMD.)  MINW > 0 overrides the bound:
+// the encoder (D 64, one or two key tiles per ~50-token sequence) is a short latency chain per
+// workgroup, so resident workgroups are its throughput; MINW 5 holds it to 88 registers (5 waves per
+// SIMD, no spills) instead of 112 (4).
+template <int D, bool CAUSAL, bool PAGED, int NW, int QT, int MINW = 0>
+__global__ __launch_bounds__(64 * NW, MINW ? MINW : ((QT == 2 && NW == 4) ? 2 : 1)) void flash_fwd_kernel(FlashParams p) {
   constexpr int KT = 64;
   constexpr int NT = 64 * NW;
   constexpr int QB = 16 * QT * NW;
@@ -384,12 +387,19 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
 }
 
-template <bool CAUSAL, bool VPIPE = false>
-__global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
-  constexpr int D = 128, KT = 64, QB = 128;
+// NW = 8 (W8): 8 waves x 32 queries share each K / V tile (half the DMA per query) and the ring is 3
+// tiles deep (96 KB: one workgroup per CU, still 2 waves per SIMD): tile t + 2 is requested right
+// after the one barrier of tile t, so each tile has two tiles' compute to land in, and the
+// per-tile wait is a counted vmcnt (tile t + 1's pieces stay in flight).
+template <bool CAUSAL, bool VPIPE = false, int NW = 4>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  constexpr int D = 128, KT = 64, QB = 32 * NW;
   constexpr int TILE = KT * D * 2;  // 16 KB
   constexpr int BUF = 2 * TILE;     // K | V
-  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+  constexpr int NBUF = NW == 8 ? 3 : 2;
+  constexpr int PPW = 16 / NW;      // 1-KB K (and V) pieces per wave per tile
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
 
   // same XCD-major (query block, head, sequence) walk as flash_fwd_kernel
   const int nqb = gridDim.x;
@@ -488,8 +498,8 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
     const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), (short)0, nvalid * D * 2, 0x00020000);
     char* kdst = smem + buf * BUF;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int i = 4 * w + j;
+    for (int j = 0; j < PPW; ++j) {
+      const int i = PPW * w + j;
       const int row = 4 * i + st_row;
       const unsigned off = (unsigned)(row * D + 8 * (st_pc ^ f128(row))) * 2u;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(kdst + i * 1024), 16, off,
@@ -650,7 +660,31 @@ __global__ __launch_bounds__(256, 2) void flash_d128_kernel(FlashParams p) {
       c4[st][e] = __builtin_bit_cast(
           float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
   if (n_tiles > 0) issue(0, 0, blk_of(0));
+  if constexpr (NBUF == 3) {
+    if (n_tiles > 1) issue(1, 1, blk_of(1));
+  }
   apply_rope();
+  if constexpr (NBUF == 3) {
+    for (int t = 0; t < n_tiles; ++t) {
+      // this wave's pieces of tile t (tile t + 1's 2 PPW stay in flight), then every wave's -- and
+      // every wave is past tile t - 1's reads, so its buffer takes tile t + 2
+      if (t + 1 < n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (t + 2 < n_tiles) {
+        const int nb = t + 2 - 3 * ((t + 2) / 3);
+        issue(t + 2, nb, blk_of(t + 2));
+      }
+      const int k0 = t * KT;
+      if (w_any && k0 <= w_kmax) compute(k0);
+      const int adv = (t % 3 == 2) ? -2 * BUF : BUF;  // next tile's buffer
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        kadr[i] += adv;
+        vadr[i] += adv;
+      }
+    }
+  } else
   for (int t = 0; t < n_tiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < n_tiles) {
@@ -1069,11 +1103,19 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   prm.scale_log2 = scale * 1.4426950408889634f;
   // Llama prefill (D = 128 over the paged cache): the 32x32 kernel below
   if (D == 128 && paged && block_size % 64 == 0) {
-    dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
     // software-pipelined V reads by default (3% faster, bit-identical: profiles/attn_vpipe_r5.md);
     // DAB_FLASH_VPIPE=0 selects the unpipelined kernel (A/B: benchmarks/kernel_bench.py attn)
     const char* vp = std::getenv("DAB_FLASH_VPIPE");
     const bool vpipe = !(vp && vp[0] == '0');
+    // DAB_FLASH_W8=1: 8 waves per workgroup sharing a 3-deep K / V ring (A/B)
+    const char* w8e = std::getenv("DAB_FLASH_W8");
+    if (w8e && w8e[0] == '1') {
+      dim3 g8((max_seqlen_q + 255) / 256, Hq, batch);
+      if (causal) hipLaunchKernelGGL((flash_d128_kernel<true, true, 8>), g8, dim3(512), 0, s, prm);
+      else hipLaunchKernelGGL((flash_d128_kernel<false, true, 8>), g8, dim3(512), 0, s, prm);
+      return hipGetLastError();
+    }
+    dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
     if (causal && vpipe) hipLaunchKernelGGL((flash_d128_kernel<true, true>), g32, dim3(256), 0, s, prm);
     else if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
     else if (vpipe) hipLaunchKernelGGL((flash_d128_kernel<false, true>), g32, dim3(256), 0, s, prm);
@@ -1085,6 +1127,9 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // query (16x1024 causal: 298 -> 355 TFLOP/s); the encoder (D <= 64) runs 64-query blocks of 4
   // waves (8 waves measured 5 % slower there; a 4-wave x 2-sub-tile form was no faster either)
   const bool wide = D == 128 && max_seqlen_q > 64;
+  // DAB_ENC_W5=1: the 5-waves-per-SIMD encoder variant (A/B: benchmarks/kernel_bench.py attn)
+  const char* e5 = std::getenv("DAB_ENC_W5");
+  const bool enc5 = e5 && e5[0] == '1';
   const int qb = wide ? 128 : 64;
   dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
 #define DAB_FLASH(DD, C, P)                                                                          \
@@ -1092,6 +1137,8 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     if (wide)                                                                                       \
       hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, (DD == 128 ? 8 : 4), 1>), grid,              \
                          dim3(DD == 128 ? 512 : 256), 0, s, prm);                                   \
+    else if (DD == 64 && enc5)                                                                      \
+      hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1, DD == 64 ? 5 : 0>), grid, dim3(256), 0, s, prm); \
     else                                                                                            \
       hipLaunchKernelGGL((flash_fwd_kernel<DD, C, P, 4, 1>), grid, dim3(256), 0, s, prm);           \
   } while (0)

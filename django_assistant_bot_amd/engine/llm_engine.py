@@ -425,6 +425,7 @@ class LLMEngine:
             n = min(total - r.computed, budget)
             if n > 0:
                 chunks.append((r, r.computed, n))
+                self.blocks.commit_prefix(r.seq, r.computed + n)
                 budget -= n
         while self.waiting and budget > 0 and len(self.running) + len(self.prefilling) < self.max_batch:
             r = self.waiting[0]
@@ -440,6 +441,11 @@ class LLMEngine:
             self.prefilling.append(r)
             n = min(len(toks) - cached, budget)
             chunks.append((r, cached, n))
+            # the chunk's full blocks enter the prefix cache as it is scheduled: a later request of
+            # the SAME step that shares them (a common system prompt) starts after them.  Every chunk
+            # scheduled here runs in one forward whose per-layer K / V write covers all of its tokens
+            # before that layer's attention reads any block, so the sharer reads them in time.
+            self.blocks.commit_prefix(r.seq, cached + n)
             budget -= n
         return chunks
 

@@ -35,17 +35,22 @@ def embed_corpus(engine, text_of: Callable[[int], str], n: int, rank: int = 0, w
     # this chunk's batches run on the GPU
     from concurrent.futures import ThreadPoolExecutor
 
-    def tokenize(s):
-        return engine.tokenize([text_of(int(i)) for i in ids[s:s + chunk]])
+    # the first block is small, so the GPU starts after ~1/8 of a block's tokenization instead of a
+    # whole one (nothing overlaps the first block's tokenization)
+    first = min(chunk, max(4096, chunk // 8))
+    starts = [0] + list(range(first, len(ids), chunk)) if len(ids) > first else [0]
+    bounds = starts[1:] + [len(ids)]
 
-    starts = list(range(0, len(ids), chunk))
+    def tokenize(k):
+        return engine.tokenize([text_of(int(i)) for i in ids[starts[k]:bounds[k]]])
+
     pool = ThreadPoolExecutor(1) if len(starts) > 1 else None
-    nxt = pool.submit(tokenize, starts[0]) if pool else None
+    nxt = pool.submit(tokenize, 0) if pool else None
     for k, s in enumerate(starts):
-        part = ids[s:s + chunk]
-        flat, offs = nxt.result() if pool else tokenize(s)
+        part = ids[s:bounds[k]]
+        flat, offs = nxt.result() if pool else tokenize(k)
         if pool and k + 1 < len(starts):
-            nxt = pool.submit(tokenize, starts[k + 1])
+            nxt = pool.submit(tokenize, k + 1)
         v = engine.embed_tokens(np.asarray(flat), np.asarray(offs), out_dtype=torch.float32)
         if index is not None:
             target = getattr(index, "local", index)  # ShardedIndex -> its local VectorIndex (we own these ids)

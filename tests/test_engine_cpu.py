@@ -233,3 +233,26 @@ def test_preemption_recompute_matches_an_unconstrained_pool():
     assert outs[2].finish_reason == "abort" and len(outs[2].token_ids) < 40
     assert [o.token_ids for i, o in enumerate(outs) if i != 2] == [t for i, t in enumerate(ref) if i != 2]
     assert small.blocks.num_free_blocks() == small.blocks.num_blocks()
+
+
+def test_prefix_blocks_are_shared_within_one_prefill_step():
+    """Requests admitted in the same prefill step share the blocks of their common prefix (committed
+    as each chunk is scheduled): only the first computes them, and every request's greedy tokens
+    equal a cold run without the prefix cache."""
+    w = _weights()
+    greedy = SamplingParams(max_new_tokens=5, do_sample=False, temperature=0.0, ignore_eos=True)
+    shared = list(range(11, 11 + 64))  # 4 full 16-token blocks
+    prompts = [shared + [300 + 7 * i + j for j in range(5 + i)] for i in range(5)]
+    outs = {}
+    for cache in (True, False):
+        eng = LLMEngine(decoder_config("tiny-llama"), device="cpu", weights=dict(w), max_batch=8, block_size=16,
+                        num_blocks=96, max_prefill_tokens=1024, use_graphs=False, prefix_cache=cache)
+        rids = [eng.add_request(p, greedy) for p in prompts]
+        eng.step()  # every prompt is admitted and prefilled in this one step
+        if cache:
+            assert eng.stats["prefill_tokens"] == sum(len(p) for p in prompts) - 4 * 64
+            assert eng.blocks.prefix_hits() >= 4 * 64
+        while eng.has_unfinished():
+            eng.step()
+        outs[cache] = [eng.pop_output(r).token_ids for r in rids]
+    assert outs[True] == outs[False]

@@ -973,3 +973,41 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
         assert int(ws.cnt.abs().sum()) == 0
     with pytest.raises(Exception):
         ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws, warm=([(w1, 100)], blocks))  # not a 16-B multiple
+
+
+@pytest.mark.parametrize("env", ["DAB_ENC_W5", "DAB_FLASH_W8"])
+def test_attention_variants_match_the_default_kernel(env, monkeypatch):
+    """Occupancy / pipeline variants of the attention kernels selected per launch by environment
+    switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
+    the 5-waves-per-SIMD encoder kernel bit for bit, the 8-wave 3-deep-ring prefill kernel
+    (a different wave -> query mapping, same per-query math) bit for bit as well."""
+    g = torch.Generator().manual_seed(3)
+    if env == "DAB_ENC_W5":
+        lens = torch.randint(20, 140, (37,), generator=g)
+        cu = torch.zeros(38, dtype=torch.int32)
+        cu[1:] = torch.cumsum(lens, 0)
+        T, H, D = int(cu[-1]), 12, 64
+        qkv = bf(T, 3 * H * D)
+        q, k, v = (qkv[:, i * H * D:(i + 1) * H * D].view(T, H, D) for i in range(3))
+        cu = cu.to(DEV)
+        run = lambda: ops.flash_attention_packed(q, k, v, cu, cu, int(lens.max()))  # noqa: E731
+        exp = ref.flash_attention_packed(q, k, v, cu, cu, False, 1 / math.sqrt(D))
+    else:
+        ctx = [1, 100, 255, 256, 257, 700, 1024, 1500]
+        Hq, Hkv, D, bs = 32, 8, 128, 64
+        nb = sum(math.ceil(c / bs) for c in ctx) + 4
+        kc, vc, bt = _paged_setup(ctx, Hkv, D, bs, nb)
+        cu = torch.zeros(len(ctx) + 1, dtype=torch.int32)
+        cu[1:] = torch.cumsum(torch.tensor(ctx), 0)
+        q = bf(int(cu[-1]), Hq, D)
+        cu, ctxt = cu.to(DEV), torch.tensor(ctx, dtype=torch.int32, device=DEV)
+        run = lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(ctx), causal=True)  # noqa: E731
+        exp = None
+    monkeypatch.setenv(env, "0")
+    base = run()
+    monkeypatch.setenv(env, "1")
+    out = run()
+    torch.cuda.synchronize()
+    assert torch.equal(out, base)
+    if exp is not None:
+        close(out, exp)
