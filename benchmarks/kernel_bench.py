@@ -149,8 +149,10 @@ def attn_suite():
     emit(op="flash-prefill-causal", B=B, T=T, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1))
     # A/B of the software-pipelined V reads (DAB_FLASH_VPIPE), interleaved rounds in this process
     # A/B of the kernel variants (env-selected per launch), interleaved rounds in this process:
-    # base = unpipelined V reads, vpipe = pipelined (default), w8 = 8 waves + 3-deep K/V ring
-    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "w8": {"DAB_FLASH_W8": "1"}}
+    # base = unpipelined V reads, vpipe = pipelined (default), w8 = 8 waves + 3-deep K/V ring,
+    # w8stag = 8 waves in two groups half a tile apart + 4-deep ring
+    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "w8": {"DAB_FLASH_W8": "1"},
+            "w8stag": {"DAB_FLASH_W8": "2"}}
 
     def with_env(env, fn):
         old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8")}
@@ -272,6 +274,31 @@ def decode_sweep():
         del kc, vc
 
 
+def attn_scan():
+    """Prefill attention at a fixed 16,384 tokens per launch, T = 256 .. 4096 per sequence, causal and
+    full: separates the per-workgroup fixed cost (Q load, first K / V tile, epilogue) from the
+    per-tile cost (time = WGs x (F + tiles x c) / slots)."""
+    Hq, Hkv, D, bs = 32, 8, 128, 64
+    for T in (256, 512, 1024, 2048, 4096):
+        B = 16384 // T
+        nb = B * T // bs
+        kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+        vc = torch.randn_like(kc)
+        bt = torch.arange(nb, dtype=torch.int32, device="cuda").view(B, T // bs)
+        q = torch.randn(B * T, Hq, D, device="cuda").to(torch.bfloat16)
+        cu = torch.arange(0, B * T + 1, T, dtype=torch.int32, device="cuda")
+        ctx = torch.full((B,), T, dtype=torch.int32, device="cuda")
+        for causal in (True, False):
+            ts = sorted(timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=causal))
+                        for _ in range(5))
+            t = ts[2]
+            flop = 4.0 * B * Hq * T * T * D / (2 if causal else 1)
+            qb = T // 128
+            tiles = B * Hq * (sum(2 * (i + 1) for i in range(qb)) if causal else qb * (T // 64))
+            emit(op="flash-scan", T=T, B=B, causal=causal, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1),
+                 workgroups=B * Hq * qb, wg_tiles=tiles)
+
+
 def select_suite():
     logits = torch.randn(64, 128256, device="cuda").to(torch.bfloat16)
     temp = torch.ones(64, device="cuda")
@@ -313,5 +340,7 @@ if __name__ == "__main__":
         gemm_suite(sys.argv[2] if len(sys.argv) > 2 else None)
     if which in ("all", "attn"):
         attn_suite()
+    if which == "attnscan":
+        attn_scan()
     if which in ("all", "select"):
         select_suite()

@@ -391,13 +391,21 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 // tiles deep (96 KB: one workgroup per CU, still 2 waves per SIMD): tile t + 2 is requested right
 // after the one barrier of tile t, so each tile has two tiles' compute to land in, and the
 // per-tile wait is a counted vmcnt (tile t + 1's pieces stay in flight).
-template <bool CAUSAL, bool VPIPE = false, int NW = 4>
+//
+// STAG (8 waves, 4-deep ring): the two wave groups (waves 0-3 / 4-7, one of each per SIMD) are half a
+// tile apart.  Group 0 runs S(t), softmax(t), PV(t); group 1 runs PV(t-1), S(t), softmax(t), holding
+// P(t-1) in registers across the barrier, so on every SIMD one group's softmax VALU runs beside the
+// other group's MFMAs instead of both groups hitting the same pipe at once.  PV(t-1) finishes before
+// softmax(t) may rescale O (cdna_hip_programming.md T13 hazard).  Tile t-1's buffer stays live through
+// iteration t, hence the 4th buffer (128 KB).
+template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(!STAG || NW == 8, "staggered groups: 8 waves");
   constexpr int D = 128, KT = 64, QB = 32 * NW;
   constexpr int TILE = KT * D * 2;  // 16 KB
   constexpr int BUF = 2 * TILE;     // K | V
-  constexpr int NBUF = NW == 8 ? 3 : 2;
+  constexpr int NBUF = STAG ? 4 : (NW == 8 ? 3 : 2);
   constexpr int PPW = 16 / NW;      // 1-KB K (and V) pieces per wave per tile
   __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
 
@@ -649,6 +657,89 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     });
   };
 
+  // STAG group 1: the two halves of compute() on their own.  ssm: S^T, mask, online softmax (O / l
+  // rescaled here), P packed to the 4 bf16 B fragments of the PV k-steps.  pv: O^T += V^T P^T from the
+  // tile buffer whose V addresses are va.
+  auto ssm = [&](const int k0, bf16x8 (&pf)[4]) DAB_ALWAYS_INLINE {
+    f32x16 s0, s1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s0[r] = s1[r] = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 ka[4], kb2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto* kp = (const __attribute__((address_space(3))) bf16x8*)(uintptr_t)(kadr[4 * half + i]);
+        ka[i] = kp[0];
+        kb2[i] = kp[8192 / 16];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s0 = mfma32(ka[i], qf[4 * half + i], s0);
+        s1 = mfma32(kb2[i], qf[4 * half + i], s1);
+      }
+    }
+    const bool need_mask = k0 + KT > kv_len || (CAUSAL && k0 + KT - 1 > kv_len - seqlen_q + q0);
+    if (need_mask) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (key >= kv_len || (CAUSAL && key > q_pos)) s0[r] = kNegInf;
+        if (key + 32 >= kv_len || (CAUSAL && key + 32 > q_pos)) s1[r] = kNegInf;
+      }
+    }
+    float mx = kNegInf;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    mx = fmaxf(mx, xor32(mx));
+    const float mxs = mx * sc;
+    const bool keep = __all(mxs - m_run <= kDeferLog2);
+    const float m_new = keep ? m_run : fmaxf(m_run, mxs);
+    const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+    float ls = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], sc, -m_new));
+      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], sc, -m_new));
+      ls += s0[r] + s1[r];
+    }
+    l_run = l_run * alpha + ls;
+    m_run = m_new;
+    if (!keep && __any(alpha < 1.f)) {
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db] *= alpha;
+    }
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const f32x16& sv = (ks >> 1) ? s1 : s0;
+      const int ss = ks & 1;
+      u32x4 pu;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pu[e] = pack2bf(sv[8 * ss + 2 * e], sv[8 * ss + 2 * e + 1]);
+      pf[ks] = __builtin_bit_cast(bf16x8, pu);
+    }
+  };
+  auto pv = [&](const int delta, const bf16x8 (&pf)[4]) DAB_ALWAYS_INLINE {
+    unsigned va[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) va[i] = vadr[i] + delta;
+    static_for<0, 4>([&](auto KS_) DAB_ALWAYS_INLINE {
+      constexpr int ks = decltype(KS_)::value;
+      u32x2 tr[8];
+      ds_tr16_x8<(ks >> 1) * 8192 + (ks & 1) * 4096>(va, tr);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        u32x4 u;
+        u[0] = tr[2 * db][0];
+        u[1] = tr[2 * db][1];
+        u[2] = tr[2 * db + 1][0];
+        u[3] = tr[2 * db + 1][1];
+        o[db] = mfma32(__builtin_bit_cast(bf16x8, u), pf[ks], o[db]);
+      }
+      return true;
+    });
+  };
+
   // One tile in flight: tile t + 1 is requested once tile t has landed and streams in under tile
   // t's math.
   // the cos/sin loads go out after the block-table loads and before the first DMA, so the waits
@@ -660,29 +751,45 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
       c4[st][e] = __builtin_bit_cast(
           float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
   if (n_tiles > 0) issue(0, 0, blk_of(0));
-  if constexpr (NBUF == 3) {
+  if constexpr (NBUF >= 3) {
     if (n_tiles > 1) issue(1, 1, blk_of(1));
   }
   apply_rope();
-  if constexpr (NBUF == 3) {
+  if constexpr (NBUF >= 3) {
+    const bool g1 = STAG && w >= 4;  // wave-uniform
+    bf16x8 pp[4];                    // STAG group 1: P of the pending tile (in the previous buffer)
+    bool pend = false;
     for (int t = 0; t < n_tiles; ++t) {
       // this wave's pieces of tile t (tile t + 1's 2 PPW stay in flight), then every wave's -- and
-      // every wave is past tile t - 1's reads, so its buffer takes tile t + 2
+      // every wave is past its reads of tile t - 2 (t - 1 without STAG), whose buffer takes tile t + 2
       if (t + 1 < n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       if (t + 2 < n_tiles) {
-        const int nb = t + 2 - 3 * ((t + 2) / 3);
+        const int nb = (t + 2) % NBUF;
         issue(t + 2, nb, blk_of(t + 2));
       }
       const int k0 = t * KT;
-      if (w_any && k0 <= w_kmax) compute(k0);
-      const int adv = (t % 3 == 2) ? -2 * BUF : BUF;  // next tile's buffer
+      if constexpr (STAG) {
+        if (g1) {
+          if (pend) pv(t % NBUF == 0 ? (NBUF - 1) * BUF : -BUF, pp);  // tile t - 1's buffer
+          pend = w_any && k0 <= w_kmax;
+          if (pend) ssm(k0, pp);
+        } else if (w_any && k0 <= w_kmax) {
+          compute(k0);
+        }
+      } else {
+        if (w_any && k0 <= w_kmax) compute(k0);
+      }
+      const int adv = (t % NBUF == NBUF - 1) ? -(NBUF - 1) * BUF : BUF;  // next tile's buffer
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         kadr[i] += adv;
         vadr[i] += adv;
       }
+    }
+    if constexpr (STAG) {
+      if (pend) pv(n_tiles % NBUF == 0 ? (NBUF - 1) * BUF : -BUF, pp);  // the last tile's buffer
     }
   } else
   for (int t = 0; t < n_tiles; ++t) {
@@ -1109,9 +1216,12 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     const bool vpipe = !(vp && vp[0] == '0');
     // DAB_FLASH_W8=1: 8 waves per workgroup sharing a 3-deep K / V ring (A/B)
     const char* w8e = std::getenv("DAB_FLASH_W8");
-    if (w8e && w8e[0] == '1') {
+    if (w8e && (w8e[0] == '1' || w8e[0] == '2')) {  // 2: with the staggered wave groups
       dim3 g8((max_seqlen_q + 255) / 256, Hq, batch);
-      if (causal) hipLaunchKernelGGL((flash_d128_kernel<true, true, 8>), g8, dim3(512), 0, s, prm);
+      const bool stag = w8e[0] == '2';
+      if (causal && stag) hipLaunchKernelGGL((flash_d128_kernel<true, false, 8, true>), g8, dim3(512), 0, s, prm);
+      else if (causal) hipLaunchKernelGGL((flash_d128_kernel<true, true, 8>), g8, dim3(512), 0, s, prm);
+      else if (stag) hipLaunchKernelGGL((flash_d128_kernel<false, false, 8, true>), g8, dim3(512), 0, s, prm);
       else hipLaunchKernelGGL((flash_d128_kernel<false, true, 8>), g8, dim3(512), 0, s, prm);
       return hipGetLastError();
     }
@@ -1127,9 +1237,10 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // query (16x1024 causal: 298 -> 355 TFLOP/s); the encoder (D <= 64) runs 64-query blocks of 4
   // waves (8 waves measured 5 % slower there; a 4-wave x 2-sub-tile form was no faster either)
   const bool wide = D == 128 && max_seqlen_q > 64;
-  // DAB_ENC_W5=1: the 5-waves-per-SIMD encoder variant (A/B: benchmarks/kernel_bench.py attn)
+  // the 5-waves-per-SIMD encoder variant by default (3 % faster on the embed bench's packed batch,
+  // bit-identical: profiles/embed_r5.md); DAB_ENC_W5=0 selects the unbounded-register kernel
   const char* e5 = std::getenv("DAB_ENC_W5");
-  const bool enc5 = e5 && e5[0] == '1';
+  const bool enc5 = !(e5 && e5[0] == '0');
   const int qb = wide ? 128 : 64;
   dim3 grid((max_seqlen_q + qb - 1) / qb, Hq, batch);
 #define DAB_FLASH(DD, C, P)                                                                          \

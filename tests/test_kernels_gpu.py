@@ -975,8 +975,8 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
         ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws, warm=([(w1, 100)], blocks))  # not a 16-B multiple
 
 
-@pytest.mark.parametrize("env", ["DAB_ENC_W5", "DAB_FLASH_W8"])
-def test_attention_variants_match_the_default_kernel(env, monkeypatch):
+@pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2")])
+def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
     the 5-waves-per-SIMD encoder kernel bit for bit, the 8-wave 3-deep-ring prefill kernel
@@ -1005,7 +1005,7 @@ def test_attention_variants_match_the_default_kernel(env, monkeypatch):
         exp = None
     monkeypatch.setenv(env, "0")
     base = run()
-    monkeypatch.setenv(env, "1")
+    monkeypatch.setenv(env, val)
     out = run()
     torch.cuda.synchronize()
     assert torch.equal(out, base)
