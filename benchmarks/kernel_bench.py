@@ -150,12 +150,12 @@ def attn_suite():
     # A/B of the software-pipelined V reads (DAB_FLASH_VPIPE), interleaved rounds in this process
     # A/B of the kernel variants (env-selected per launch), interleaved rounds in this process:
     # base = unpipelined V reads, vpipe = pipelined (default), w8 = 8 waves + 3-deep K/V ring,
-    # w8stag = 8 waves in two groups half a tile apart + 4-deep ring
-    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "w8": {"DAB_FLASH_W8": "1"},
-            "w8stag": {"DAB_FLASH_W8": "2"}}
+    # pair = one workgroup per (long, short) causal query-block pair
+    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "pair": {"DAB_FLASH_PAIR": "1"},
+            "w8": {"DAB_FLASH_W8": "1"}}
 
     def with_env(env, fn):
-        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8")}
+        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR")}
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -288,14 +288,17 @@ def attn_scan():
         q = torch.randn(B * T, Hq, D, device="cuda").to(torch.bfloat16)
         cu = torch.arange(0, B * T + 1, T, dtype=torch.int32, device="cuda")
         ctx = torch.full((B,), T, dtype=torch.int32, device="cuda")
-        for causal in (True, False):
+        for causal, pair in ((True, False), (True, True), (False, False)):
+            os.environ["DAB_FLASH_PAIR"] = "1" if pair else "0"
             ts = sorted(timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=causal))
                         for _ in range(5))
+            os.environ.pop("DAB_FLASH_PAIR")
             t = ts[2]
             flop = 4.0 * B * Hq * T * T * D / (2 if causal else 1)
             qb = T // 128
             tiles = B * Hq * (sum(2 * (i + 1) for i in range(qb)) if causal else qb * (T // 64))
-            emit(op="flash-scan", T=T, B=B, causal=causal, us=round(t * 1e6, 1), tflops=round(flop / t / 1e12, 1),
+            emit(op="flash-scan", T=T, B=B, causal=causal, pair=pair, us=round(t * 1e6, 1),
+                 tflops=round(flop / t / 1e12, 1),
                  workgroups=B * Hq * qb, wg_tiles=tiles)
 
 

@@ -398,10 +398,15 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 // other group's MFMAs instead of both groups hitting the same pipe at once.  PV(t-1) finishes before
 // softmax(t) may rescale O (cdna_hip_programming.md T13 hazard).  Tile t-1's buffer stays live through
 // iteration t, hence the 4th buffer (128 KB).
-template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false>
+//
+// PAIR (causal, 4 waves): one workgroup runs query block nqb-1-i and then block i of its (sequence,
+// head), so every workgroup has 2 (nqb + 1) key tiles of work, and block i's first K / V tile and the
+// rest of its stream continue from block nqb-1-i's last tile on without a cold start (same keys).
+template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!STAG || NW == 8, "staggered groups: 8 waves");
+  static_assert(!PAIR || (NW == 4 && CAUSAL), "paired blocks: 4 waves, causal");
   constexpr int D = 128, KT = 64, QB = 32 * NW;
   constexpr int TILE = KT * D * 2;  // 16 KB
   constexpr int BUF = 2 * TILE;     // K | V
@@ -422,38 +427,53 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   // causal: a sequence's last query block (the most key tiles) starts first, so the short blocks
   // fill the end of each XCD's walk instead of a long one trailing alone
   const int nqb_b = div_up(seqlen_q, QB);
-  const int qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
-  const int q0 = qb * QB;
+  int qb, qb2 = -1;  // qb2: PAIR's second (short) block
+  if constexpr (PAIR) {
+    const int pi = sid % nqb;
+    if (pi >= div_up(nqb_b, 2)) return;  // whole workgroup
+    qb = nqb_b - 1 - pi;
+    if (pi < qb) qb2 = pi;
+  } else {
+    qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
+  }
+  int q0 = qb * QB;
   if (q0 >= seqlen_q) return;  // whole workgroup
   const int kv_len = p.ctx_k[b];
   const int hk = h / (p.Hq / p.Hkv);
   const int tid = threadIdx.x, lane = tid & 63, lq = lane & 31, hi = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int my_q = q0 + 32 * w + lq;
-  const bool q_valid = my_q < seqlen_q;
-  const int q_pos = kv_len - seqlen_q + my_q;
-  // highest key position any valid query of this wave attends to (wave-uniform)
-  const int w_last_q = min(q0 + 32 * w + 31, seqlen_q - 1);
-  const int w_kmax = CAUSAL ? kv_len - seqlen_q + w_last_q : kv_len - 1;
-  const bool w_any = q0 + 32 * w < seqlen_q;
+  int my_q, q_pos, w_kmax;
+  bool q_valid, w_any;
+  auto set_block = [&](const int q0_) DAB_ALWAYS_INLINE {
+    q0 = q0_;
+    my_q = q0 + 32 * w + lq;
+    q_valid = my_q < seqlen_q;
+    q_pos = kv_len - seqlen_q + my_q;
+    // highest key position any valid query of this wave attends to (wave-uniform)
+    const int w_last_q = min(q0 + 32 * w + 31, seqlen_q - 1);
+    w_kmax = CAUSAL ? kv_len - seqlen_q + w_last_q : kv_len - 1;
+    w_any = q0 + 32 * w < seqlen_q;
+  };
+  set_block(q0);
 
   // Q^T fragments (B operand): lane (q, hi) holds Q[q][16 s + 8 hi .. + 8], s = 0..7
   bf16x8 qf[8];
-  {
+  auto load_q = [&]() DAB_ALWAYS_INLINE {
     const bf16* qrow = p.q + (size_t)(q_start + (q_valid ? my_q : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
       qf[st] = q_valid ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
     }
-  }
+  };
+  load_q();
   // RoPE of Q on load (rope_cs): dims 16 st + 8 hi + j (st < 4) pair with the same lane's dims + 64
   // (st + 4).  Applied after the first K/V tile's DMA is issued, so its loads and math overlap it.
-  const bool rope_q = p.rope_cs && q_valid;
+  bool rope_q = p.rope_cs && q_valid;
   // cos/sin rows through a wave-uniform buffer descriptor (empty range without RoPE: the loads
   // return zeros and touch nothing), so the loads are unconditional and hipcc's wait counting stays
   // exact across them (a conditional load made it drain the first tile's DMA)
-  const int cs_row = p.rope_cs ? p.rope_pos[q_start + (q_valid ? my_q : 0)] : 0;
+  int cs_row = p.rope_cs ? p.rope_pos[q_start + (q_valid ? my_q : 0)] : 0;
   const auto cs_rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.rope_cs ? (const void*)p.rope_cs : (const void*)p.q),
                                                        (short)0, p.rope_cs ? 0x7ffffff0 : 0, 0x00020000);
   float4 c4[4][4];
@@ -473,12 +493,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     }
   };
 
-  int n_keys = kv_len;
-  if (CAUSAL) {
-    const int last_q = min(q0 + QB - 1, seqlen_q - 1);
-    n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
-  }
-  const int n_tiles = div_up(n_keys, KT);
+  auto tiles_of = [&](const int q0_) DAB_ALWAYS_INLINE {
+    int n_keys = kv_len;
+    if (CAUSAL) {
+      const int last_q = min(q0_ + QB - 1, seqlen_q - 1);
+      n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
+    }
+    return div_up(n_keys, KT);
+  };
+  const int n_tiles = tiles_of(q0);  // (PAIR: of the long block; the short one's are a prefix)
 
   // LDS-DMA staging (buffer_load ... lds): wave w issues K / V pieces i = 4 w .. 4 w + 3 (1 KB =
   // 4 rows each); LDS slot (row 4 i + lane / 16, physical chunk lane % 16) receives logical chunk
@@ -657,6 +680,24 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     });
   };
 
+  // ---- epilogue: O[q][d], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hi
+  auto epilogue = [&]() DAB_ALWAYS_INLINE {
+    const float l_tot = l_run + __shfl_xor(l_run, 32, 64);
+    if (q_valid) {
+      const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+      bf16* orow = p.out + (size_t)(q_start + my_q) * p.o_stride_tok + (size_t)h * p.o_stride_head;
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          u32x2 v;
+          v[0] = pack2bf(o[db][4 * rg] * inv, o[db][4 * rg + 1] * inv);
+          v[1] = pack2bf(o[db][4 * rg + 2] * inv, o[db][4 * rg + 3] * inv);
+          *reinterpret_cast<u32x2*>(orow + 32 * db + 8 * rg + 4 * hi) = v;
+        }
+    }
+  };
+
   // STAG group 1: the two halves of compute() on their own.  ssm: S^T, mask, online softmax (O / l
   // rescaled here), P packed to the 4 bf16 B fragments of the PV k-steps.  pv: O^T += V^T P^T from the
   // tile buffer whose V addresses are va.
@@ -744,13 +785,50 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   // t's math.
   // the cos/sin loads go out after the block-table loads and before the first DMA, so the waits
   // for them neither drain the DMA nor wait behind it
+  auto load_cs = [&]() DAB_ALWAYS_INLINE {
 #pragma unroll
-  for (int st = 0; st < 4; ++st)
+    for (int st = 0; st < 4; ++st)
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-      c4[st][e] = __builtin_bit_cast(
-          float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
+      for (int e = 0; e < 4; ++e)
+        c4[st][e] = __builtin_bit_cast(
+            float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
+  };
+  load_cs();
   if (n_tiles > 0) issue(0, 0, blk_of(0));
+  // PAIR: the short block's Q (RoPE applied) is loaded now, beside the long block's, so the loop
+  // holds no loads but the K / V DMA (a load at the seam made hipcc wait for the in-flight DMA in
+  // every step); one cos / sin row group at a time keeps the prologue's register peak down
+  bf16x8 qfB[8];
+  if constexpr (PAIR) {
+    const int myB = (qb2 >= 0 ? qb2 * QB : 0) + 32 * w + lq;
+    const bool vB = qb2 >= 0 && myB < seqlen_q;
+    const bf16* qrow = p.q + (size_t)(q_start + (vB ? myB : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qfB[st] = vB ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
+    }
+    if (p.rope_cs && vB) {
+      const int row = p.rope_pos[q_start + myB];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        float4 cr[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          cr[e] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 cc = cr[j >> 1];
+          const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
+          float x1 = bf2f((uint16_t)qfB[st][j]), x2 = bf2f((uint16_t)qfB[st + 4][j]);
+          rope_rot(x1, x2, cs);
+          qfB[st][j] = (short)f2bf(x1);
+          qfB[st + 4][j] = (short)f2bf(x2);
+        }
+      }
+    }
+  }
   if constexpr (NBUF >= 3) {
     if (n_tiles > 1) issue(1, 1, blk_of(1));
   }
@@ -791,41 +869,45 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     if constexpr (STAG) {
       if (pend) pv(n_tiles % NBUF == 0 ? (NBUF - 1) * BUF : -BUF, pp);  // the last tile's buffer
     }
-  } else
-  for (int t = 0; t < n_tiles; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < n_tiles) {
-      __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (t + 1) & 1 (tile t - 1)
-      const int blk = blk_of(t + 1);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
-      issue(t + 1, buf ^ 1, blk);
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile t
-    const int k0 = t * KT;
-    if (w_any && k0 <= w_kmax) compute(k0);  // else this wave's queries see no key of the tile
+  } else {
+    // PAIR: steps [0, nA) walk the long block's tiles, [nA, nA + nB) the short block's (tile s - nA)
+    const int nA = n_tiles;
+    const int nB = PAIR && qb2 >= 0 ? tiles_of(qb2 * QB) : 0;
+    for (int s = 0; s < nA + nB; ++s) {
+      const int t = s < nA ? s : s - nA;
+      const int buf = s & 1;
+      if (s + 1 < nA + nB) {
+        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s + 1) & 1 (step s - 1)
+        const int tn = s + 1 < nA ? s + 1 : s + 1 - nA;
+        const int blk = blk_of(tn);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
+        issue(tn, buf ^ 1, blk);
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile t
+      const int k0 = t * KT;
+      if (w_any && k0 <= w_kmax) compute(k0);  // else this wave's queries see no key of the tile
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      kadr[i] ^= BUF;
-      vadr[i] ^= BUF;
+      for (int i = 0; i < 8; ++i) {
+        kadr[i] ^= BUF;
+        vadr[i] ^= BUF;
+      }
+      if (PAIR && s == nA - 1 && nB > 0) {
+        epilogue();  // the long block's rows
+        set_block(qb2 * QB);
+#pragma unroll
+        for (int db = 0; db < 4; ++db)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+        m_run = -1e30f;
+        l_run = 0.f;
+#pragma unroll
+        for (int st = 0; st < 8; ++st) qf[st] = qfB[st];  // loaded (and rotated) in the prologue
+      }
     }
   }
-
-  // ---- epilogue: O[q][d], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hi
-  float l_tot = l_run + __shfl_xor(l_run, 32, 64);
-  if (!q_valid) return;
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16* orow = p.out + (size_t)(q_start + my_q) * p.o_stride_tok + (size_t)h * p.o_stride_head;
-#pragma unroll
-  for (int db = 0; db < 4; ++db)
-#pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      u32x2 v;
-      v[0] = pack2bf(o[db][4 * rg] * inv, o[db][4 * rg + 1] * inv);
-      v[1] = pack2bf(o[db][4 * rg + 2] * inv, o[db][4 * rg + 3] * inv);
-      *reinterpret_cast<u32x2*>(orow + 32 * db + 8 * rg + 4 * hi) = v;
-    }
+  epilogue();
 }
 
 // -----------------------------------------------------------------------------------------------
@@ -1226,6 +1308,13 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       return hipGetLastError();
     }
     dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
+    // DAB_FLASH_PAIR=1 (causal): one workgroup per (long, short) query-block pair (A/B)
+    const char* pe = std::getenv("DAB_FLASH_PAIR");
+    if (causal && vpipe && pe && pe[0] == '1') {
+      dim3 gp(((max_seqlen_q + 127) / 128 + 1) / 2, Hq, batch);
+      hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true>), gp, dim3(256), 0, s, prm);
+      return hipGetLastError();
+    }
     if (causal && vpipe) hipLaunchKernelGGL((flash_d128_kernel<true, true>), g32, dim3(256), 0, s, prm);
     else if (causal) hipLaunchKernelGGL((flash_d128_kernel<true>), g32, dim3(256), 0, s, prm);
     else if (vpipe) hipLaunchKernelGGL((flash_d128_kernel<false, true>), g32, dim3(256), 0, s, prm);

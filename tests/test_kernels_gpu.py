@@ -975,12 +975,14 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
         ops.paged_decode(q, kc, vc, bt, ctxt, 512, ws, warm=([(w1, 100)], blocks))  # not a 16-B multiple
 
 
-@pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2")])
+@pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2"),
+                                     ("DAB_FLASH_PAIR", "1")])
 def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
     the 5-waves-per-SIMD encoder kernel bit for bit, the 8-wave 3-deep-ring prefill kernel
-    (a different wave -> query mapping, same per-query math) bit for bit as well."""
+    (a different wave -> query mapping, same per-query math) bit for bit as well, and so does the
+    paired-block causal kernel (both blocks of a pair, odd block counts, a 1-token sequence)."""
     g = torch.Generator().manual_seed(3)
     if env == "DAB_ENC_W5":
         lens = torch.randint(20, 140, (37,), generator=g)
