@@ -150,12 +150,13 @@ def attn_suite():
     # A/B of the software-pipelined V reads (DAB_FLASH_VPIPE), interleaved rounds in this process
     # A/B of the kernel variants (env-selected per launch), interleaved rounds in this process:
     # base = unpipelined V reads, vpipe = pipelined (default), w8 = 8 waves + 3-deep K/V ring,
-    # pair = one workgroup per (long, short) causal query-block pair
-    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {}, "pair": {"DAB_FLASH_PAIR": "1"},
-            "w8": {"DAB_FLASH_W8": "1"}}
+    # pair = (long, short) causal query-block pairs, G per workgroup (default: G from the launch
+    # size; pair-g1 / pair-g4 force G)
+    arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {"DAB_FLASH_PAIR": "0"}, "pair": {},
+            "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "w8": {"DAB_FLASH_W8": "1"}}
 
     def with_env(env, fn):
-        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR")}
+        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR", "DAB_FLASH_G")}
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env)

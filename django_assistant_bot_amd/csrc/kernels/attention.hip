@@ -60,6 +60,7 @@ struct FlashParams {
   // float2 cos/sin table), when the RoPE/KV-write kernel wrote only K / V
   const int* rope_pos;
   const float2* rope_cs;
+  int pairs_per_wg;  // flash_d128 PAIR: causal query-block pairs walked by one workgroup (>= 1)
 };
 
 // One workgroup = 16 QT NW queries (NW waves x QT 16-query sub-tiles) of one (sequence, head);
@@ -422,17 +423,36 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
   const int h = (sid / nqb) % gridDim.y;
   const int b = sid / (nqb * gridDim.y);
+  // the sequence's block ids are requested first: they depend on b alone, so their round trip runs
+  // beside the cu_q / ctx_k loads instead of after them (in-bounds for any row: lane / tpb < max_blocks)
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  const int tpb = p.block_size / KT;  // tiles per cache block
+  const int bt_a = (threadIdx.x & 63) / tpb < p.max_blocks ? bt[(threadIdx.x & 63) / tpb] : 0;
+  const int bt_b = (64 + (threadIdx.x & 63)) / tpb < p.max_blocks ? bt[(64 + (threadIdx.x & 63)) / tpb] : 0;
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
   // causal: a sequence's last query block (the most key tiles) starts first, so the short blocks
   // fill the end of each XCD's walk instead of a long one trailing alone
   const int nqb_b = div_up(seqlen_q, QB);
-  int qb, qb2 = -1;  // qb2: PAIR's second (short) block
+  // PAIR: this workgroup's blocks are, for its pairs pp = p_first .. p_first + G - 1, the long block
+  // nqb_b - 1 - pp then the short block pp (absent for the middle block of an odd count)
+  const int G = PAIR ? p.pairs_per_wg : 1;
+  const int p_first = (sid % nqb) * G;
+  const int npairs = div_up(nqb_b, 2);
+  auto blk_qb = [&](const int j) DAB_ALWAYS_INLINE {
+    const int pp = p_first + (j >> 1);
+    if (j >= 2 * G || pp >= npairs) return -1;
+    const int lng = nqb_b - 1 - pp;
+    return (j & 1) ? (pp < lng ? pp : -1) : lng;
+  };
+  auto next_blk = [&](const int j) DAB_ALWAYS_INLINE {
+    if (blk_qb(j + 1) >= 0) return j + 1;
+    return blk_qb(j + 2) >= 0 ? j + 2 : -1;  // (only a missing short block is skipped)
+  };
+  int qb;
   if constexpr (PAIR) {
-    const int pi = sid % nqb;
-    if (pi >= div_up(nqb_b, 2)) return;  // whole workgroup
-    qb = nqb_b - 1 - pi;
-    if (pi < qb) qb2 = pi;
+    if (p_first >= npairs) return;  // whole workgroup
+    qb = blk_qb(0);
   } else {
     qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
   }
@@ -510,10 +530,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   // block ids of the first 128 tiles (8192 keys) in two registers per lane, read once; per tile a
   // readlane (no memory round trip in the loop: a block-id load there exposed a full global-memory
   // latency per tile, because the DMA request that needs it waits for it)
-  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
-  const int tpb = p.block_size / KT;  // tiles per cache block
-  const int bt_a = lane < n_tiles ? bt[lane / tpb] : 0;
-  const int bt_b = 64 + lane < n_tiles ? bt[(64 + lane) / tpb] : 0;
   auto blk_of = [&](int t) {
     if (t < 64) return __builtin_amdgcn_readlane(bt_a, t);
     if (t < 128) return __builtin_amdgcn_readlane(bt_b, t - 64);
@@ -795,39 +811,22 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   };
   load_cs();
   if (n_tiles > 0) issue(0, 0, blk_of(0));
-  // PAIR: the short block's Q (RoPE applied) is loaded now, beside the long block's, so the loop
-  // holds no loads but the K / V DMA (a load at the seam made hipcc wait for the in-flight DMA in
-  // every step); one cos / sin row group at a time keeps the prologue's register peak down
+  // PAIR: the next block's Q is loaded one block ahead into qfB (raw; RoPE is applied when it
+  // becomes the current block's, at the seam).  Loading qf itself at the seam made hipcc wait for the
+  // in-flight DMA before every step's MFMAs.
   bf16x8 qfB[8];
-  if constexpr (PAIR) {
-    const int myB = (qb2 >= 0 ? qb2 * QB : 0) + 32 * w + lq;
-    const bool vB = qb2 >= 0 && myB < seqlen_q;
+  auto load_qB = [&](const int qbn) DAB_ALWAYS_INLINE {
+    const int myB = qbn * QB + 32 * w + lq;
+    const bool vB = myB < seqlen_q;
     const bf16* qrow = p.q + (size_t)(q_start + (vB ? myB : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
 #pragma unroll
     for (int st = 0; st < 8; ++st) {
       const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
       qfB[st] = vB ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
     }
-    if (p.rope_cs && vB) {
-      const int row = p.rope_pos[q_start + myB];
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        float4 cr[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          cr[e] = __builtin_bit_cast(
-              float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 cc = cr[j >> 1];
-          const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
-          float x1 = bf2f((uint16_t)qfB[st][j]), x2 = bf2f((uint16_t)qfB[st + 4][j]);
-          rope_rot(x1, x2, cs);
-          qfB[st][j] = (short)f2bf(x1);
-          qfB[st + 4][j] = (short)f2bf(x2);
-        }
-      }
-    }
+  };
+  if constexpr (PAIR) {
+    if (next_blk(0) >= 0) load_qB(blk_qb(next_blk(0)));
   }
   if constexpr (NBUF >= 3) {
     if (n_tiles > 1) issue(1, 1, blk_of(1));
@@ -870,15 +869,17 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
       if (pend) pv(n_tiles % NBUF == 0 ? (NBUF - 1) * BUF : -BUF, pp);  // the last tile's buffer
     }
   } else {
-    // PAIR: steps [0, nA) walk the long block's tiles, [nA, nA + nB) the short block's (tile s - nA)
-    const int nA = n_tiles;
-    const int nB = PAIR && qb2 >= 0 ? tiles_of(qb2 * QB) : 0;
-    for (int s = 0; s < nA + nB; ++s) {
-      const int t = s < nA ? s : s - nA;
+    // PAIR: the steps walk the tiles of the workgroup's blocks one after the other (tile t of block
+    // j); the DMA of the next step's tile, the next block's tile 0 at a seam, always goes out under
+    // the current step's MFMAs
+    int j = 0, t = 0, nt = n_tiles;
+    int jn = PAIR ? next_blk(0) : -1;
+    int ntn = jn >= 0 ? tiles_of(blk_qb(jn) * QB) : 0;
+    for (int s = 0; nt > 0; ++s) {
       const int buf = s & 1;
-      if (s + 1 < nA + nB) {
+      if (t + 1 < nt || jn >= 0) {
+        const int tn = t + 1 < nt ? t + 1 : 0;
         __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s + 1) & 1 (step s - 1)
-        const int tn = s + 1 < nA ? s + 1 : s + 1 - nA;
         const int blk = blk_of(tn);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
         issue(tn, buf ^ 1, blk);
@@ -893,18 +894,51 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
         kadr[i] ^= BUF;
         vadr[i] ^= BUF;
       }
-      if (PAIR && s == nA - 1 && nB > 0) {
-        epilogue();  // the long block's rows
-        set_block(qb2 * QB);
-#pragma unroll
-        for (int db = 0; db < 4; ++db)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
-        m_run = -1e30f;
-        l_run = 0.f;
-#pragma unroll
-        for (int st = 0; st < 8; ++st) qf[st] = qfB[st];  // loaded (and rotated) in the prologue
+      if (t + 1 < nt) {
+        ++t;
+        continue;
       }
+      if (!PAIR || jn < 0) break;
+      // seam: the block's rows out, the next block's state in
+      epilogue();
+      set_block(blk_qb(jn) * QB);
+#pragma unroll
+      for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+      m_run = -1e30f;
+      l_run = 0.f;
+#pragma unroll
+      for (int st = 0; st < 8; ++st) qf[st] = qfB[st];
+      rope_q = p.rope_cs && q_valid;
+      if (rope_q) {
+        // RoPE of the new block's Q, one cos / sin row group at a time (16 registers, not the
+        // prologue's 64); its loads are waited here, next to the next tile's DMA wait
+        cs_row = p.rope_pos[q_start + my_q];
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+          float4 cr[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            cr[e] = __builtin_bit_cast(
+                float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, cs_row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const float4 cc = cr[jj >> 1];
+            const float2 cs = (jj & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
+            float x1 = bf2f((uint16_t)qf[st][jj]), x2 = bf2f((uint16_t)qf[st + 4][jj]);
+            rope_rot(x1, x2, cs);
+            qf[st][jj] = (short)f2bf(x1);
+            qf[st + 4][jj] = (short)f2bf(x2);
+          }
+        }
+      }
+      j = jn;
+      t = 0;
+      nt = ntn;
+      jn = next_blk(j);
+      ntn = jn >= 0 ? tiles_of(blk_qb(jn) * QB) : 0;
+      if (jn >= 0) load_qB(blk_qb(jn));
     }
   }
   epilogue();
@@ -1290,6 +1324,7 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   prm.Hq = Hq;
   prm.Hkv = Hkv;
   prm.scale_log2 = scale * 1.4426950408889634f;
+  prm.pairs_per_wg = 1;
   // Llama prefill (D = 128 over the paged cache): the 32x32 kernel below
   if (D == 128 && paged && block_size % 64 == 0) {
     // software-pipelined V reads by default (3% faster, bit-identical: profiles/attn_vpipe_r5.md);
@@ -1308,10 +1343,19 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       return hipGetLastError();
     }
     dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
-    // DAB_FLASH_PAIR=1 (causal): one workgroup per (long, short) query-block pair (A/B)
+    // causal: one workgroup per (long, short) query-block pair by default (+8 % on 16 x 1024,
+    // bit-identical: profiles/attn_vpipe_r5.md); DAB_FLASH_PAIR=0 selects one workgroup per block
     const char* pe = std::getenv("DAB_FLASH_PAIR");
-    if (causal && vpipe && pe && pe[0] == '1') {
-      dim3 gp(((max_seqlen_q + 127) / 128 + 1) / 2, Hq, batch);
+    if (causal && vpipe && !(pe && pe[0] == '0')) {
+      // G pairs per workgroup: enough workgroups for ~2 rounds of the chip's 512 slots (2 per CU),
+      // fewer start-ups beyond that; DAB_FLASH_G overrides (A/B)
+      const int npairs = ((max_seqlen_q + 127) / 128 + 1) / 2;
+      const long wg1 = (long)npairs * Hq * batch;
+      int G = (int)(wg1 / 1024);
+      if (const char* ge = std::getenv("DAB_FLASH_G")) G = std::atoi(ge);
+      G = G < 1 ? 1 : (G > npairs ? npairs : G);
+      prm.pairs_per_wg = G;
+      dim3 gp((npairs + G - 1) / G, Hq, batch);
       hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true>), gp, dim3(256), 0, s, prm);
       return hipGetLastError();
     }
