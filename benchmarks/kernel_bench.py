@@ -153,10 +153,12 @@ def attn_suite():
     # pair = (long, short) causal query-block pairs, G per workgroup (default: G from the launch
     # size; pair-g1 / pair-g4 force G)
     arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {"DAB_FLASH_PAIR": "0"}, "pair": {},
-            "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "w8": {"DAB_FLASH_W8": "1"}}
+            "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "pair-1bar": {"DAB_FLASH_1BAR": "1"},
+            "q64": {"DAB_FLASH_Q64": "1"}, "w8": {"DAB_FLASH_W8": "1"}}
 
     def with_env(env, fn):
-        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR", "DAB_FLASH_G")}
+        old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR", "DAB_FLASH_G",
+                                           "DAB_FLASH_1BAR", "DAB_FLASH_Q64")}
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -289,11 +291,13 @@ def attn_scan():
         q = torch.randn(B * T, Hq, D, device="cuda").to(torch.bfloat16)
         cu = torch.arange(0, B * T + 1, T, dtype=torch.int32, device="cuda")
         ctx = torch.full((B,), T, dtype=torch.int32, device="cuda")
-        for causal, pair in ((True, False), (True, True), (False, False)):
+        for causal, pair in ((True, False), (True, True), (True, "q64"), (False, False), (False, "q64")):
             os.environ["DAB_FLASH_PAIR"] = "1" if pair else "0"
+            os.environ["DAB_FLASH_Q64"] = "1" if pair == "q64" else "0"
             ts = sorted(timeit(lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, T, causal=causal))
                         for _ in range(5))
             os.environ.pop("DAB_FLASH_PAIR")
+            os.environ.pop("DAB_FLASH_Q64")
             t = ts[2]
             flop = 4.0 * B * Hq * T * T * D / (2 if causal else 1)
             qb = T // 128

@@ -403,7 +403,11 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 // PAIR (causal, 4 waves): one workgroup runs query block nqb-1-i and then block i of its (sequence,
 // head), so every workgroup has 2 (nqb + 1) key tiles of work, and block i's first K / V tile and the
 // rest of its stream continue from block nqb-1-i's last tile on without a cold start (same keys).
-template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false>
+//
+// ONEBAR (4 waves): one barrier per tile instead of two.  Each wave waits for its own pieces of tile
+// t, then the barrier says both "every piece of tile t landed" and "every wave is past tile t - 1",
+// so tile t + 1's DMA goes into t - 1's buffer right after it.
+template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false, bool ONEBAR = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!STAG || NW == 8, "staggered groups: 8 waves");
@@ -877,16 +881,25 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     int ntn = jn >= 0 ? tiles_of(blk_qb(jn) * QB) : 0;
     for (int s = 0; nt > 0; ++s) {
       const int buf = s & 1;
-      if (t + 1 < nt || jn >= 0) {
-        const int tn = t + 1 < nt ? t + 1 : 0;
-        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s + 1) & 1 (step s - 1)
-        const int blk = blk_of(tn);
+      if constexpr (ONEBAR) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
-        issue(tn, buf ^ 1, blk);
+        __builtin_amdgcn_s_barrier();  // every wave's pieces of t; every wave past step s - 1
+        if (t + 1 < nt || jn >= 0) {
+          const int tn = t + 1 < nt ? t + 1 : 0;
+          issue(tn, buf ^ 1, blk_of(tn));
+        }
       } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (t + 1 < nt || jn >= 0) {
+          const int tn = t + 1 < nt ? t + 1 : 0;
+          __builtin_amdgcn_s_barrier();  // every wave is done reading buffer (s + 1) & 1 (step s - 1)
+          const int blk = blk_of(tn);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces of tile t
+          issue(tn, buf ^ 1, blk);
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile t
       }
-      __builtin_amdgcn_s_barrier();  // ... and every other wave's pieces of tile t
       const int k0 = t * KT;
       if (w_any && k0 <= w_kmax) compute(k0);  // else this wave's queries see no key of the tile
 #pragma unroll
@@ -942,6 +955,286 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     }
   }
   epilogue();
+}
+
+// -----------------------------------------------------------------------------------------------
+// Prefill attention with 64 queries per wave (Q64; A/B arm DAB_FLASH_Q64=1).  The 32-query kernel
+// above reads each wave's whole K / V tile from LDS for 32 queries: 8 waves per CU x 32 KB per tile
+// is as many LDS cycles (128 B / clk) as the tile's MFMA cycles, so LDS bandwidth and the matrix
+// cores bind together (MFMA busy ~40 % on long sequences).  Here each wave owns two 32-query halves
+// u = 0 / 1 and feeds every K / V fragment it reads to both: half the LDS bytes per FLOP.  The cost
+// is registers -- O 128, Q 64, S 64 -- so one wave per SIMD (4 waves, 256 queries per workgroup, one
+// workgroup per CU) with the whole 512-entry register file, and a 3-deep K / V ring (96 KB): tile
+// t + 2 is requested after tile t's barrier, each wave waits only for its own pieces of tile t.
+// Causal blocks are taken heavy-first.  Same math per query as flash_d128_kernel (bit-identical).
+template <bool CAUSAL>
+__global__ __launch_bounds__(256, 1) void flash_q64_kernel(FlashParams p) {
+  constexpr int D = 128, KT = 64, QB = 256;
+  constexpr int TILE = KT * D * 2;  // 16 KB
+  constexpr int BUF = 2 * TILE;     // K | V
+  constexpr int NBUF = 3;
+  constexpr int PPW = 4;            // 1-KB K (and V) pieces per wave per tile
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * BUF];
+
+  const int nqb = gridDim.x;
+  const int nwg = nqb * gridDim.y * gridDim.z;
+  const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+  const int h = (sid / nqb) % gridDim.y;
+  const int b = sid / (nqb * gridDim.y);
+  const int* bt = p.block_tables + (size_t)b * p.max_blocks;
+  const int tpb = p.block_size / KT;
+  const int bt_a = (threadIdx.x & 63) / tpb < p.max_blocks ? bt[(threadIdx.x & 63) / tpb] : 0;
+  const int bt_b = (64 + (threadIdx.x & 63)) / tpb < p.max_blocks ? bt[(64 + (threadIdx.x & 63)) / tpb] : 0;
+  const int q_start = p.cu_q[b];
+  const int seqlen_q = p.cu_q[b + 1] - q_start;
+  const int nqb_b = div_up(seqlen_q, QB);
+  const int qb = CAUSAL && sid % nqb < nqb_b ? nqb_b - 1 - sid % nqb : sid % nqb;
+  const int q0 = qb * QB;
+  if (q0 >= seqlen_q) return;  // whole workgroup
+  const int kv_len = p.ctx_k[b];
+  const int hk = h / (p.Hq / p.Hkv);
+  const int tid = threadIdx.x, lane = tid & 63, lq = lane & 31, hi = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int my_q[2], q_pos[2];
+  bool q_valid[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    my_q[u] = q0 + 64 * w + 32 * u + lq;
+    q_valid[u] = my_q[u] < seqlen_q;
+    q_pos[u] = kv_len - seqlen_q + my_q[u];
+  }
+  const int w_last_q = min(q0 + 64 * w + 63, seqlen_q - 1);
+  const int w_kmax = CAUSAL ? kv_len - seqlen_q + w_last_q : kv_len - 1;
+  const bool w_any = q0 + 64 * w < seqlen_q;
+
+  bf16x8 qf[2][8];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const bf16* qrow =
+        p.q + (size_t)(q_start + (q_valid[u] ? my_q[u] : 0)) * p.q_stride_tok + (size_t)h * p.q_stride_head;
+#pragma unroll
+    for (int st = 0; st < 8; ++st) {
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      qf[u][st] = q_valid[u] ? *reinterpret_cast<const bf16x8*>(qrow + 16 * st + 8 * hi) : z;
+    }
+  }
+  if (p.rope_cs) {  // RoPE of Q on load, one cos / sin row group at a time
+    const auto cs_rs = __builtin_amdgcn_make_buffer_rsrc((void*)p.rope_cs, (short)0, 0x7ffffff0, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (!q_valid[u]) continue;
+      const int row = p.rope_pos[q_start + my_q[u]];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        float4 cr[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          cr[e] = __builtin_bit_cast(
+              float4, __builtin_amdgcn_raw_buffer_load_b128(cs_rs, row * 512 + ((16 * st + 8 * hi) / 2 + e) * 16, 0, 0));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 cc = cr[j >> 1];
+          const float2 cs = (j & 1) ? make_float2(cc.z, cc.w) : make_float2(cc.x, cc.y);
+          float x1 = bf2f((uint16_t)qf[u][st][j]), x2 = bf2f((uint16_t)qf[u][st + 4][j]);
+          rope_rot(x1, x2, cs);
+          qf[u][st][j] = (short)f2bf(x1);
+          qf[u][st + 4][j] = (short)f2bf(x2);
+        }
+      }
+    }
+  }
+
+  int n_keys = kv_len;
+  if (CAUSAL) {
+    const int last_q = min(q0 + QB - 1, seqlen_q - 1);
+    n_keys = min(kv_len, kv_len - seqlen_q + last_q + 1);
+  }
+  const int n_tiles = div_up(n_keys, KT);
+
+  const int st_row = lane >> 4, st_pc = lane & 15;
+  auto blk_of = [&](int t) {
+    if (t < 64) return __builtin_amdgcn_readlane(bt_a, t);
+    if (t < 128) return __builtin_amdgcn_readlane(bt_b, t - 64);
+    return __builtin_amdgcn_readfirstlane(((volatile const int*)bt)[t / tpb]);
+  };
+  auto issue = [&](int t, int buf, int blk) {
+    const int k0 = t * KT;
+    const int nvalid = min(KT, kv_len - k0);
+    const size_t base = (((size_t)blk * p.Hkv + hk) * p.block_size + (k0 % p.block_size)) * D;
+    const auto rk = __builtin_amdgcn_make_buffer_rsrc((void*)(p.k_cache + base), (short)0, nvalid * D * 2, 0x00020000);
+    const auto rv = __builtin_amdgcn_make_buffer_rsrc((void*)(p.v_cache + base), (short)0, nvalid * D * 2, 0x00020000);
+    char* kdst = smem + buf * BUF;
+#pragma unroll
+    for (int j = 0; j < PPW; ++j) {
+      const int i = PPW * w + j;
+      const int row = 4 * i + st_row;
+      const unsigned off = (unsigned)(row * D + 8 * (st_pc ^ f128(row))) * 2u;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(kdst + i * 1024), 16, off,
+                                               0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(kdst + TILE + i * 1024),
+                                               16, off, 0, 0, 0);
+    }
+  };
+
+  f32x16 o[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[u][db][r] = 0.f;
+  float m_run[2] = {-1e30f, -1e30f}, l_run[2] = {0.f, 0.f};
+  const float sc = p.scale_log2;
+
+  const unsigned smem0 = lds_addr(smem);
+  unsigned kadr[8];
+  {
+    const int fr = f128(lq);
+#pragma unroll
+    for (int st = 0; st < 8; ++st) kadr[st] = smem0 + lq * 256 + 16 * ((2 * st + hi) ^ fr);
+  }
+  unsigned vadr[8];
+  {
+    const int G = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+    const int r0 = 4 * (G >> 1) + qq;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      const int c = 4 * db + 2 * (G & 1) + (pp >> 1);
+      const int boff = 8 * (pp & 1);
+      vadr[2 * db] = smem0 + TILE + r0 * 256 + 16 * (c ^ f128(r0)) + boff;
+      vadr[2 * db + 1] = smem0 + TILE + (r0 + 8) * 256 + 16 * (c ^ f128(r0 + 8)) + boff;
+    }
+  }
+
+  auto compute = [&](const int k0) DAB_ALWAYS_INLINE {
+    // ---- S^T = K Q^T for both halves: each K fragment feeds two MFMAs
+    f32x16 s0[2], s1[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s0[u][r] = s1[u][r] = 0.f;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      bf16x8 ka[4], kb2[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const auto* kp = (const __attribute__((address_space(3))) bf16x8*)(uintptr_t)(kadr[4 * half + i]);
+        ka[i] = kp[0];
+        kb2[i] = kp[8192 / 16];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          s0[u] = mfma32(ka[i], qf[u][4 * half + i], s0[u]);
+          s1[u] = mfma32(kb2[i], qf[u][4 * half + i], s1[u]);
+        }
+    }
+    const bool need_mask = k0 + KT > kv_len || (CAUSAL && k0 + KT - 1 > kv_len - seqlen_q + q0);
+    bf16x8 pf[2][4];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (need_mask) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+          if (key >= kv_len || (CAUSAL && key > q_pos[u])) s0[u][r] = kNegInf;
+          if (key + 32 >= kv_len || (CAUSAL && key + 32 > q_pos[u])) s1[u][r] = kNegInf;
+        }
+      }
+      float mx = kNegInf;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[u][r], s1[u][r]));
+      mx = fmaxf(mx, xor32(mx));
+      const float mxs = mx * sc;
+      const bool keep = __all(mxs - m_run[u] <= kDeferLog2);
+      const float m_new = keep ? m_run[u] : fmaxf(m_run[u], mxs);
+      const float alpha = __builtin_amdgcn_exp2f(m_run[u] - m_new);
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[u][r] = __builtin_amdgcn_exp2f(fmaf(s0[u][r], sc, -m_new));
+        s1[u][r] = __builtin_amdgcn_exp2f(fmaf(s1[u][r], sc, -m_new));
+        ls += s0[u][r] + s1[u][r];
+      }
+      l_run[u] = l_run[u] * alpha + ls;
+      m_run[u] = m_new;
+      if (!keep && __any(alpha < 1.f)) {
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[u][db] *= alpha;
+      }
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f32x16& sv = (ks >> 1) ? s1[u] : s0[u];
+        const int ss = ks & 1;
+        u32x4 pu;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) pu[e] = pack2bf(sv[8 * ss + 2 * e], sv[8 * ss + 2 * e + 1]);
+        pf[u][ks] = __builtin_bit_cast(bf16x8, pu);
+      }
+    }
+    // ---- O^T += V^T P^T for both halves: each transposed V fragment feeds two MFMAs
+    static_for<0, 4>([&](auto KS_) DAB_ALWAYS_INLINE {
+      constexpr int ks = decltype(KS_)::value;
+      u32x2 tr[8];
+      ds_tr16_x8<(ks >> 1) * 8192 + (ks & 1) * 4096>(vadr, tr);
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        u32x4 uu;
+        uu[0] = tr[2 * db][0];
+        uu[1] = tr[2 * db][1];
+        uu[2] = tr[2 * db + 1][0];
+        uu[3] = tr[2 * db + 1][1];
+        const bf16x8 va = __builtin_bit_cast(bf16x8, uu);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) o[u][db] = mfma32(va, pf[u][ks], o[u][db]);
+      }
+      return true;
+    });
+  };
+
+  if (n_tiles > 0) issue(0, 0, blk_of(0));
+  if (n_tiles > 1) issue(1, 1, blk_of(1));
+  // Q is consumed here, behind the first two tiles' DMA (a counted wait hipcc computes in this
+  // straight-line prologue): with its first use inside the loop, hipcc put a vmcnt(0) there that
+  // drained the in-flight tile on every step
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int st = 0; st < 8; ++st) asm volatile("" ::"v"(qf[u][st]));
+  for (int t = 0; t < n_tiles; ++t) {
+    if (t + 1 < n_tiles) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(2 * PPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < n_tiles) issue(t + 2, (t + 2) % NBUF, blk_of(t + 2));
+    const int k0 = t * KT;
+    if (w_any && k0 <= w_kmax) compute(k0);
+    const int adv = (t % NBUF == NBUF - 1) ? -(NBUF - 1) * BUF : BUF;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      kadr[i] += adv;
+      vadr[i] += adv;
+    }
+  }
+
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const float l_tot = l_run[u] + __shfl_xor(l_run[u], 32, 64);
+    if (!q_valid[u]) continue;
+    const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+    bf16* orow = p.out + (size_t)(q_start + my_q[u]) * p.o_stride_tok + (size_t)h * p.o_stride_head;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        u32x2 v;
+        v[0] = pack2bf(o[u][db][4 * rg] * inv, o[u][db][4 * rg + 1] * inv);
+        v[1] = pack2bf(o[u][db][4 * rg + 2] * inv, o[u][db][4 * rg + 3] * inv);
+        *reinterpret_cast<u32x2*>(orow + 32 * db + 8 * rg + 4 * hi) = v;
+      }
+  }
 }
 
 // -----------------------------------------------------------------------------------------------
@@ -1343,6 +1636,14 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       return hipGetLastError();
     }
     dim3 g32((max_seqlen_q + 127) / 128, Hq, batch);
+    // DAB_FLASH_Q64=1: 64 queries per wave, one wave per SIMD (A/B)
+    const char* q64 = std::getenv("DAB_FLASH_Q64");
+    if (q64 && q64[0] == '1') {
+      dim3 gq((max_seqlen_q + 255) / 256, Hq, batch);
+      if (causal) hipLaunchKernelGGL((flash_q64_kernel<true>), gq, dim3(256), 0, s, prm);
+      else hipLaunchKernelGGL((flash_q64_kernel<false>), gq, dim3(256), 0, s, prm);
+      return hipGetLastError();
+    }
     // causal: one workgroup per (long, short) query-block pair by default (+8 % on 16 x 1024,
     // bit-identical: profiles/attn_vpipe_r5.md); DAB_FLASH_PAIR=0 selects one workgroup per block
     const char* pe = std::getenv("DAB_FLASH_PAIR");
@@ -1356,7 +1657,11 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       G = G < 1 ? 1 : (G > npairs ? npairs : G);
       prm.pairs_per_wg = G;
       dim3 gp((npairs + G - 1) / G, Hq, batch);
-      hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true>), gp, dim3(256), 0, s, prm);
+      const char* ob = std::getenv("DAB_FLASH_1BAR");  // A/B: one barrier per tile
+      if (ob && ob[0] == '1')
+        hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, true>), gp, dim3(256), 0, s, prm);
+      else
+        hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true>), gp, dim3(256), 0, s, prm);
       return hipGetLastError();
     }
     if (causal && vpipe) hipLaunchKernelGGL((flash_d128_kernel<true, true>), g32, dim3(256), 0, s, prm);
