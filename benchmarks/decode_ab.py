@@ -47,6 +47,11 @@ ARMS = {
     "down11_4": {"down": (11, 4)},
     "qkv9_2": {"qkv": (9, 2)},
     "od9_4": {"o": (9, 4), "down": (9, 4)},
+    # batch 65-128: narrow tiles at 2 K-slices (stream_gemm cfg 34 BN 32, 35 BN 48)
+    "o34_2": {"o": (34, 2)},
+    "down34_2": {"down": (34, 2)},
+    "qkv35_2": {"qkv": (35, 2)},
+    "narrow": {"o": (34, 2), "down": (34, 2), "qkv": (35, 2)},
     "part1024": {"_part": 1024},
     "part512": {"_part": 512},
     "m16via13": {"_m16": 13},                # batches <= 16 on the M <= 64 configuration (cfg 13)

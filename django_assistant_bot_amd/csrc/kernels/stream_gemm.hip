@@ -419,6 +419,10 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // weight ring per compute wave
     {1, 1, 1, 4, 8, 1, true, 0, 1},  // 32: BN 16, 1 compute + 1 loader wave
     {1, 1, 1, 4, 8, 1, true, 0, 2},  // 33: BN 32, 2 compute + 1 loader wave
+    // M <= 128 with narrow tiles, so the small projections reach 256 workgroups at 2 K-slices
+    // instead of 4-8 (a quarter of the fp32 slab bytes): 8-stage weight ring per compute wave
+    {8, 1, 1, 4, 8, 2, true, 0, 2},  // 34: BN 32, 2 compute + 2 loader waves (o / down 4096 x S2)
+    {8, 1, 1, 4, 8, 2, true, 0, 3},  // 35: BN 48, 3 + 2 waves (qkv 6144 x S2)
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
