@@ -1238,6 +1238,209 @@ __global__ __launch_bounds__(256, 1) void flash_q64_kernel(FlashParams p) {
 }
 
 // -----------------------------------------------------------------------------------------------
+// Persistent encoder attention (ENC_P; A/B arm DAB_ENC_PERSIST=1): D 64, packed varlen,
+// bidirectional, the embed path's ~50-token chunks.  flash_fwd_kernel runs one workgroup per
+// (query block, head, sequence): at ~50 tokens that is a single tile, and each workgroup's life is one
+// dependent chain (sequence bounds -> Q / K / V loads -> LDS -> MFMAs -> stores) with nothing to
+// overlap it.  Here a workgroup walks (sequence, head) items with a grid stride, and the next step's
+// K / V tile and Q (the next item's, at an item seam) are loaded into registers while the current
+// step computes, so the load round trip hides under the previous item's math and stores.
+// Same per-query math as flash_fwd_kernel<64, false, false, 4, 1> (bit-identical).
+__global__ __launch_bounds__(256, 5) void flash_enc_kernel(FlashParams p, int n_items) {
+  constexpr int D = 64, KT = 64, NT = 256, QB = 64;
+  constexpr int NKK = D / 32, NTD = D / 16, CPR = D / 8;
+  constexpr int TILE_BYTES = KT * D * 2;
+  constexpr int CH = KT * CPR / NT;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+  char* ks = smem;
+  char* vs = smem + TILE_BYTES;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int H = p.Hq;
+
+  // the item / step being computed (c_*) and the one being loaded (n_*)
+  struct Step {
+    int it, qb, kt;
+    int b, h, q_start, seqlen_q, k_start, kv_len, nqb, nkt;
+  };
+  auto item_of = [&](Step& s, const int it) DAB_ALWAYS_INLINE {
+    s.it = it;
+    s.b = it / H;
+    s.h = it - s.b * H;
+    s.q_start = p.cu_q[s.b];
+    s.seqlen_q = p.cu_q[s.b + 1] - s.q_start;
+    s.k_start = p.cu_k[s.b];
+    s.kv_len = p.cu_k[s.b + 1] - s.k_start;
+    s.nqb = div_up(s.seqlen_q, QB);
+    s.nkt = div_up(s.kv_len, KT);
+    s.qb = 0;
+    s.kt = 0;
+  };
+  u32x4 kreg[CH], vreg[CH];
+  auto load_tile = [&](const Step& s) DAB_ALWAYS_INLINE {
+    const int k0 = s.kt * KT;
+    const int last = s.kv_len - 1 - k0;
+    const int hk = s.h / (p.Hq / p.Hkv);
+    const size_t base = (size_t)(s.k_start + k0) * p.kv_stride_tok + (size_t)hk * p.kv_stride_head;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * NT;
+      const int row = min(idx / CPR, last), ch = idx % CPR;
+      const size_t off = base + (size_t)row * p.kv_stride_tok + ch * 8;
+      kreg[c] = *reinterpret_cast<const u32x4*>(p.k + off);
+      vreg[c] = *reinterpret_cast<const u32x4*>(p.v + off);
+    }
+  };
+  auto store_tile = [&]() DAB_ALWAYS_INLINE {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int idx = tid + c * NT;
+      const int row = idx / CPR, ch = idx % CPR;
+      *reinterpret_cast<u32x4*>(ks + swz<D>(row, ch)) = kreg[c];
+      *reinterpret_cast<u32x4*>(vs + swz<D>(row, ch)) = vreg[c];
+    }
+  };
+  bf16x8 qf[NKK], qn[NKK];
+  auto load_q = [&](const Step& s, bf16x8 (&dst)[NKK]) DAB_ALWAYS_INLINE {
+    const int mq = s.qb * QB + 16 * w + li;
+    const bool v = mq < s.seqlen_q;
+    const bf16* qrow = p.q + (size_t)(s.q_start + (v ? mq : 0)) * p.q_stride_tok + (size_t)s.h * p.q_stride_head;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk) {
+      const bf16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+      dst[kk] = v ? *reinterpret_cast<const bf16x8*>(qrow + 32 * kk + 8 * g) : z;
+    }
+  };
+  // the step after s (same item: next tile / next query block; else the next item), or it = -1
+  auto advance = [&](Step& s) DAB_ALWAYS_INLINE {
+    if (s.kt + 1 < s.nkt) {
+      ++s.kt;
+    } else if (s.qb + 1 < s.nqb) {
+      ++s.qb;
+      s.kt = 0;
+    } else {
+      const int nit = s.it + (int)gridDim.x;
+      if (nit < n_items) item_of(s, nit);
+      else s.it = -1;
+    }
+  };
+
+  if ((int)blockIdx.x >= n_items) return;
+  Step c;
+  item_of(c, blockIdx.x);
+  load_q(c, qf);
+  load_tile(c);
+  f32x4 o[NTD];
+#pragma unroll
+  for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -1e30f, l_run = 0.f;
+  for (;;) {
+    __syncthreads();  // every wave is past the previous step's LDS reads
+    store_tile();
+    __syncthreads();
+    Step n = c;
+    advance(n);
+    const bool new_q = n.it >= 0 && n.kt == 0;  // the next step starts a query block
+    if (n.it >= 0) load_tile(n);
+    if (new_q) load_q(n, qn);
+    // ---- compute tile c.kt of query block c.qb (flash_fwd_kernel's math, QT = 1)
+    {
+      const int kt = c.kt;
+      const int my_q = c.qb * QB + 16 * w + li;
+      f32x4 s[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        s[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(ks + swz<D>(16 * m + li, 4 * kk + g));
+          s[m] = mfma16(a, qf[kk], s[m]);
+        }
+      }
+      const bool need_mask = (kt + 1) * KT > c.kv_len;
+      float mx = kNegInf;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float v = s[m][r] * p.scale_log2;
+          if (need_mask && kt * KT + 16 * m + 4 * g + r >= c.kv_len) v = kNegInf;
+          s[m][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const bool keep = __all(mx - m_run <= kDeferLog2);
+      const float m_new = keep ? m_run : fmaxf(m_run, mx);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+      float ls = 0.f;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float e = __builtin_amdgcn_exp2f(s[m][r] - m_new);
+          s[m][r] = e;
+          ls += e;
+        }
+      }
+      l_run = l_run * alpha + ls;
+      m_run = m_new;
+      bf16x8 pb[2];
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pb[ss][j] = (short)f2bf(s[2 * ss][j]);
+          pb[ss][j + 4] = (short)f2bf(s[2 * ss + 1][j]);
+        }
+      if (!keep) {
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) o[t] *= alpha;
+      }
+      const int qq = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) {
+          const int ch = 2 * t + (pp >> 1);
+          const int boff = 8 * (pp & 1);
+          const bf16x4 lo = ds_read_tr16(vs + swz<D>(32 * ss + 4 * g + qq, ch) + boff);
+          const bf16x4 hi = ds_read_tr16(vs + swz<D>(32 * ss + 16 + 4 * g + qq, ch) + boff);
+          const bf16x8 a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          o[t] = mfma16(a, pb[ss], o[t]);
+        }
+      }
+      if (kt + 1 == c.nkt) {  // the query block is complete: its rows out, the state reset
+        float l_tot = l_run;
+        l_tot += __shfl_xor(l_tot, 16, 64);
+        l_tot += __shfl_xor(l_tot, 32, 64);
+        if (my_q < c.seqlen_q) {
+          const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+          bf16* orow = p.out + (size_t)(c.q_start + my_q) * p.o_stride_tok + (size_t)c.h * p.o_stride_head;
+#pragma unroll
+          for (int t = 0; t < NTD; ++t) {
+            u32x2 v;
+            v[0] = pack2bf(o[t][0] * inv, o[t][1] * inv);
+            v[1] = pack2bf(o[t][2] * inv, o[t][3] * inv);
+            *reinterpret_cast<u32x2*>(orow + 16 * t + 4 * g) = v;
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < NTD; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        m_run = -1e30f;
+        l_run = 0.f;
+      }
+    }
+    if (n.it < 0) break;
+    if (new_q) {
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) qf[kk] = qn[kk];
+    }
+    c = n;
+  }
+}
+
+// -----------------------------------------------------------------------------------------------
 // Paged decode.  grid = (max_parts, Hkv, B); one workgroup reduces keys [part*part_size, +part_size)
 // of one (sequence, kv head) for all G = Hq/Hkv query heads of the GQA group (the MFMA N dimension,
 // padded to 16).  Each wave streams 32-key sub-tiles through a private LDS slot (no block barriers in
@@ -1674,6 +1877,15 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
   // Long D = 128 sequences: 128-query blocks of 8 waves x 16 queries halve the K/V tile traffic per
   // query (16x1024 causal: 298 -> 355 TFLOP/s); the encoder (D <= 64) runs 64-query blocks of 4
   // waves (8 waves measured 5 % slower there; a 4-wave x 2-sub-tile form was no faster either)
+  // DAB_ENC_PERSIST=1: the persistent encoder kernel (D 64, packed, bidirectional; A/B)
+  if (const char* ep = std::getenv("DAB_ENC_PERSIST")) {
+    if (ep[0] == '1' && D == 64 && !paged && !causal && !rope_cs) {
+      const int items = batch * Hq;
+      const int grid = items < 256 * 5 ? items : 256 * 5;
+      hipLaunchKernelGGL(flash_enc_kernel, dim3(grid), dim3(256), 0, s, prm, items);
+      return hipGetLastError();
+    }
+  }
   const bool wide = D == 128 && max_seqlen_q > 64;
   // the 5-waves-per-SIMD encoder variant by default (3 % faster on the embed bench's packed batch,
   // bit-identical: profiles/embed_r5.md); DAB_ENC_W5=0 selects the unbounded-register kernel

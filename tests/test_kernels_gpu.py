@@ -978,7 +978,7 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
 
 @pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2"),
                                      ("DAB_FLASH_PAIR", "0"), ("DAB_FLASH_G", "3"), ("DAB_FLASH_1BAR", "1"),
-                                     ("DAB_FLASH_Q64", "1")])
+                                     ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1")])
 def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
@@ -986,7 +986,7 @@ def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     (a different wave -> query mapping, same per-query math) bit for bit as well, and so does the
     paired-block causal kernel (both blocks of a pair, odd block counts, a 1-token sequence)."""
     g = torch.Generator().manual_seed(3)
-    if env == "DAB_ENC_W5":
+    if env in ("DAB_ENC_W5", "DAB_ENC_PERSIST"):
         lens = torch.randint(20, 140, (37,), generator=g)
         cu = torch.zeros(38, dtype=torch.int32)
         cu[1:] = torch.cumsum(lens, 0)
