@@ -52,6 +52,14 @@ ARMS = {
     "down34_2": {"down": (34, 2)},
     "qkv35_2": {"qkv": (35, 2)},
     "narrow": {"o": (34, 2), "down": (34, 2), "qkv": (35, 2)},
+    # batch 65-128: two workgroups per CU (cfg 36 / 37, BN 64, 2-stage X ring)
+    "o36_8": {"o": (36, 8)},
+    "down36_8": {"down": (36, 8)},
+    "qkv36_4": {"qkv": (36, 4)},
+    "qkv36_8": {"qkv": (36, 8)},
+    "o37_8": {"o": (37, 8)},
+    "down37_8": {"down": (37, 8)},
+    "occ2": {"o": (36, 8), "down": (36, 8), "qkv": (36, 4)},
     "part1024": {"_part": 1024},
     "part512": {"_part": 512},
     "m16via13": {"_m16": 13},                # batches <= 16 on the M <= 64 configuration (cfg 13)

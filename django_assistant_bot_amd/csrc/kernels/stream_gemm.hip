@@ -423,6 +423,10 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // instead of 4-8 (a quarter of the fp32 slab bytes): 8-stage weight ring per compute wave
     {8, 1, 1, 4, 8, 2, true, 0, 2},  // 34: BN 32, 2 compute + 2 loader waves (o / down 4096 x S2)
     {8, 1, 1, 4, 8, 2, true, 0, 3},  // 35: BN 48, 3 + 2 waves (qkv 6144 x S2)
+    // M <= 128, two workgroups per CU: a 2-stage X ring (64 KB of LDS) and one row tile per compute
+    // wave (~134 registers), so one workgroup's pipeline fill / drain overlaps the other's stream
+    {8, 1, 1, 2, 3, 2, true, 0, 4},  // 36: BN 64, 4 compute + 2 loader waves, 3-stage weight ring
+    {8, 1, 1, 2, 4, 2, true, 0, 4},  // 37: = 36 with a 4-stage weight ring
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 

@@ -423,7 +423,7 @@ def test_gemm_swiglu():
 
 
 @pytest.mark.parametrize("cfg,M,N,K,S", _stream_cases(
-    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30, 31, 32, 33, 34, 35],
+    list(range(17)) + [20, 21, 22, 23, 25, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37],
     [1, 16, 30, 37, 64, 100, 128, 200, 256],
     [(256, 512, 1), (384, 1024, 4), (128, 1792, 7), (256, 4096, 16), (512, 1280, 1), (672, 512, 1),
      (1344, 1024, 4), (2688, 1792, 7)]))
