@@ -153,12 +153,12 @@ def attn_suite():
     # pair = (long, short) causal query-block pairs, G per workgroup (default: G from the launch
     # size; pair-g1 / pair-g4 force G)
     arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {"DAB_FLASH_PAIR": "0"}, "pair": {},
-            "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "pair-1bar": {"DAB_FLASH_1BAR": "1"},
+            "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "pair-1bar": {"DAB_FLASH_1BAR": "1"}, "pair-sms": {"DAB_FLASH_SMS": "1"},
             "q64": {"DAB_FLASH_Q64": "1"}, "w8": {"DAB_FLASH_W8": "1"}}
 
     def with_env(env, fn):
         old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR", "DAB_FLASH_G",
-                                           "DAB_FLASH_1BAR", "DAB_FLASH_Q64")}
+                                           "DAB_FLASH_1BAR", "DAB_FLASH_Q64", "DAB_FLASH_SMS")}
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env)

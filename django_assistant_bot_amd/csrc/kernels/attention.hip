@@ -407,7 +407,14 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 // ONEBAR (4 waves): one barrier per tile instead of two.  Each wave waits for its own pieces of tile
 // t, then the barrier says both "every piece of tile t landed" and "every wave is past tile t - 1",
 // so tile t + 1's DMA goes into t - 1's buffer right after it.
-template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false, bool ONEBAR = false>
+//
+// SMS (with VPIPE): the softmax split across the PV k-steps -- the row maximum first, then the
+// exponentials of k-step ks + 1's 16 keys issued behind k-step ks's MFMAs, so the transcendental
+// work of one slice runs beside the matrix cores instead of all of it before them (the
+// 'sm-split' of cdna_hip_programming.md Appendix B).  The row sum accumulates slice by slice (a
+// different fp32 summation order than the unsplit kernel: equal to within a bf16 rounding).
+template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false, bool ONEBAR = false,
+          bool SMS = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!STAG || NW == 8, "staggered groups: 8 waves");
@@ -645,15 +652,29 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
     // raw v_exp_f32 (exp2f adds a denormal-range fix-up around each one; results below 2^-126 are
     // irrelevant next to the row maximum's 1)
     const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
-    float ls = 0.f;
+    // exponentials of k-step ks (registers 8 ss .. 8 ss + 7 of S block kb)
+    float ls_sms = 0.f;  // SMS: the row sum, slice by slice
+    auto exp_slice = [&](const int ks) DAB_ALWAYS_INLINE {
+      f32x16& sv = (ks >> 1) ? s1 : s0;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], sc, -m_new));
-      s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], sc, -m_new));
-      ls += s0[r] + s1[r];
+      for (int j = 0; j < 8; ++j) {
+        sv[8 * (ks & 1) + j] = __builtin_amdgcn_exp2f(fmaf(sv[8 * (ks & 1) + j], sc, -m_new));
+        ls_sms += sv[8 * (ks & 1) + j];
+      }
+    };
+    if constexpr (!(SMS && VPIPE)) {
+      float ls = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = __builtin_amdgcn_exp2f(fmaf(s0[r], sc, -m_new));
+        s1[r] = __builtin_amdgcn_exp2f(fmaf(s1[r], sc, -m_new));
+        ls += s0[r] + s1[r];
+      }
+      l_run = l_run * alpha + ls;
+      m_run = m_new;
+    } else {
+      exp_slice(0);  // the rest go out one k-step ahead inside the PV loop
     }
-    l_run = l_run * alpha + ls;
-    m_run = m_new;
     if (!keep && __any(alpha < 1.f)) {  // the running max moved for some query of the wave
 #pragma unroll
       for (int db = 0; db < 4; ++db) o[db] *= alpha;
@@ -696,8 +717,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
         u[3] = tr[2 * db + 1][1];
         o[db] = mfma32(__builtin_bit_cast(bf16x8, u), pf, o[db]);
       }
+      if constexpr (SMS && VPIPE && ks < 3) exp_slice(ks + 1);  // beside this k-step's MFMAs
       return true;
     });
+    if constexpr (SMS && VPIPE) {
+      l_run = l_run * alpha + ls_sms;  // (summed in slice order: l differs from the unsplit form in
+      m_run = m_new;                    // its last fp32 bits, the output by at most a bf16 rounding)
+    }
   };
 
   // ---- epilogue: O[q][d], d = 32 db + (r & 3) + 8 (r >> 2) + 4 hi
@@ -1861,7 +1887,10 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       prm.pairs_per_wg = G;
       dim3 gp((npairs + G - 1) / G, Hq, batch);
       const char* ob = std::getenv("DAB_FLASH_1BAR");  // A/B: one barrier per tile
-      if (ob && ob[0] == '1')
+      const char* sm = std::getenv("DAB_FLASH_SMS");   // A/B: softmax split across the PV k-steps
+      if (sm && sm[0] == '1')
+        hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, false, true>), gp, dim3(256), 0, s, prm);
+      else if (ob && ob[0] == '1')
         hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, true>), gp, dim3(256), 0, s, prm);
       else
         hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true>), gp, dim3(256), 0, s, prm);

@@ -978,7 +978,7 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
 
 @pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2"),
                                      ("DAB_FLASH_PAIR", "0"), ("DAB_FLASH_G", "3"), ("DAB_FLASH_1BAR", "1"),
-                                     ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1")])
+                                     ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1"), ("DAB_FLASH_SMS", "1")])
 def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
@@ -1013,6 +1013,9 @@ def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     monkeypatch.setenv(env, val)
     out = run()
     torch.cuda.synchronize()
-    assert torch.equal(out, base)
+    if env == "DAB_FLASH_SMS":  # (the row sum in slice order: equal to within a bf16 rounding)
+        close(out, base, atol=1e-2, rtol=1e-2)
+    else:
+        assert torch.equal(out, base)
     if exp is not None:
         close(out, exp)
