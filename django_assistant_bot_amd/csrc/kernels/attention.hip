@@ -438,8 +438,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   // beside the cu_q / ctx_k loads instead of after them (in-bounds for any row: lane / tpb < max_blocks)
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   const int tpb = p.block_size / KT;  // tiles per cache block
-  const int bt_a = (threadIdx.x & 63) / tpb < p.max_blocks ? bt[(threadIdx.x & 63) / tpb] : 0;
-  const int bt_b = (64 + (threadIdx.x & 63)) / tpb < p.max_blocks ? bt[(64 + (threadIdx.x & 63)) / tpb] : 0;
+  const int bl = (int)(threadIdx.x & 63);
+  const int bt_a = bl / tpb < p.max_blocks ? bt[bl / tpb] : 0;
+  const int bt_b = (64 + bl) / tpb < p.max_blocks ? bt[(64 + bl) / tpb] : 0;
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
   // causal: a sequence's last query block (the most key tiles) starts first, so the short blocks
@@ -1011,8 +1012,9 @@ __global__ __launch_bounds__(256, 1) void flash_q64_kernel(FlashParams p) {
   const int b = sid / (nqb * gridDim.y);
   const int* bt = p.block_tables + (size_t)b * p.max_blocks;
   const int tpb = p.block_size / KT;
-  const int bt_a = (threadIdx.x & 63) / tpb < p.max_blocks ? bt[(threadIdx.x & 63) / tpb] : 0;
-  const int bt_b = (64 + (threadIdx.x & 63)) / tpb < p.max_blocks ? bt[(64 + (threadIdx.x & 63)) / tpb] : 0;
+  const int bl = (int)(threadIdx.x & 63);
+  const int bt_a = bl / tpb < p.max_blocks ? bt[bl / tpb] : 0;
+  const int bt_b = (64 + bl) / tpb < p.max_blocks ? bt[(64 + bl) / tpb] : 0;
   const int q_start = p.cu_q[b];
   const int seqlen_q = p.cu_q[b + 1] - q_start;
   const int nqb_b = div_up(seqlen_q, QB);
