@@ -560,7 +560,10 @@ def main():
                      if args.qps > 0 else
                      f"serve (closed loop, {B} in flight per replica, admit {G}, mixed {args.mixed_tokens})"),
             "index_rows": n_rows,
-            "index": "replicated per GPU" if (serve or overlap) else "sharded (all_to_all merge)",
+            # what ran: without a process group (world 1, no DAB_FORCE_GROUP) ShardedIndex.search
+            # takes its local path and no collective is issued
+            "index": ("replicated per GPU" if (serve or overlap) else
+                      "sharded (all_to_all merge)" if index.distributed else "single shard, local top-k (no collective)"),
             "docs_per_prompt": round(float(np.mean(n_docs_used)), 2) if n_docs_used else 0,
             "sampling": "temperature=1.0 top_k=50 top_p=0.95 ignore_eos",
             "graphs": llm.use_graphs,

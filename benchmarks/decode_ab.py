@@ -142,6 +142,11 @@ def main():
             eng.model.STREAM_CFG_M16 = spec.get("_m16", type(eng.model).STREAM_CFG_M16)
             eng.model.STREAM_CFG_M32 = spec.get("_m32", type(eng.model).STREAM_CFG_M32)
             eng.model.small_norm_fused = spec.get("_fuse", False)
+            if eng.model.small_norm_fused:
+                # random init: unit RMSNorm gains, so the weights are already "folded" (W diag(1) = W)
+                assert all(bool(torch.all(L.attn_norm == 1)) and bool(torch.all(L.mlp_norm == 1))
+                           for L in eng.model.layers)
+                eng.model.fold_norms = eng.model.frag
             eng.model.l3_warm_mb = spec.get("_warm", type(eng.model).l3_warm_mb)
             eng.model.l3_warm_blocks = spec.get("_warm_blocks", type(eng.model).l3_warm_blocks)
             eng.model.STREAM_CFG_RES16 = spec.get("_res_cfg", type(eng.model).STREAM_CFG_RES16)

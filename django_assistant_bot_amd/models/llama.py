@@ -80,7 +80,7 @@ class LlamaModel:
 
     def __init__(self, cfg: DecoderConfig, weights: dict, device, tp_group=None, tp_size: int = 1,
                  interleaved_mlp: bool = False, fragment_layout: bool = True, consume: bool = False,
-                 tp_rank: int | None = None, vocab_parallel: bool = True):
+                 tp_rank: int | None = None, vocab_parallel: bool = True, small_norm_fused: bool | None = None):
         """``consume``: the entries of ``weights`` are popped as the model takes them over, so each
         original is freed as soon as its fragment-layout copy exists (peak HBM = model + one
         tensor: 70B at TP 1 needs it, 2 x 140 GB would not fit in 288 GB).
@@ -134,11 +134,15 @@ class LlamaModel:
             head = head.contiguous()
         self.lm_head = ops.shuffle_weights(head) if self.frag else head
         del head
-        # GPU: the attention / MLP RMSNorm gains live in the columns of the projection each norm feeds
-        # (rmsnorm(x) g W^T = rmsnorm(x) (W diag g)^T), the norms themselves run with unit gains.
-        # Small decode batches then normalise inside the consumer GEMM (``_layer_small``); the
-        # prefill / large-batch paths are unchanged apart from where g is applied.
-        self.fold_norms = self.frag
+        # ``small_norm_fused`` (opt-in, measured slower: profiles/decode_small_r5.md): the attention /
+        # MLP RMSNorm gains move into the columns of the projection each norm feeds
+        # (rmsnorm(x) g W^T = rmsnorm(x) (W diag g)^T) and the norms run with unit gains, so small
+        # decode batches can normalise inside the consumer GEMM (``_layer_small``).  The fold is one
+        # more bf16 rounding of W diag(g), so the default model keeps the reference norm -> GEMM
+        # order and does not fold.
+        if small_norm_fused is not None:
+            self.small_norm_fused = bool(small_norm_fused)
+        self.fold_norms = self.frag and self.small_norm_fused
         self.layers = []
         for i in range(cfg.layers):
             an = take(f"l{i}.attn_norm").to(self.device)

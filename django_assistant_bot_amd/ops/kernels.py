@@ -762,32 +762,25 @@ def topk_rows(scores, k, index_base=0, want_global=False):
 
 def linear(x, w, b=None, residual=None, act=None):
     """y = x W^T (+b) (+act) (+residual) on the native MFMA GEMMs (``gemm_bt``: the phased 256x256
-    kernel for large token counts, the 128x128 kernel otherwise), epilogues fused.  Shapes the
-    kernels cannot take (K % 64, N % 4) fall back to torch with a one-time warning."""
+    kernel for large token counts, the 128x128 kernel otherwise), epilogues fused.
+
+    Widths the kernels do not tile (K % 64, N % 4) are zero-padded to the next native shape (zero
+    k-columns add nothing to a dot product; padded output columns are sliced off), so every GPU
+    call runs the native kernel -- there is no torch fallback (``ops/_lib.py`` dispatch rule)."""
     epi = {None: EPI_NONE, "gelu": EPI_GELU, "swiglu": EPI_SWIGLU}[act]
     if not x.is_cuda:
         return ref.gemm_bt(x, w, b, residual, epi)
     K, N = x.shape[-1], w.shape[0]
-    if K % 64 or N % 4 or (epi == EPI_SWIGLU and N % 32):
-        _warn_once(f"linear: K={K} N={N} not supported by the native GEMM; torch fallback")
-        y = F.linear(x, w, b)
-        if act == "gelu":
-            y = F.gelu(y)
-        elif act == "swiglu":
-            y = silu_mul(y, interleaved=True)
-        return y + residual if residual is not None else y
+    expect(epi != EPI_SWIGLU or N % 32 == 0, "swiglu linear needs 16-row [gate | up] groups (N % 32 == 0)")
     x2 = x.reshape(-1, K)
     r2 = residual.reshape(x2.shape[0], -1) if residual is not None else None
+    pk, pn = (-K) % 64, (-N) % 4
+    if pk or pn:
+        x2 = F.pad(x2, (0, pk)) if pk else x2
+        w = F.pad(w, (0, pk, 0, pn))
+        b = F.pad(b, (0, pn)) if (b is not None and pn) else b
+        r2 = F.pad(r2, (0, pn)) if (r2 is not None and pn) else r2
     y = gemm_bt(x2, w, b, r2, epi)
+    if pn:
+        y = y[:, :N].contiguous()
     return y.view(*x.shape[:-1], y.shape[-1])
-
-
-_WARNED: set = set()
-
-
-def _warn_once(msg: str) -> None:
-    if msg not in _WARNED:
-        _WARNED.add(msg)
-        import logging
-
-        logging.getLogger(__name__).warning(msg)

@@ -58,6 +58,29 @@ def test_decode_stream_matches_row_major_path_and_reference(B):
     assert err < 0.15, err
 
 
+@pytest.mark.parametrize("B", [4, 128])
+def test_default_path_keeps_unfolded_norm_gains(B):
+    """the default GPU model does NOT fold the RMSNorm gains into the projections (one
+    more bf16 rounding of W diag(g)); with non-unit gains its decode matches the fp32 reference."""
+    cfg = decoder_config("tiny-llama")
+    w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=11, interleave_mlp=True)
+    gen = torch.Generator().manual_seed(3)
+    for k in list(w32):
+        if k.endswith("_norm"):
+            w32[k] = 0.5 + torch.rand(w32[k].shape, generator=gen)
+    prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
+               for n in torch.randint(10, 150, (B,), generator=gen)]
+    wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
+    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+    assert m.frag and not m.fold_norms
+    assert not torch.all(m.layers[0].attn_norm == 1)
+    h, _ = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    m_ref = LlamaModel(cfg, {k: v.bfloat16().float() for k, v in w32.items()}, "cpu", interleaved_mlp=True)
+    h_ref, _ = _run(m_ref, cfg, prompts, "cpu", torch.float32)
+    err = (h.float().cpu() - h_ref).abs().max().item()
+    assert err < 0.15, err
+
+
 @pytest.mark.parametrize("B", [1, 5, 16])
 def test_small_batch_norm_in_consumer_matches_norm_kernels(B):
     """Batches <= 16 decode without the RMSNorm launches (``LlamaModel._layer_small``: o / down add
@@ -73,9 +96,9 @@ def test_small_batch_norm_in_consumer_matches_norm_kernels(B):
     prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
                for n in torch.randint(10, 150, (B,), generator=gen)]
     wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
-    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+    # opt-in path (off by default: slower, profiles/decode_small_r5.md); folds the gains at load
+    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True, small_norm_fused=True)
     assert m.frag and m.fold_norms and B <= m.SMALL_FUSED_MAX_M
-    m.small_norm_fused = True  # opt-in path (off by default: slower, profiles/decode_small_r5.md)
     h_f, lg_f = _run(m, cfg, prompts, DEV, torch.bfloat16)
     m.small_norm_fused = False
     h_u, lg_u = _run(m, cfg, prompts, DEV, torch.bfloat16)
