@@ -27,7 +27,7 @@ SHAPES = {
     "square": [("sq4096", 4096, 4096, 4096, "none"), ("sq8192", 8192, 8192, 8192, "none")],
     "edge": [("edge-m1000", 1000, 1024, 512, "none"), ("edge-m300", 300, 512, 256, "bias")],
     # mixed prefill + decode steps: M = 384 / 640 / 1024 tokens per step
-    "mid": [(f"mid{M}-{n}", M, N, K, kind) for M in (384, 640, 1024)
+    "mid": [(f"mid{M}-{n}", M, N, K, kind) for M in (384, 512, 640, 768, 1024, 2048)
             for n, N, K, kind in (("qkv", 6144, 4096, "none"), ("o", 4096, 4096, "none"),
                                   ("gateup", 28672, 4096, "swiglu"), ("down", 4096, 14336, "none"))],
 }
@@ -99,15 +99,21 @@ def main():
             torch.cuda.synchronize()
             err, scale = check(a, w, b, kind, out, 256)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+            extra = {}
             nat, lib = [], []
             arms = [("nat", lambda: run_native(a, ws, b, kind, out, frag)), ("lib", lambda: run_lib(a, w, b, kind))]
             if args.native_only:
                 arms = arms[:1]
             if group == "mid" and frag and ops.native().gemm256_ok(M, N, K, K, K):
                 arms.append(("g256", lambda: ops.kernels.gemm256(a, ws, epilogue=EPI[kind], shuffled=True)))
+            if frag and kind in ("none", "swiglu") and ops.kernels.gemm_mid_ok(M, N, K, K):
+                # the mid-M stream-K kernel (gemm_mid.hip), checked against the same reference first
+                gm_out = ops.kernels.gemm_mid(a, ws, epilogue=EPI[kind])
+                torch.cuda.synchronize()
+                extra["gmid_err"] = [check(a, w, b, kind, gm_out, 256)[0]]
+                arms.append(("gmid", lambda: ops.kernels.gemm_mid(a, ws, epilogue=EPI[kind], out=out)))
             if args.ab_layout and frag:
                 arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
-            extra = {}
             for _ in range(args.rounds):
                 for arm, fn in arms:
                     fn()
@@ -132,7 +138,8 @@ def main():
                               "ref_max": round(scale, 3), "ok": err <= 0.02 * max(scale, 1.0),
                               "roofline_us": round(roofline_us(M, N, K), 1),
                               "vs_roofline": round(tn / roofline_us(M, N, K), 3),
-                              **{f"{k}_us": round(sorted(v)[len(v) // 2], 1) for k, v in extra.items()}}),
+                              **{(k if k.endswith("_err") else f"{k}_us"): round(sorted(v)[len(v) // 2], 4 if k.endswith("_err") else 1)
+                                 for k, v in extra.items()}}),
                   flush=True)
             del a, w, ws, b, out
             torch.cuda.empty_cache()

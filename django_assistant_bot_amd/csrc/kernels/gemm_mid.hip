@@ -1,0 +1,427 @@
+// Mid-M bf16 GEMM  C[M,N] = A[M,K] . B[N,K]^T  (+ residual, or fused SwiGLU over 8-row [gate | up]
+// groups) for M = 256..4096 rows: the token counts of mixed prefill + decode serving steps and of
+// request-at-a-time prompts (the reference runs one HF ``generate`` per request:
+// ai/providers/transformers.py:57-66, served by gunicorn_conf.py:9 workers).  B is in the
+// ops.shuffle_weights fragment layout (the one copy of every projection the decoder keeps).
+//
+// Why a third GEMM: at these M the 256x256 phased kernel (gemm256.hip) has 12-64 tiles for 256 CUs
+// and the 128x128 kernel (gemm.hip) runs at ~20 % of the MFMA rate (profiles/gemm_mid_r5.md).
+// Design (cdna_hip_programming.md section 5, "Projection GEMM at M = 256"; stream-K):
+//   * tile 128 (rows of A) x 256 (weight rows), K-tile 64; 8 waves = 2 (M) x 4 (N), each wave a
+//     64 x 64 piece = 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators, 32 MFMAs per K-tile;
+//   * A / B staged by LDS-DMA (buffer_load ... lds, 16 B per lane) into a ring of 3 K-tile stages
+//     of 48 KB (A 16 KB | B0 16 KB | B1 16 KB); one phase per K-tile: [fragment reads, DMA of the
+//     K-tile two ahead, counted vmcnt] barrier [32 MFMAs] barrier; the two wave groups (wr = 0 / 1)
+//     run one barrier apart (one group's MFMAs beside the other's LDS reads), as in gemm256;
+//   * work decomposition: the tiles_m workgroups of one "group" (one per 128-row tile of A) march
+//     in lockstep through the SAME range of the (weight tile, K-tile) iteration space, so a weight
+//     K-tile is fetched from HBM once and served to the group's other workgroups from their XCD's
+//     L2 (groups are formed from blocks that share blockIdx % 8).  The iteration space
+//     tiles_n x (K / 64) is split evenly over the 8 x floor(32 / tiles_m) groups (stream-K in the
+//     N x K plane): every CU gets the same number of MFMAs whatever the tile count;
+//   * a tile whose K range spans several groups is combined in-launch by the last arriver: every
+//     segment stores its fp32 partial (write-through sc1 stores, 1 KB per wave-instruction), drains,
+//     and bumps the tile's arrival counter (agent-scope atomic); the workgroup that draws the last
+//     ticket reads the other partials with sc1 loads (no fence needed: cdna_hip_programming.md
+//     section 5 item 2), sums ALL segments in segment order (its own from registers: the result is
+//     the same whichever segment arrives last), resets the counter and runs the epilogue.  Nothing
+//     waits on another workgroup, so there is no spin and no residency requirement.
+#include "common.h"
+#include "launchers.h"
+
+namespace dab {
+
+namespace {
+
+enum { MID_NONE = 0, MID_SWIGLU8 = 4 };
+
+struct GMid {
+  const bf16* A;
+  const bf16* B;  // shuffle_weights layout, [N][K]
+  bf16* C;
+  const bf16* residual;
+  float* slabs;  // [tiles_m][gn][2] partial tiles of 128 x 256 fp32 (in accumulator order)
+  int* cnt;      // [tiles_m * tiles_n] arrival counters, zero at rest
+  int M, N, K;
+  long lda, ldc, ldr;
+  int tiles_m, tiles_n, kt;
+  int spx;  // blocks per XCD label (grid / 8)
+  int gpx;  // groups per XCD label
+  int gn;   // groups = 8 * gpx
+  int q, r;  // tiles_n * kt = q * gn + r iterations: group j owns q (+1 for j < r)
+  unsigned b_bytes, slab_bytes;
+};
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
+template <int VMC>
+__device__ __forceinline__ void wait_vmc() {
+  static_assert(VMC >= 0 && VMC <= 63, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(VMC) : "memory");
+}
+
+__device__ __forceinline__ void mbar() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// the barrier after a phase's LDS reads: they are retired first (s_barrier waits for no counter)
+__device__ __forceinline__ void mread_bar() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  mbar();
+}
+
+constexpr int kStage = 49152;  // A 128 x 64 | B0 128 x 64 | B1 128 x 64 (bf16)
+constexpr int kStages = 3;
+constexpr int kFlagOff = kStages * kStage;  // one int: the "last arriver" broadcast
+constexpr int kSmem = kFlagOff + 16;
+constexpr int kE = 8;        // VMEM stores per wave in every epilogue variant
+constexpr int kDma = 6;      // LDS-DMA instructions per wave per stage
+constexpr int kSlabFloats = 512 * 64;  // one partial tile: 512 threads x 16 f32x4
+static_assert(kSmem <= 163840, "LDS");
+
+// group start of the balanced split of the iteration space
+__device__ __forceinline__ int grp_start(int j, int q, int r) { return j * q + min(j, r); }
+__device__ __forceinline__ int grp_owner(int i, int q, int r) {
+  const int big = r * (q + 1);
+  return i < big ? i / (q + 1) : r + (i - big) / q;
+}
+
+}  // namespace
+
+template <int EPI, bool RES>
+__global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
+  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+
+  // ---- which group / row tile this block is: blocks b, b + 8, ... share an XCD label
+  const int bid = blockIdx.x;
+  const int x = bid & 7, slot = bid >> 3;
+  const int g = slot / p.tiles_m, mt = slot - g * p.tiles_m;
+  if (g >= p.gpx) return;  // whole workgroup (uniform)
+  const int j = x * p.gpx + g;
+  const int start = grp_start(j, p.q, p.r);
+  const int end = start + p.q + (j < p.r ? 1 : 0);
+  if (end <= start) return;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = w >> 2, wc = w & 3;
+  const int li = lane & 15, gq = lane >> 4;
+  const int m0 = mt * 128;
+
+  // ---- LDS-DMA staging (per-lane parts in VOFFSET, the K / panel offset in SOFFSET)
+  const int sw = (4 * (w & 1) + (lane >> 4)) & 7;
+  const int cc = (lane & 7) ^ sw;
+  const int srow = 8 * w + (lane >> 3);
+  const unsigned vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2), vA1 = vA0 + (unsigned)(64 * p.lda * 2);
+  const unsigned kblk = (unsigned)(p.K / 32) * 1024u;  // bytes of one 16-row block over all of K
+  const unsigned vB0 = (unsigned)(lane * 16) + (unsigned)w * kblk, vB1 = vB0 + 1024u;
+  const unsigned vB2 = vB0 + 8u * kblk, vB3 = vB2 + 1024u;
+  const long a_rows = min(128, p.M - m0);
+  const __amdgpu_buffer_rsrc_t rA = mk_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(((a_rows - 1) * p.lda + p.K) * 2));
+  const __amdgpu_buffer_rsrc_t rB = mk_rsrc(p.B, p.b_bytes);
+  const int kt = p.kt;
+
+  auto stage = [&](int buf, int nt, int kk) {
+    char* dst = smem + buf * kStage;
+    const unsigned sa = (unsigned)kk * 128u;
+    const unsigned sb = (unsigned)nt * 16u * kblk + (unsigned)kk * 2048u;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + 8192 + w * 1024), 16, vA1, sa, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 16384 + w * 2048), 16, vB0, sb, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 16384 + w * 2048 + 1024), 16, vB1, sb, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 32768 + w * 2048), 16, vB2, sb, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 32768 + w * 2048 + 1024), 16, vB3, sb, 0, 0);
+  };
+
+  // ---- fragment reads: A rows 64 wr + 16 i + li (128-B rows, chunk c at c ^ ((row >> 1) & 7));
+  // B row blocks 4 wc + jn (1 KB per 16 rows x 32 k, lane-linear), k-step ks at + 1 KB
+  const int swr = li >> 1;
+  const int rdA0 = (64 * wr + li) * 128 + 16 * (gq ^ swr), rdA1 = (64 * wr + li) * 128 + 16 * ((4 + gq) ^ swr);
+  const int rdB = 16384 + wc * 8192 + lane * 16;
+
+  bf16x8 af[4][2];
+  bf16x8 bfr[4][2];
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // staging cursor: the iteration two ahead of the one being computed
+  int s_nt = start / kt, s_kk = start - s_nt * kt;
+  auto advance = [&]() {
+    if (++s_kk == kt) {
+      s_kk = 0;
+      ++s_nt;
+    }
+  };
+  // prologue: iterations start (buffer 0) and start + 1 (buffer 1) in flight, the first landed
+  stage(0, s_nt, s_kk);
+  advance();
+  if (start + 1 < end) {
+    stage(1, s_nt, s_kk);
+    advance();
+    wait_vmc<kDma>();
+  } else {
+    wait_vmc<0>();
+  }
+  mbar();
+
+  int it = start;
+  int b = 0;  // ring buffer of iteration `it`
+  bool after_epi = false;
+  const __amdgpu_buffer_rsrc_t rS = mk_rsrc(p.slabs, p.slab_bytes);
+  while (it < end) {
+    const int nt = it / kt;
+    const int k0 = it - nt * kt;
+    const int k1 = min(kt, k0 + (end - it));
+    if (wr == 1) mbar();  // group 1 one barrier behind through the K-loop (ping-pong)
+    for (int kk = k0; kk < k1; ++kk, ++it) {
+      const char* sb = smem + b * kStage;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = *reinterpret_cast<const bf16x8*>(sb + i * 2048 + rdA0);
+        af[i][1] = *reinterpret_cast<const bf16x8*>(sb + i * 2048 + rdA1);
+      }
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) {
+        bfr[jn][0] = *reinterpret_cast<const bf16x8*>(sb + rdB + jn * 2048);
+        bfr[jn][1] = *reinterpret_cast<const bf16x8*>(sb + rdB + jn * 2048 + 1024);
+      }
+      const int b2 = b == 0 ? 2 : b - 1;  // (b + 2) % 3
+      if (it + 2 < end) {
+        stage(b2, s_nt, s_kk);
+        advance();
+        if (after_epi) wait_vmc<kDma + kE>();
+        else wait_vmc<kDma>();
+      } else {
+        wait_vmc<0>();
+      }
+      after_epi = false;
+      mread_bar();
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn) acc[i][jn] = mfma16(bfr[jn][ks], af[i][ks], acc[i][jn]);
+      __builtin_amdgcn_s_setprio(0);
+      mbar();
+      b = b == 2 ? 0 : b + 1;
+    }
+    if (wr == 0) mbar();  // pairs with group 1's last K-loop barrier
+
+    // ---- segment end: a whole tile goes straight to the epilogue; a part is combined
+    const int n0 = nt * 256;
+    bool write = true;
+    if (k0 != 0 || k1 != kt) {
+      const int tile = mt * p.tiles_n + nt;
+      const int side = grp_start(j, p.q, p.r) >= nt * kt ? 0 : 1;
+      const unsigned own = (unsigned)(((mt * p.gn + j) * 2 + side) * kSlabFloats) * 4u;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jn = 0; jn < 4; ++jn)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][jn]), rS,
+                                                 own + (unsigned)(((i * 4 + jn) * 512 + tid) * 16), 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (R1)
+      __syncthreads();
+      const int j_lo = grp_owner(nt * kt, p.q, p.r), j_hi = grp_owner(nt * kt + kt - 1, p.q, p.r);
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<int*>(smem + kFlagOff) = old;
+      }
+      __syncthreads();
+      const int old = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + kFlagOff));
+      write = old == j_hi - j_lo;
+      if (write) {
+        if (tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        f32x4 tot[4][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn) tot[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+        // every segment in segment order (its own from registers): the sum does not depend on
+        // which segment arrived last
+        for (int jj = j_lo; jj <= j_hi; ++jj) {
+          if (jj == j) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int jn = 0; jn < 4; ++jn) tot[i][jn] += acc[i][jn];
+          } else {
+            const int sd = grp_start(jj, p.q, p.r) >= nt * kt ? 0 : 1;
+            const unsigned off = (unsigned)(((mt * p.gn + jj) * 2 + sd) * kSlabFloats) * 4u;
+            u32x4 v[4][4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int jn = 0; jn < 4; ++jn)
+                v[i][jn] = __builtin_amdgcn_raw_buffer_load_b128(rS, off + (unsigned)(((i * 4 + jn) * 512 + tid) * 16),
+                                                                 0, 16);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+              for (int jn = 0; jn < 4; ++jn) tot[i][jn] += __builtin_bit_cast(f32x4, v[i][jn]);
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jn = 0; jn < 4; ++jn) acc[i][jn] = tot[i][jn];
+      }
+    }
+    if (write) {
+      // ---- epilogue: acc[i][jn][r] = C[m0 + 64 wr + 16 i + li][n0 + 64 wc + 16 jn + 4 gq + r];
+      // exactly kE stores per wave (rows >= M fall outside the descriptor and are dropped)
+      int e_li = li, e_g = gq, e_wc = wc;
+      asm volatile("" : "+v"(e_li), "+v"(e_g), "+v"(e_wc));
+      const long c_rows = min(128, p.M - m0);
+      const __amdgpu_buffer_rsrc_t rC = mk_rsrc(p.C + (size_t)m0 * p.ldc, (unsigned)(c_rows * p.ldc * 2));
+      if constexpr (EPI == MID_SWIGLU8) {
+        // 8-row [gate | up] groups inside each 16-row block: one permlane32_swap of the (jn, jn + 1)
+        // pair gives lanes 0-31 block jn's gate / up rows and lanes 32-63 block jn + 1's
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mr = 64 * wr + 16 * i + e_li;
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            float o[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(acc[i][2 * pr][r]),
+                                                              __float_as_uint(acc[i][2 * pr + 1][r]), false, false);
+              o[r] = silu_f(__uint_as_float(s[0])) * __uint_as_float(s[1]);
+            }
+            u32x2 v;
+            v[0] = pack2bf(o[0], o[1]);
+            v[1] = pack2bf(o[2], o[3]);
+            const int oc = (n0 + 64 * e_wc + 32 * pr) / 2 + 4 * e_g;
+            __builtin_amdgcn_raw_buffer_store_b64(v, rC, (unsigned)((mr * p.ldc + oc) * 2), 0, 0);
+          }
+        }
+      } else {
+        // permlane16_swap of the (jn, jn + 1) pair: each lane then holds 8 contiguous columns
+        // n0 + 64 wc + 32 pr + cq -> one 16-B store
+        const int cq = 16 * (e_g & 1) + 8 * (e_g >> 1);
+        u32x4 rv[4][2];
+        if constexpr (RES) {
+          const __amdgpu_buffer_rsrc_t rR = mk_rsrc(p.residual + (size_t)m0 * p.ldr, (unsigned)(c_rows * p.ldr * 2));
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int pr = 0; pr < 2; ++pr)
+              rv[i][pr] = __builtin_amdgcn_raw_buffer_load_b128(
+                  rR, (unsigned)(((64 * wr + 16 * i + e_li) * p.ldr + n0 + 64 * e_wc + 32 * pr + cq) * 2), 0, 0);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mr = 64 * wr + 16 * i + e_li;
+#pragma unroll
+          for (int pr = 0; pr < 2; ++pr) {
+            float o[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(acc[i][2 * pr][r]),
+                                                              __float_as_uint(acc[i][2 * pr + 1][r]), false, false);
+              o[r] = __uint_as_float(s[0]);
+              o[4 + r] = __uint_as_float(s[1]);
+            }
+            if constexpr (RES) {
+              const u32x4 rw = rv[i][pr];
+#pragma unroll
+              for (int qd = 0; qd < 4; ++qd) {  // round like a bf16 GEMM output, then the bf16 add (HF)
+                o[2 * qd] = bf2f(f2bf(o[2 * qd])) + __uint_as_float(rw[qd] << 16);
+                o[2 * qd + 1] = bf2f(f2bf(o[2 * qd + 1])) + __uint_as_float(rw[qd] & 0xffff0000u);
+              }
+            }
+            u32x4 v;
+#pragma unroll
+            for (int qd = 0; qd < 4; ++qd) v[qd] = pack2bf(o[2 * qd], o[2 * qd + 1]);
+            const int nc = n0 + 64 * e_wc + 32 * pr + cq;
+            __builtin_amdgcn_raw_buffer_store_b128(v, rC, (unsigned)((mr * p.ldc + nc) * 2), 0, 0);
+          }
+        }
+      }
+      after_epi = true;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+namespace {
+int cu_count() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  return cus;
+}
+}  // namespace
+
+// Eligible: N % 256 == 0, K % 64 == 0, 16-B aligned A rows, ceil(M / 128) row tiles <= blocks per
+// XCD label (32 on MI355X: M <= 4096), 32-bit buffer offsets.
+int gemm_mid_ok(int M, int N, int K, long lda) {
+  if (M <= 0 || N <= 0 || K <= 0 || N % 256 || K % 64 || lda % 8 || lda < K) return 0;
+  const int spx = cu_count() / 8;
+  if ((M + 127) / 128 > spx) return 0;
+  if ((long)N * K * 2 >= (1L << 32) || (127L * lda + K) * 2 >= (1L << 31)) return 0;
+  return 1;
+}
+
+// Workspace the launcher needs: partial slabs (bytes) and arrival counters (ints).
+long gemm_mid_slab_bytes() { return (long)cu_count() * 2 * kSlabFloats * 4; }
+int gemm_mid_counters(int M, int N) { return ((M + 127) / 128) * (N / 256); }
+
+// epilogue 0: C = A B^T (+ residual, bf16 add after rounding); 4: SwiGLU over 8-row [gate | up]
+// groups (C has N / 2 columns).  slabs: gemm_mid_slab_bytes() bytes; cnt: >= gemm_mid_counters()
+// ints, zero on first use (the launch leaves them zero).
+int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s) {
+  if (!gemm_mid_ok(M, N, K, lda)) return hipErrorInvalidValue;
+  if (epilogue != MID_NONE && epilogue != MID_SWIGLU8) return hipErrorInvalidValue;
+  if (epilogue == MID_SWIGLU8 && residual) return hipErrorInvalidValue;
+  if (!slabs || !cnt || slab_bytes < gemm_mid_slab_bytes() || n_cnt < gemm_mid_counters(M, N) ||
+      slab_bytes >= (1L << 32))
+    return hipErrorInvalidValue;
+  GMid p{};
+  p.A = (const bf16*)A;
+  p.B = (const bf16*)B;
+  p.C = (bf16*)C;
+  p.residual = (const bf16*)residual;
+  p.slabs = (float*)slabs;
+  p.cnt = cnt;
+  p.M = M;
+  p.N = N;
+  p.K = K;
+  p.lda = lda;
+  p.ldc = ldc;
+  p.ldr = ldr;
+  p.tiles_m = (M + 127) / 128;
+  p.tiles_n = N / 256;
+  p.kt = K / 64;
+  const int grid = cu_count() & ~7;
+  p.spx = grid / 8;
+  p.gpx = p.spx / p.tiles_m;
+  p.gn = 8 * p.gpx;
+  const int iters = p.tiles_n * p.kt;
+  p.q = iters / p.gn;
+  p.r = iters % p.gn;
+  p.b_bytes = (unsigned)((long)N * K * 2);
+  p.slab_bytes = (unsigned)slab_bytes;
+  if (epilogue == MID_SWIGLU8) hipLaunchKernelGGL((gemm_mid_kernel<MID_SWIGLU8, false>), dim3(grid), dim3(512), 0, s, p);
+  else if (residual) hipLaunchKernelGGL((gemm_mid_kernel<MID_NONE, true>), dim3(grid), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL((gemm_mid_kernel<MID_NONE, false>), dim3(grid), dim3(512), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace dab

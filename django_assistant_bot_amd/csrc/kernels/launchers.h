@@ -78,6 +78,15 @@ int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void*
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
             const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
 
+// gemm_mid.hip (M = 256..4096: mixed serving steps / single prompts; grouped stream-K over the N x K
+// plane, 128 x 256 tiles, in-launch last-arriver combine; B in the shuffle_weights layout;
+// epilogue 0 none (+ residual) or 4 SwiGLU over 8-row [gate | up] groups)
+int gemm_mid_ok(int M, int N, int K, long lda);
+long gemm_mid_slab_bytes();
+int gemm_mid_counters(int M, int N);
+int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s);
+
 // stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,

@@ -432,6 +432,54 @@ def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
     return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
 
 
+_MID_WS: dict = {}
+
+
+def _mid_workspace(device: torch.device, s: int):
+    """Partial-tile slabs + arrival counters of ``gemm_mid``, one set per (device, stream): two
+    streams running the kernel at once must not share counters.  The counters are zero at rest (every
+    launch leaves them zero)."""
+    key = (device.index, s)
+    ws = _MID_WS.get(key)
+    if ws is None:
+        nat = native()
+        slabs = torch.empty((nat.gemm_mid_slab_bytes() // 4,), dtype=torch.float32, device=device)
+        cnt = torch.zeros((1 << 16,), dtype=torch.int32, device=device)
+        ws = _MID_WS[key] = (slabs, cnt)
+    return ws
+
+
+def gemm_mid_ok(M: int, N: int, K: int, lda: int) -> bool:
+    """Shapes ``gemm_mid`` serves: N % 256, K % 64, ceil(M / 128) <= 32 (M <= 4096)."""
+    return bool(native().gemm_mid_ok(M, N, K, lda)) and -(-M // 128) * (N // 256) <= (1 << 16)
+
+
+def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None):
+    """C = A . B^T (+ residual) or SwiGLU over 8-row [gate | up] groups, B a ``shuffle_weights`` copy:
+    the mid-M kernel (``gemm_mid.hip``: grouped stream-K, 128 x 256 tiles, in-launch combine) for
+    M = 256..4096 (mixed serving steps, single prompts).  Bit-reproducible: the split-K partials are
+    summed in a fixed order."""
+    M, K = A.shape
+    N = B.shape[0]
+    expect(A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 CUDA operands required")
+    expect(A.stride(-1) == 1 and B.is_contiguous() and B.shape[1] == K, "A K-contiguous, B a contiguous [N, K] copy")
+    expect(epilogue in (EPI_NONE, EPI_SWIGLU8), "gemm_mid epilogues: none (+residual) or SwiGLU8")
+    expect(gemm_mid_ok(M, N, K, A.stride(0)), "gemm_mid: N % 256, K % 64, M <= 4096, 16-B rows")
+    n_out = N // 2 if epilogue == EPI_SWIGLU8 else N
+    if residual is not None:
+        expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
+               and tuple(residual.shape) == (M, N), "residual must be bf16 [M, N]")
+    if out is None:
+        out = torch.empty((M, n_out), dtype=torch.bfloat16, device=A.device)
+    expect(out.dtype == torch.bfloat16 and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output")
+    s = stream(A)
+    slabs, cnt = _mid_workspace(A.device, s)
+    native().gemm_mid(ptr(A), A.stride(0), ptr(B), ptr(out), out.stride(0), ptr(residual),
+                      residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), ptr(slabs),
+                      slabs.numel() * 4, ptr(cnt), cnt.numel(), s)
+    return out
+
+
 def score_candidates(A, B, thr, cap, row_group=None, q_group=None):
     """Filtered cosine scores of A [M, K] against B [N, K] that are >= thr[m], appended per query
     (no [M, N] score matrix).  -> (cand_val fp32 [M, cap] (-inf padded), cand_idx int32 [M, cap]

@@ -319,6 +319,46 @@ def test_gemm256(M, N, K, shuffled):
               ref.silu_mul(ref.gemm_bt(A, torch.cat([wg, wu], 0), torch.cat([bg, bu]))), atol=3e-2, rtol=3e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 256), (129, 768, 640), (640, 4096, 4096),
+                                   (768, 6144, 4096), (1000, 1024, 14336), (4096, 512, 128), (2048, 2048, 1024),
+                                   (384, 28672, 4096)])
+def test_gemm_mid(M, N, K):
+    """Mid-M stream-K kernel (gemm_mid.hip) against the fp32 reference: ragged M, tiles split over
+    1..8 groups (in-launch last-arriver combine), a single iteration, 32 row tiles; plain, residual
+    and SwiGLU8 epilogues on the fragment-layout weights.  Bit-reproducible across launches and the
+    arrival counters are left at zero."""
+    assert ops.kernels.gemm_mid_ok(M, N, K, K)
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    Bs = ops.shuffle_weights(B)
+    res = bf(M, N)
+    exp = ref.gemm_bt(A, B)
+    got = ops.kernels.gemm_mid(A, Bs)
+    close(got, exp, atol=3e-2, rtol=2e-2)
+    close(ops.kernels.gemm_mid(A, Bs, residual=res), ref.gemm_bt(A, B, None, res), atol=3e-2, rtol=2e-2)
+    wg, wu = bf(N // 2, K, scale=0.05), bf(N // 2, K, scale=0.05)
+    w8 = ops.shuffle_weights(ops.interleave_gate_up(wg, wu, 8))
+    close(ops.kernels.gemm_mid(A, w8, epilogue=ops.EPI_SWIGLU8),
+          ref.silu_mul(ref.gemm_bt(A, torch.cat([wg, wu], 0))), atol=3e-2, rtol=3e-2)
+    for _ in range(3):
+        assert torch.equal(ops.kernels.gemm_mid(A, Bs), got)
+    torch.cuda.synchronize()
+    for slabs, cnt in ops.kernels._MID_WS.values():
+        assert int(cnt.abs().sum()) == 0
+
+
+def test_gemm_mid_in_a_strided_view_and_out_buffer():
+    """A as a row slice of a wider buffer (lda > K) and a caller-provided output view."""
+    M, N, K = 700, 1024, 512
+    big = bf(M, K + 64)
+    A = big[:, :K]
+    B = bf(N, K, scale=0.05)
+    out_big = torch.zeros((M, N + 256), dtype=torch.bfloat16, device=DEV)
+    out = out_big[:, :N]
+    ops.kernels.gemm_mid(A, ops.shuffle_weights(B), out=out)
+    close(out, ref.gemm_bt(A.contiguous(), B), atol=3e-2, rtol=2e-2)
+    assert torch.all(out_big[:, N:] == 0)
+
+
 @pytest.mark.parametrize("aux", [0, 2, 16, 18])
 def test_gemm256_stamped_matches_and_stamps(aux):
     """The diagnostic STAMP instantiation (benchmarks/gemm_stamps.py) computes the same C as the
