@@ -80,6 +80,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--native-only", action="store_true", help="profile mode: only the native arm")
     ap.add_argument("--only", default="", help="comma list of op names to run")
+    ap.add_argument("--mid-variants", action="store_true", help="gemm_mid A/B arms (BK 64, no combine)")
     ap.add_argument("--ab-layout", action="store_true",
                     help="llama shapes: also time the row-major weight layout (arm 'rowmajor')")
     args = ap.parse_args()
@@ -112,6 +113,10 @@ def main():
                 torch.cuda.synchronize()
                 extra["gmid_err"] = [check(a, w, b, kind, gm_out, 256)[0]]
                 arms.append(("gmid", lambda: ops.kernels.gemm_mid(a, ws, epilogue=EPI[kind], out=out)))
+                if args.mid_variants:
+                    for v in (64, 1032, 1064):  # BK 64; split tiles left uncombined (timing only)
+                        arms.append((f"gmid{v}", lambda v=v: ops.kernels.gemm_mid(a, ws, epilogue=EPI[kind], out=out,
+                                                                                  variant=v)))
             if args.ab_layout and frag:
                 arms.append(("rowmajor", lambda: run_native(a, w, b, kind, out, False)))
             for _ in range(args.rounds):

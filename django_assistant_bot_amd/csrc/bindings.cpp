@@ -156,13 +156,13 @@ PYBIND11_MODULE(_native, m) {
   m.def("gemm_mid_slab_bytes", &dab::gemm_mid_slab_bytes);
   m.def("gemm_mid_counters", &dab::gemm_mid_counters);
   m.def("gemm_mid", [](u A, long lda, u B, u C, long ldc, u residual, long ldr, int M, int N, int K, int epilogue,
-                       u slabs, long slab_bytes, u cnt, int n_cnt, u s) {
+                       u slabs, long slab_bytes, u cnt, int n_cnt, u s, int variant) {
     check(dab::gemm_mid(CVP(A), lda, CVP(B), VP(C), ldc, CVP(residual), ldr, M, N, K, epilogue, VP(slabs), slab_bytes,
-                        (int*)cnt, n_cnt, ST(s)),
+                        (int*)cnt, n_cnt, ST(s), variant),
           "gemm_mid");
   }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("C"), py::arg("ldc"), py::arg("residual"), py::arg("ldr"),
      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("slabs"), py::arg("slab_bytes"),
-     py::arg("cnt"), py::arg("n_cnt"), py::arg("s"));
+     py::arg("cnt"), py::arg("n_cnt"), py::arg("s"), py::arg("variant") = 0);
   m.def("gemm256_ok", &dab::gemm256_ok);
   m.def("gemm256_stamped", [](u A, long lda, u B, u C, u bias, u residual, int M, int N, int K, int epilogue,
                               int b_shuf, u stamps, int stamp_tiles, u s, int store_aux) {

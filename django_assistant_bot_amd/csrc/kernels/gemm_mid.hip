@@ -76,14 +76,20 @@ __device__ __forceinline__ void mread_bar() {
   mbar();
 }
 
-constexpr int kStage = 49152;  // A 128 x 64 | B0 128 x 64 | B1 128 x 64 (bf16)
-constexpr int kStages = 3;
-constexpr int kFlagOff = kStages * kStage;  // one int: the "last arriver" broadcast
-constexpr int kSmem = kFlagOff + 16;
-constexpr int kE = 8;        // VMEM stores per wave in every epilogue variant
-constexpr int kDma = 6;      // LDS-DMA instructions per wave per stage
+// ring geometry per K-step width BK (64: 3 stages of 48 KB, DMA distance 2; 32: 6 stages of 24 KB,
+// distance 5 -- the same LDS, two and a half times the latency cover in cycles)
+template <int BK>
+struct MidGeo {
+  static constexpr int kA = 128 * BK * 2;        // A bytes per stage
+  static constexpr int kStage = 384 * BK * 2;    // A | B (256 weight rows)
+  static constexpr int kStages = BK == 64 ? 3 : 6;
+  static constexpr int kDist = kStages - 1;     // stage issued kDist iterations ahead
+  static constexpr int kDma = BK == 64 ? 6 : 3;  // LDS-DMA instructions per wave per stage
+  static constexpr int kSmem = kStages * kStage;
+  static_assert(kSmem <= 163840, "LDS");
+};
+constexpr int kE = 8;                  // VMEM stores per wave in every epilogue variant
 constexpr int kSlabFloats = 512 * 64;  // one partial tile: 512 threads x 16 f32x4
-static_assert(kSmem <= 163840, "LDS");
 
 // group start of the balanced split of the iteration space
 __device__ __forceinline__ int grp_start(int j, int q, int r) { return j * q + min(j, r); }
@@ -94,9 +100,14 @@ __device__ __forceinline__ int grp_owner(int i, int q, int r) {
 
 }  // namespace
 
-template <int EPI, bool RES>
+// BK: K-step width (see MidGeo); DIAG (timing only, benchmarks/gemm_bench.py): 1 = partial tiles
+// are stored and counted but never combined (the output of split tiles is left unwritten)
+template <int EPI, bool RES, int BK, int DIAG = 0>
 __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
-  __shared__ __attribute__((aligned(16))) char smem[kSmem];
+  using Geo = MidGeo<BK>;
+  constexpr int kStage = Geo::kStage, kStages = Geo::kStages, kDist = Geo::kDist, kDma = Geo::kDma;
+  constexpr int kA = Geo::kA;
+  __shared__ __attribute__((aligned(16))) char smem[Geo::kSmem];
 
   // ---- which group / row tile this block is: blocks b, b + 8, ... share an XCD label
   const int bid = blockIdx.x;
@@ -113,63 +124,97 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
   const int wr = w >> 2, wc = w & 3;
   const int li = lane & 15, gq = lane >> 4;
   const int m0 = mt * 128;
+  const int kt = p.kt;  // K-steps of BK per tile
 
-  // ---- LDS-DMA staging (per-lane parts in VOFFSET, the K / panel offset in SOFFSET)
-  const int sw = (4 * (w & 1) + (lane >> 4)) & 7;
-  const int cc = (lane & 7) ^ sw;
-  const int srow = 8 * w + (lane >> 3);
-  const unsigned vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2), vA1 = vA0 + (unsigned)(64 * p.lda * 2);
+  // ---- LDS-DMA staging (per-lane parts in VOFFSET, the K / panel offset in SOFFSET).
+  // A: BK = 64: rows of 128 B, 16-B chunk c of row r at c ^ ((r >> 1) & 7), wave w stages rows
+  //    8w..8w+7 (+64);  BK = 32: rows of 64 B, chunk c at c ^ ((r >> 2) & 3), wave w rows 16w..16w+15.
+  //    (conflict-free for the 4 x 16-lane groups of ds_read_b128; the swizzle goes on the SOURCE
+  //    address since LDS-DMA writes lane-linearly)
+  // B: the fragment layout: a 16-row x 32-k block is 1 KB in lane order; BK = 64 stages blocks
+  //    (rb, 2kk) and (rb, 2kk + 1) back to back (2 KB per row block), BK = 32 block (rb, kk).
+  unsigned vA0, vA1 = 0;
+  if constexpr (BK == 64) {
+    const int sw = (4 * (w & 1) + (lane >> 4)) & 7;
+    const int cc = (lane & 7) ^ sw;
+    const int srow = 8 * w + (lane >> 3);
+    vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2);
+    vA1 = vA0 + (unsigned)(64 * p.lda * 2);
+  } else {
+    const int srow = 16 * w + (lane >> 2);
+    const int cc = (lane & 3) ^ ((srow >> 2) & 3);
+    vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2);
+  }
   const unsigned kblk = (unsigned)(p.K / 32) * 1024u;  // bytes of one 16-row block over all of K
-  const unsigned vB0 = (unsigned)(lane * 16) + (unsigned)w * kblk, vB1 = vB0 + 1024u;
-  const unsigned vB2 = vB0 + 8u * kblk, vB3 = vB2 + 1024u;
+  const unsigned vB0 = (unsigned)(lane * 16) + (unsigned)w * kblk, vB2 = vB0 + 8u * kblk;
   const long a_rows = min(128, p.M - m0);
   const __amdgpu_buffer_rsrc_t rA = mk_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(((a_rows - 1) * p.lda + p.K) * 2));
   const __amdgpu_buffer_rsrc_t rB = mk_rsrc(p.B, p.b_bytes);
-  const int kt = p.kt;
 
   auto stage = [&](int buf, int nt, int kk) {
     char* dst = smem + buf * kStage;
-    const unsigned sa = (unsigned)kk * 128u;
-    const unsigned sb = (unsigned)nt * 16u * kblk + (unsigned)kk * 2048u;
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + 8192 + w * 1024), 16, vA1, sa, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 16384 + w * 2048), 16, vB0, sb, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 16384 + w * 2048 + 1024), 16, vB1, sb, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 32768 + w * 2048), 16, vB2, sb, 0, 0);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + 32768 + w * 2048 + 1024), 16, vB3, sb, 0, 0);
+    const unsigned sa = (unsigned)kk * (unsigned)(BK * 2);
+    const unsigned sb = (unsigned)nt * 16u * kblk + (unsigned)kk * (unsigned)(BK * 32);
+    if constexpr (BK == 64) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + 8192 + w * 1024), 16, vA1, sa, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 2048), 16, vB0, sb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 2048 + 1024), 16, vB0 + 1024u, sb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 16384 + w * 2048), 16, vB2, sb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 16384 + w * 2048 + 1024), 16, vB2 + 1024u, sb,
+                                               0, 0);
+    } else {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 1024), 16, vB0, sb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 8192 + w * 1024), 16, vB2, sb, 0, 0);
+    }
   };
 
-  // ---- fragment reads: A rows 64 wr + 16 i + li (128-B rows, chunk c at c ^ ((row >> 1) & 7));
-  // B row blocks 4 wc + jn (1 KB per 16 rows x 32 k, lane-linear), k-step ks at + 1 KB
-  const int swr = li >> 1;
-  const int rdA0 = (64 * wr + li) * 128 + 16 * (gq ^ swr), rdA1 = (64 * wr + li) * 128 + 16 * ((4 + gq) ^ swr);
-  const int rdB = 16384 + wc * 8192 + lane * 16;
+  // ---- fragment reads: A rows 64 wr + 16 i + li, B row blocks 4 wc + jn
+  constexpr int KS = BK / 32;  // MFMA k-steps per stage
+  int rdA[KS];
+  if constexpr (BK == 64) {
+    const int swr = li >> 1;
+    rdA[0] = (64 * wr + li) * 128 + 16 * (gq ^ swr);
+    rdA[KS - 1] = (64 * wr + li) * 128 + 16 * ((4 + gq) ^ swr);
+  } else {
+    rdA[0] = (64 * wr + li) * 64 + 16 * (gq ^ ((li >> 2) & 3));
+  }
+  constexpr int kRowBlk = BK * 32;  // LDS bytes of one 16-row block of A / B in a stage
+  const int rdB = kA + wc * 4 * kRowBlk + lane * 16;
 
-  bf16x8 af[4][2];
-  bf16x8 bfr[4][2];
+  bf16x8 af[4][KS];
+  bf16x8 bfr[4][KS];
   f32x4 acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int jn = 0; jn < 4; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // staging cursor: the iteration two ahead of the one being computed
+  // staging cursor: the iteration kDist ahead of the one being computed
   int s_nt = start / kt, s_kk = start - s_nt * kt;
+  int s_it = start;
   auto advance = [&]() {
+    ++s_it;
     if (++s_kk == kt) {
       s_kk = 0;
       ++s_nt;
     }
   };
-  // prologue: iterations start (buffer 0) and start + 1 (buffer 1) in flight, the first landed
-  stage(0, s_nt, s_kk);
-  advance();
-  if (start + 1 < end) {
-    stage(1, s_nt, s_kk);
-    advance();
-    wait_vmc<kDma>();
-  } else {
-    wait_vmc<0>();
+  // prologue: iterations start .. start + kDist - 1 in flight (buffers 0 ..), the first landed
+#pragma unroll
+  for (int d = 0; d < kDist; ++d)
+    if (s_it < end) {
+      stage(d, s_nt, s_kk);
+      advance();
+    }
+  {
+    const int beyond = s_it - start - 1;  // issued stages past the first
+    if (beyond >= 4) wait_vmc<4 * kDma>();
+    else if (beyond == 3) wait_vmc<3 * kDma>();
+    else if (beyond == 2) wait_vmc<2 * kDma>();
+    else if (beyond == 1) wait_vmc<kDma>();
+    else wait_vmc<0>();
   }
   mbar();
 
@@ -185,36 +230,41 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
     for (int kk = k0; kk < k1; ++kk, ++it) {
       const char* sb = smem + b * kStage;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        af[i][0] = *reinterpret_cast<const bf16x8*>(sb + i * 2048 + rdA0);
-        af[i][1] = *reinterpret_cast<const bf16x8*>(sb + i * 2048 + rdA1);
-      }
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int jn = 0; jn < 4; ++jn) {
-        bfr[jn][0] = *reinterpret_cast<const bf16x8*>(sb + rdB + jn * 2048);
-        bfr[jn][1] = *reinterpret_cast<const bf16x8*>(sb + rdB + jn * 2048 + 1024);
-      }
-      const int b2 = b == 0 ? 2 : b - 1;  // (b + 2) % 3
-      if (it + 2 < end) {
-        stage(b2, s_nt, s_kk);
+        for (int ks = 0; ks < KS; ++ks) af[i][ks] = *reinterpret_cast<const bf16x8*>(sb + i * 16 * (BK * 2) + rdA[ks]);
+#pragma unroll
+      for (int jn = 0; jn < 4; ++jn)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          bfr[jn][ks] = *reinterpret_cast<const bf16x8*>(sb + rdB + jn * kRowBlk + ks * 1024);
+      // the stage kDist ahead goes into the buffer read one phase ago
+      if (s_it < end) {
+        stage(b == 0 ? kStages - 1 : b - 1, s_nt, s_kk);
         advance();
-        if (after_epi) wait_vmc<kDma + kE>();
-        else wait_vmc<kDma>();
+        if (after_epi) wait_vmc<(kDist - 1) * kDma + kE>();
+        else wait_vmc<(kDist - 1) * kDma>();
       } else {
-        wait_vmc<0>();
+        // tail: the stages after `it + 1` that are still in flight may stay so
+        const int beyond = after_epi ? 0 : s_it - it - 2;
+        if (beyond >= 4) wait_vmc<4 * kDma>();
+        else if (beyond == 3) wait_vmc<3 * kDma>();
+        else if (beyond == 2) wait_vmc<2 * kDma>();
+        else if (beyond == 1) wait_vmc<kDma>();
+        else wait_vmc<0>();
       }
       after_epi = false;
       mread_bar();
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+      for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int jn = 0; jn < 4; ++jn) acc[i][jn] = mfma16(bfr[jn][ks], af[i][ks], acc[i][jn]);
       __builtin_amdgcn_s_setprio(0);
       mbar();
-      b = b == 2 ? 0 : b + 1;
+      b = b == kStages - 1 ? 0 : b + 1;
     }
     if (wr == 0) mbar();  // pairs with group 1's last K-loop barrier
 
@@ -223,7 +273,7 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
     bool write = true;
     if (k0 != 0 || k1 != kt) {
       const int tile = mt * p.tiles_n + nt;
-      const int side = grp_start(j, p.q, p.r) >= nt * kt ? 0 : 1;
+      const int side = start >= nt * kt ? 0 : 1;
       const unsigned own = (unsigned)(((mt * p.gn + j) * 2 + side) * kSlabFloats) * 4u;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -234,15 +284,15 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (R1)
       __syncthreads();
       const int j_lo = grp_owner(nt * kt, p.q, p.r), j_hi = grp_owner(nt * kt + kt - 1, p.q, p.r);
-      if (tid == 0) {
-        const int old = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *reinterpret_cast<int*>(smem + kFlagOff) = old;
-      }
+      // the broadcast word: the buffer of the stage just consumed (nothing in flight writes it)
+      int* flag = reinterpret_cast<int*>(smem + (b == 0 ? kStages - 1 : b - 1) * kStage);
+      if (tid == 0) *flag = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      const int old = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const int*>(smem + kFlagOff));
-      write = old == j_hi - j_lo;
+      const int old = __builtin_amdgcn_readfirstlane(*flag);
+      mread_bar();  // every wave has its copy before the next stage's DMA may overwrite the word
+      write = old == j_hi - j_lo && DIAG == 0;
+      if (old == j_hi - j_lo && tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (write) {
-        if (tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         f32x4 tot[4][4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -384,15 +434,20 @@ int gemm_mid_counters(int M, int N) { return ((M + 127) / 128) * (N / 256); }
 
 // epilogue 0: C = A B^T (+ residual, bf16 add after rounding); 4: SwiGLU over 8-row [gate | up]
 // groups (C has N / 2 columns).  slabs: gemm_mid_slab_bytes() bytes; cnt: >= gemm_mid_counters()
-// ints, zero on first use (the launch leaves them zero).
+// ints, zero on first use (the launch leaves them zero).  variant (A/B harness only): 0 default
+// (BK 64), 32 / 64 force the K-step, + 1000 = DIAG 1 (split tiles not combined: timing only).
+// BK 32 (6-stage ring) measured 5-20 % slower than BK 64 on every mid shape, with LDS bank
+// conflicts on its 64-B A rows (profiles/gemm_mid_r6.md): kept as an A/B arm only.
 int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
-             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s) {
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant) {
   if (!gemm_mid_ok(M, N, K, lda)) return hipErrorInvalidValue;
   if (epilogue != MID_NONE && epilogue != MID_SWIGLU8) return hipErrorInvalidValue;
   if (epilogue == MID_SWIGLU8 && residual) return hipErrorInvalidValue;
   if (!slabs || !cnt || slab_bytes < gemm_mid_slab_bytes() || n_cnt < gemm_mid_counters(M, N) ||
       slab_bytes >= (1L << 32))
     return hipErrorInvalidValue;
+  const bool diag = variant >= 1000;
+  const int bk = (variant % 1000) == 32 ? 32 : 64;
   GMid p{};
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
@@ -408,7 +463,7 @@ int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const vo
   p.ldr = ldr;
   p.tiles_m = (M + 127) / 128;
   p.tiles_n = N / 256;
-  p.kt = K / 64;
+  p.kt = K / bk;
   const int grid = cu_count() & ~7;
   p.spx = grid / 8;
   p.gpx = p.spx / p.tiles_m;
@@ -418,9 +473,23 @@ int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const vo
   p.r = iters % p.gn;
   p.b_bytes = (unsigned)((long)N * K * 2);
   p.slab_bytes = (unsigned)slab_bytes;
-  if (epilogue == MID_SWIGLU8) hipLaunchKernelGGL((gemm_mid_kernel<MID_SWIGLU8, false>), dim3(grid), dim3(512), 0, s, p);
-  else if (residual) hipLaunchKernelGGL((gemm_mid_kernel<MID_NONE, true>), dim3(grid), dim3(512), 0, s, p);
-  else hipLaunchKernelGGL((gemm_mid_kernel<MID_NONE, false>), dim3(grid), dim3(512), 0, s, p);
+#define MID_LAUNCH(E, R, BKV, D) hipLaunchKernelGGL((gemm_mid_kernel<E, R, BKV, D>), dim3(grid), dim3(512), 0, s, p)
+#define MID_BK(E, R)                       \
+  do {                                     \
+    if (diag) {                            \
+      if (bk == 64) MID_LAUNCH(E, R, 64, 1); \
+      else MID_LAUNCH(E, R, 32, 1);        \
+    } else if (bk == 64) {                 \
+      MID_LAUNCH(E, R, 64, 0);             \
+    } else {                               \
+      MID_LAUNCH(E, R, 32, 0);             \
+    }                                      \
+  } while (0)
+  if (epilogue == MID_SWIGLU8) MID_BK(MID_SWIGLU8, false);
+  else if (residual) MID_BK(MID_NONE, true);
+  else MID_BK(MID_NONE, false);
+#undef MID_BK
+#undef MID_LAUNCH
   return hipGetLastError();
 }
 

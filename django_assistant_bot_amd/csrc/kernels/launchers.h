@@ -85,7 +85,7 @@ int gemm_mid_ok(int M, int N, int K, long lda);
 long gemm_mid_slab_bytes();
 int gemm_mid_counters(int M, int N);
 int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
-             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s);
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant = 0);
 
 // stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)

@@ -344,9 +344,26 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
 GEMM256_MIN_M = 1024  # the phased 256x256 kernel from here on; the 128x128 kernel below
 
 
+GEMM_MID_MIN_M = 192
+GEMM_MID_FILL = 192  # gemm256 keeps a shape whose 256 x 256 tiles fill this many of the 256 CUs
+
+
+def use_gemm_mid(M: int, N: int, K: int, lda: int) -> bool:
+    """Mid-M shapes on fragment-layout weights go to the stream-K kernel (gemm_mid.hip) where the
+    256 x 256 kernel would leave CUs idle: -(-M // 256) * (N / 256) < GEMM_MID_FILL tiles.  Measured
+    (profiles/gemm_mid_r6.md): Llama-3-8B qkv / o / down at M = 384..2048 run 1.2-2.3x faster than the
+    round-5 dispatch (the 128 x 128 kernel / underfilled gemm256); gate_up (112 tile columns) and
+    qkv at M >= 2048 stay on gemm256."""
+    return (M >= GEMM_MID_MIN_M and N % 256 == 0 and -(-M // 256) * (N // 256) < GEMM_MID_FILL
+            and gemm_mid_ok(M, N, K, lda))
+
+
 def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
-    """Large-M shapes go to the phased 256x256 kernel (gemm256.hip)."""
-    return M >= GEMM256_MIN_M and bool(native().gemm256_ok(M, N, K, lda, ldb))
+    """Large-M shapes go to the phased 256x256 kernel (gemm256.hip), and so do shapes from M = 256 on
+    whose 256 x 256 tiles fill >= GEMM_MID_FILL CUs (gate_up at M = 384-768: 84-161 us against
+    105-184 on the 128 x 128 kernel, profiles/gemm_mid_r6.md)."""
+    wide = M >= 256 and N % 256 == 0 and -(-M // 256) * (N // 256) >= GEMM_MID_FILL  # e.g. gate_up at M 256-1023
+    return (M >= GEMM256_MIN_M or wide) and bool(native().gemm256_ok(M, N, K, lda, ldb))
 
 
 def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, row_group=None, q_group=None,
@@ -400,8 +417,11 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     if out is None:
         out = torch.empty((M, n_out), dtype=dtype, device=A.device)
     expect(out.dtype == dtype and out.stride(-1) == 1 and tuple(out.shape) == (M, n_out), "bad output buffer")
-    if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SWIGLU8) and not out_f32 and row_group is None
-            and q_group is None and allow is None and (not shuffled or N == B.shape[0])
+    plain = not out_f32 and row_group is None and q_group is None and allow is None
+    if (plain and shuffled and N == B.shape[0] and bias is None and epilogue in (EPI_NONE, EPI_SWIGLU8)
+            and use_gemm_mid(M, N, K, A.stride(0))):
+        return gemm_mid(A, B, residual=residual, epilogue=epilogue, out=out)
+    if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SWIGLU8) and plain and (not shuffled or N == B.shape[0])
             and use_gemm256(M, N, K, A.stride(0), B.stride(0))):
         return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
     native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
@@ -454,11 +474,12 @@ def gemm_mid_ok(M: int, N: int, K: int, lda: int) -> bool:
     return bool(native().gemm_mid_ok(M, N, K, lda)) and -(-M // 128) * (N // 256) <= (1 << 16)
 
 
-def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None):
+def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0):
     """C = A . B^T (+ residual) or SwiGLU over 8-row [gate | up] groups, B a ``shuffle_weights`` copy:
     the mid-M kernel (``gemm_mid.hip``: grouped stream-K, 128 x 256 tiles, in-launch combine) for
     M = 256..4096 (mixed serving steps, single prompts).  Bit-reproducible: the split-K partials are
-    summed in a fixed order."""
+    summed in a fixed order.  ``variant`` (A/B harness): 32 / 64 force the K-step; + 1000 leaves
+    split tiles uncombined (timing only)."""
     M, K = A.shape
     N = B.shape[0]
     expect(A.is_cuda and A.dtype == torch.bfloat16 and B.dtype == torch.bfloat16, "bf16 CUDA operands required")
@@ -476,7 +497,7 @@ def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None):
     slabs, cnt = _mid_workspace(A.device, s)
     native().gemm_mid(ptr(A), A.stride(0), ptr(B), ptr(out), out.stride(0), ptr(residual),
                       residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), ptr(slabs),
-                      slabs.numel() * 4, ptr(cnt), cnt.numel(), s)
+                      slabs.numel() * 4, ptr(cnt), cnt.numel(), s, int(variant))
     return out
 
 

@@ -346,6 +346,16 @@ def test_gemm_mid(M, N, K):
         assert int(cnt.abs().sum()) == 0
 
 
+@pytest.mark.parametrize("M,N,K", [(300, 512, 256), (1000, 1024, 4096)])
+def test_gemm_mid_k64_variant(M, N, K):
+    """The 64-deep K-step ring (3 stages) of gemm_mid, kept as an A/B arm: same numerics contract."""
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    Bs = ops.shuffle_weights(B)
+    close(ops.kernels.gemm_mid(A, Bs, variant=64), ref.gemm_bt(A, B), atol=3e-2, rtol=2e-2)
+    res = bf(M, N)
+    close(ops.kernels.gemm_mid(A, Bs, residual=res, variant=64), ref.gemm_bt(A, B, None, res), atol=3e-2, rtol=2e-2)
+
+
 def test_gemm_mid_in_a_strided_view_and_out_buffer():
     """A as a row slice of a wider buffer (lda > K) and a caller-provided output view."""
     M, N, K = 700, 1024, 512
