@@ -55,6 +55,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("ipc_probe", [](u ptr) { check(dab::ipc_probe(ptr), "ipc_probe"); });
   m.def("ipc_close_handle", [](u ptr) { check(dab::ipc_close_handle(ptr), "ipc_close_handle"); });
   m.def("allreduce_error", &dab::allreduce_error, py::arg("base"), py::arg("clear") = 1);
+  m.def("allreduce_error_async", [](u base, u host_word, u s) {
+    check(dab::allreduce_error_async(base, VP(host_word), ST(s)), "allreduce_error_async");
+  });
   m.def("roctx_push", [](const std::string& name) { return dab::trace::range_push(name.c_str()); });
   m.def("roctx_pop", &dab::trace::range_pop);
   m.def("roctx_mark", [](const std::string& name) { dab::trace::mark(name.c_str()); });

@@ -19,8 +19,12 @@
 //   * Parity double-buffers the staging.  A peer that is one call ahead writes the other half.  It
 //     cannot get two calls ahead, because its next barrier needs our flag.  One barrier per call
 //     is therefore enough.
-//   * Spins are bounded.  A missing peer sets `error` and the block moves on, so a broken group
-//     cannot hang the GPU.  The host checks `error` after synchronising.
+//   * Spins are bounded.  A missing peer sets `error` and the block gives up, so a broken group
+//     cannot hang the GPU.  A block that gave up writes NaN over its output segment and does NOT
+//     advance its epoch; the error word is sticky (until the host clears it), and every later call
+//     on this rank only poisons its output.  The engine copies the word to the host behind every
+//     TP step and fails the step's requests when it is set (engine/llm_engine.py
+//     ``_tp_fault_check``); the group is then restarted.
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,14 +61,26 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArParams p) {
   const int b = blockIdx.x, tid = threadIdx.x;
   const size_t sig_bytes = (sizeof(ArSignal) + 4095) / 4096 * 4096;
   ArSignal* me = reinterpret_cast<ArSignal*>(p.base[p.rank]);
-  __shared__ uint32_t e_sh;
-  if (tid == 0) e_sh = me->epoch[b] + 1;
+  __shared__ uint32_t e_sh, bad_sh;
+  if (tid == 0) {
+    e_sh = me->epoch[b] + 1;
+    bad_sh = __hip_atomic_load(&me->error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   __syncthreads();
   const uint32_t e = e_sh;
   const size_t stage_off = sig_bytes + (size_t)(e & 1) * p.half_bytes;
 
   const long per = (p.n16 + AR_BLOCKS - 1) / AR_BLOCKS;
   const long s0 = min(p.n16, (long)b * per), s1 = min(p.n16, s0 + per);
+  u32x4* dst = reinterpret_cast<u32x4*>(p.data);
+  auto poison = [&]() {  // bf16 quiet NaN over this block's segment
+    const u32x4 nan4 = {0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u, 0x7fc07fc0u};
+    for (long i = s0 + tid; i < s1; i += AR_THREADS) dst[i] = nan4;
+  };
+  if (bad_sh) {  // this rank's group already broke: no flags, no epoch, NaN out (uniform)
+    poison();
+    return;
+  }
   u32x4* mine = reinterpret_cast<u32x4*>(p.base[p.rank] + stage_off);
   const u32x4* src = reinterpret_cast<const u32x4*>(p.data);
   for (long i = s0 + tid; i < s1; i += AR_THREADS) mine[i] = src[i];
@@ -78,17 +94,21 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_kernel(ArParams p) {
     while ((int)(__hip_atomic_load(&me->flag[b][tid], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       if (++spins > p.spin_limit) {
         __hip_atomic_store(&me->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        bad_sh = 1u;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
   }
   __syncthreads();
+  if (bad_sh) {  // a peer never arrived: this block's sum would mix stale staging (uniform)
+    poison();
+    return;
+  }
 
   const u32x4* stage[W];
 #pragma unroll
   for (int r = 0; r < W; ++r) stage[r] = reinterpret_cast<const u32x4*>(p.base[r] + stage_off);
-  u32x4* dst = reinterpret_cast<u32x4*>(p.data);
   for (long i = s0 + tid; i < s1; i += AR_THREADS) {
     u32x4 v[W];
 #pragma unroll
@@ -186,6 +206,13 @@ int ipc_probe(uintptr_t ptr) {
 }
 
 int ipc_close_handle(uintptr_t ptr) { return hipIpcCloseMemHandle(reinterpret_cast<void*>(ptr)); }
+
+// the error word copied to host memory behind the work already on `s` (no synchronisation: the
+// engine reads it after the step's own sync point)
+int allreduce_error_async(uintptr_t base, void* host_word, hipStream_t s) {
+  ArSignal* sig = reinterpret_cast<ArSignal*>(base);
+  return hipMemcpyAsync(host_word, &sig->error, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+}
 
 int allreduce_error(uintptr_t base, int clear) {
   uint32_t err = 0;

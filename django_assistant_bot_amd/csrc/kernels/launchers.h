@@ -153,5 +153,6 @@ int ipc_open_handle(const std::string& handle, uintptr_t* out);
 int ipc_close_handle(uintptr_t ptr);
 int ipc_probe(uintptr_t ptr);
 int allreduce_error(uintptr_t base, int clear);
+int allreduce_error_async(uintptr_t base, void* host_word, hipStream_t s);
 
 }  // namespace dab

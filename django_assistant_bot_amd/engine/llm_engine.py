@@ -494,6 +494,7 @@ class LLMEngine:
             # the shared prefix (e.g. the system prompt) instead of recomputing it
             self.blocks.commit_prefix(r.seq, s + n)
         pend = (chunks, reqs, toks, t0)
+        self._tp_fault_enqueue()
         if self.is_gpu:
             self._pending_prefill = pend  # read back after the next launch (step)
         else:
@@ -505,6 +506,7 @@ class LLMEngine:
         chunks, reqs, toks, t0 = pend
         if torch.is_tensor(toks):
             toks = toks.cpu().tolist()
+            self._tp_fault_check()  # synchronised: the error word copied behind the chunk is current
         self._collect_gpu_times(block=bool(reqs))
         now = time.perf_counter()
         for r, s, n in chunks:
@@ -584,7 +586,9 @@ class LLMEngine:
         sel_d = torch.as_tensor(sel, dtype=torch.long).to(dev, non_blocking=True)
         logits = self.model.logits(hidden.index_select(0, sel_d))
         preqs = [chunks[i][0] for i in last_rows]
+        self._tp_fault_enqueue()
         toks = self._sample(logits, preqs + batch)
+        self._tp_fault_check()
         self._collect_gpu_times()
         now = time.perf_counter()
         self.stats["prefill_tokens"] += Tp
@@ -703,6 +707,24 @@ class LLMEngine:
             logits = self.model.full_logits(logits)
         g = torch.Generator().manual_seed(int(self.seed * 7919 + int(cnt[0]) if n else 0))
         return ops.sample_tokens(logits, temps, topk, topp, self.seed, cnt, generator=g).tolist()
+
+    # ------------------------------------------------------------------ TP fault path
+    def _tp_fault_enqueue(self) -> None:
+        """TP on the GPU: the one-shot all-reduce's sticky error word is copied to the host behind
+        the step just enqueued (no sync here)."""
+        ar = getattr(self.model, "custom_ar", None)
+        if ar is not None and self.is_gpu:
+            ar.enqueue_error_check()
+
+    def _tp_fault_check(self) -> None:
+        """After the step's own sync: a set word means a TP peer missed an all-reduce (desynchronised
+        or dead group).  The step's outputs are poisoned, so it raises ``CustomAllReduceError`` before
+        any of its tokens is accepted; ``LLMWorker`` fails the in-flight requests (HTTP 500, as the
+        reference's failed ``generate``: gpu_service/main.py:105-107) and turns unhealthy (/health
+        503), and the launcher restarts the group."""
+        ar = getattr(self.model, "custom_ar", None)
+        if ar is not None and self.is_gpu:
+            ar.raise_if_error()
 
     def _tp_sync_tokens(self, toks):
         if self.tp_size > 1:
@@ -950,7 +972,9 @@ class LLMEngine:
             else:
                 self._tp_sync_tokens(self._d_tokens[:Bp])
             self._h_tokens[:Bp].copy_(self._d_tokens[:Bp], non_blocking=True)
+            self._tp_fault_enqueue()
             torch.cuda.current_stream(self.device).synchronize()
+            self._tp_fault_check()  # before any token of this step is accepted
         t2 = time.perf_counter()
         self._collect_gpu_times()
         toks = self._h_tokens[:B].tolist()

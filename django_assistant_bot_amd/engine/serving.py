@@ -119,7 +119,12 @@ class LLMWorker:
 
 def _sticky_device_error(exc: BaseException) -> bool:
     """HIP errors that leave the device context unusable (memory faults, illegal instructions,
-    ECC, hardware exceptions); after one the process must be restarted."""
+    ECC, hardware exceptions), and a broken TP group (a peer missed a one-shot all-reduce: every
+    later reduction on this rank is poisoned); after one the process must be restarted."""
+    from ..parallel.custom_allreduce import CustomAllReduceError
+
+    if isinstance(exc, CustomAllReduceError):
+        return True
     msg = str(exc).lower()
     return any(k in msg for k in ("illegal address", "illegal memory access", "memory access fault", "hiperrorillegal", "ecc error",
                                   "hardware exception", "device-side assert", "unspecified launch failure",

@@ -12,8 +12,14 @@ The buffers come from ``hipExtMallocWithFlags(..., hipDeviceMallocUncached)`` (f
 uncached: flag and staging accesses are coherent across xGMI, not only at kernel boundaries),
 outside the torch caching allocator, so IPC handles cover the whole allocation.  Each rank has one buffer: a signal area plus two staging halves of
 ``max_bytes``.  The kernel's epochs live on the device, so calls can be captured in HIP graphs.
-A peer that never arrives makes the kernel set an error flag instead of hanging;
-``check_error`` raises it on the host.
+A peer that never arrives makes the kernel set an error flag instead of hanging, write NaN over
+the segments it could not reduce and leave its epoch where it was; the flag is sticky, so every
+later call on this rank only poisons its output.  The engine enqueues a copy of the flag behind
+every TP step (``enqueue_error_check``) and raises ``CustomAllReduceError`` when it reads it set
+after the step's own sync (``raise_if_error``): the step's requests fail (gpu_service answers 500),
+the worker turns unhealthy (/health 503) and the launcher restarts the group -- the reference's
+"a failed generation is an HTTP 500" (gpu_service/main.py:105-107) for a desynchronised TP group.
+``check_error`` is the synchronous form (tests, benchmarks).
 """
 from __future__ import annotations
 
@@ -58,6 +64,11 @@ class CustomAllReduce:
                 n.ipc_probe(b)  # a bad mapping raises here, never inside the kernel
         self._closed = False
         self._exchange = exchange_group or group
+        # the error word's host copy (pinned: the async copy never stalls the stream)
+        self._err_host = torch.zeros((1,), dtype=torch.int32, pin_memory=True)
+        # fault injection (tests): this many of the next calls return without reducing, as a rank
+        # that dropped out of the collective would
+        self.skip_next = 0
         if self.world > 1:
             dist.barrier(group=self._exchange)
 
@@ -71,6 +82,9 @@ class CustomAllReduce:
         sum runs in rank order."""
         if not self.eligible(x):
             raise ValueError("custom all-reduce needs a contiguous bf16 CUDA tensor of <= max_bytes (16-B multiple)")
+        if self.skip_next > 0:
+            self.skip_next -= 1
+            return x
         self._n.custom_allreduce(self.bases, self.rank, x.data_ptr(), x.numel() * 2, self.max_bytes, self.spin_limit,
                                  stream(x))
         return x
@@ -79,6 +93,24 @@ class CustomAllReduce:
         """Call after a synchronisation point: raises if a peer failed to arrive within the spin limit."""
         if self._n.allreduce_error(self.base, 1):
             raise CustomAllReduceError("custom all-reduce: a peer did not arrive (group broken or desynchronised)")
+
+    def enqueue_error_check(self, s: int | None = None) -> None:
+        """Copies the error word to the pinned host word behind the work on stream ``s`` (default:
+        the current stream).  Read it with ``raise_if_error`` after that stream is synchronised."""
+        self._n.allreduce_error_async(self.base, self._err_host.data_ptr(),
+                                      torch.cuda.current_stream(self.device).cuda_stream if s is None else s)
+
+    def raise_if_error(self) -> None:
+        """After the stream that ran ``enqueue_error_check`` was synchronised: raises if a peer failed
+        to arrive in any all-reduce enqueued before it.  The word stays set on the device (sticky)
+        until ``reset_error``."""
+        if int(self._err_host[0]):
+            raise CustomAllReduceError("custom all-reduce: a TP peer did not arrive (group broken or desynchronised); "
+                                       "the step's outputs are poisoned")
+
+    def reset_error(self) -> None:
+        self._n.allreduce_error(self.base, 1)
+        self._err_host.zero_()
 
     def close(self) -> None:
         """Collective: no rank frees its buffer while a peer's last kernel may still read it."""

@@ -1,5 +1,6 @@
 """LLMEngine scheduling on CPU (reference ops, native block manager): mixed prefill+decode steps must
 give the same greedy tokens as the prefill-then-decode schedule, and the mixed path must actually run."""
+import pytest
 import torch
 
 from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
@@ -117,6 +118,35 @@ def test_worker_survives_injected_faults_and_flags_sticky_ones():
             assert not h["healthy"] and "fault-test" in h["unhealthy_workers"]
         finally:
             serving._llm.pop("fault-test", None)
+    finally:
+        worker.stop()
+
+
+def test_worker_marks_a_broken_tp_group_unhealthy():
+    """A TP step that raises ``CustomAllReduceError`` (a peer missed a one-shot all-reduce: the
+    step's outputs are poisoned) fails the in-flight requests and turns the worker unhealthy, so
+    gpu_service /health answers 503 and the launcher restarts the group."""
+    from django_assistant_bot_amd.engine import serving
+    from django_assistant_bot_amd.parallel.custom_allreduce import CustomAllReduceError
+
+    eng = _engine(0, _weights())
+    worker = serving.LLMWorker(eng)
+    try:
+        sp = SamplingParams(max_new_tokens=5, do_sample=False, temperature=0.0, ignore_eos=True)
+
+        def broken(e):
+            raise CustomAllReduceError("custom all-reduce: a TP peer did not arrive")
+        eng.fault_hook = broken
+        fut = worker.submit(list(range(5, 25)), sp)
+        with pytest.raises(CustomAllReduceError):
+            fut.result(timeout=60)
+        assert not worker.healthy and "TP peer" in worker.last_error
+        assert not eng.has_unfinished() and not eng.finished
+        serving._llm["tp-test"] = worker
+        try:
+            assert not serving.health()["healthy"]
+        finally:
+            serving._llm.pop("tp-test", None)
     finally:
         worker.stop()
 
