@@ -100,18 +100,22 @@ __device__ uint32_t radix_kth(KeyAt key_at, int n, int k, SelShared& sh, uint32_
 }
 
 // Gathers the k largest keys (ties at the k-th key taken in arbitrary order) into sh.cand_*[0..k)
-// and sorts them descending by key (ascending index among equal keys).
-template <class KeyAt>
-__device__ void select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
+// and sorts them descending by key (ascending index among equal keys).  TIES_ALL: every key equal
+// to the k-th is kept too (HF TopKLogitsWarper keeps all logits >= the k-th value), up to SEL_MAXK
+// candidates; returns the number kept (k without TIES_ALL).
+template <bool TIES_ALL = false, class KeyAt>
+__device__ int select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
   const int tid = threadIdx.x;
   uint32_t ties;
   const uint32_t kth = radix_kth(key_at, n, k, sh, ties);
+  const uint32_t n_gt0 = (uint32_t)k - ties;
+  if (TIES_ALL) ties = (uint32_t)SEL_MAXK - n_gt0;  // capacity for the tied keys
   if (tid == 0) {
     sh.cnt_gt = 0;
     sh.cnt_eq = 0;
   }
   __syncthreads();
-  const uint32_t n_gt = (uint32_t)k - ties;
+  const uint32_t n_gt = n_gt0;
   for (int i0 = 0; i0 < n; i0 += SEL_NT) {
     const int i = i0 + tid;
     uint32_t key = 0;
@@ -128,6 +132,7 @@ __device__ void select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
     }
   }
   __syncthreads();
+  if (TIES_ALL) k = (int)(n_gt + min(sh.cnt_eq, ties));
   int P = 1;
   while (P < k) P <<= 1;
   for (int i = k + tid; i < P; i += SEL_NT) {
@@ -156,6 +161,7 @@ __device__ void select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
       __syncthreads();
     }
   }
+  return k;
 }
 
 __device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
@@ -183,7 +189,9 @@ __global__ __launch_bounds__(SEL_NT) void sample_kernel(const void* __restrict__
   const float* lf = reinterpret_cast<const float*>(logits) + (size_t)row * ld;
   const bf16* lb = reinterpret_cast<const bf16*>(logits) + (size_t)row * ld;
   auto key_at = [&](int i) -> uint32_t { return float_key(f32 ? lf[i] : bf2f(lb[i])); };
-  select_topk(key_at, vocab, k, sh);
+  // HF TopKLogitsWarper keeps every logit >= the k-th value (ties beyond k included); greedy takes
+  // the lowest index among equal maxima (torch.argmax)
+  k = select_topk<true>(key_at, vocab, k, sh);
   if (threadIdx.x != 0) return;
   if (T <= 0.f) {
     out_tokens[row] = sh.cand_idx[0];
@@ -481,11 +489,12 @@ __global__ __launch_bounds__(SEL_NT) void sample_merge_kernel(const uint32_t* __
                                                               int* __restrict__ out_tokens) {
   __shared__ uint32_t skey[SEL_MAXK];
   __shared__ int sidx[SEL_MAXK];
-  __shared__ float probs[64];
+  __shared__ float probs[SEL_MAXK];
   const int row = blockIdx.x, tid = threadIdx.x;
   const float T = temperature ? temperature[row] : 1.f;
   int k = (T <= 0.f) ? 1 : (top_k && top_k[row] > 0 ? top_k[row] : 64);
   k = min(k, min(64, vocab));
+  const int nc = min(ncand, SEL_MAXK);
   for (int i = tid; i < SEL_MAXK; i += SEL_NT) {
     skey[i] = i < ncand ? cand_key[(size_t)row * ncand + i] : 0u;
     sidx[i] = i < ncand ? cand_idx[(size_t)row * ncand + i] : 0x7fffffff;
@@ -516,6 +525,9 @@ __global__ __launch_bounds__(SEL_NT) void sample_merge_kernel(const uint32_t* __
     out_tokens[row] = sidx[0];
     return;
   }
+  // HF TopKLogitsWarper: the candidates tied with the k-th value stay in (exact while no 8192-token
+  // chunk holds more than 64 logits >= the k-th value: the chunk stage keeps 64 per chunk)
+  while (k < nc && skey[k] == skey[k - 1] && skey[k] != 0u) ++k;
   const float P = top_p ? top_p[row] : 1.f;
   const float x0 = key_float(skey[0]) / T;
   float total = 0.f;
