@@ -531,6 +531,14 @@ def main():
                 "full_pipeline_qps": round(n_rep * B / (batch_s + fast["total_s"]), 3),
                 "full_pipeline_p50_latency_ms": round(1000 * (p50 + fast["total_s"]), 1)}
     cfg5 = args.config == 5
+    tp_info = {}
+    if args.tp > 1:
+        hbm = [round(x / 2 ** 30, 2) for x in pdist.gather_floats(
+            float(torch.cuda.max_memory_allocated(dev)) if dev.type == "cuda" else 0.0, dev)]
+        tp_info = {"tp_allreduce_calls_rank0": dict(llm.model.ar_counts),
+                   "tp_allreduce_note": "Python-issued calls; a call captured in a decode graph counts once",
+                   "kv_blocks_rank0": int(llm.blocks.num_blocks()),
+                   "hbm_peak_gb_per_rank": hbm}
     out = {
         "metric": METRIC_CONFIG5 if cfg5 else METRIC,
         "value": round(qps, 3),
@@ -573,6 +581,7 @@ def main():
             "engine_rank0": eng,
             **({"fast_steps": fast} if fast else {}),
             "phases_rank0_s": {k: round(float(np.mean(v)), 4) for k, v in phases.items() if v},
+            **tp_info,
         },
     }
     if R == 0:

@@ -158,6 +158,9 @@ class LlamaModel:
             torch.cuda.empty_cache()
 
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
+        # TP all-reduces issued from Python: one-shot IPC vs the process group (RCCL / gloo); a call
+        # captured into a decode graph counts once, at capture, not per replay
+        self.ar_counts = {"ipc": 0, "group": 0}
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -199,9 +202,11 @@ class LlamaModel:
         if self.tp_size > 1:
             ar = self.custom_ar
             if ar is not None and ar.eligible(x):
+                self.ar_counts["ipc"] += 1
                 return ar.all_reduce(x)
             import torch.distributed as dist
 
+            self.ar_counts["group"] += 1
             dist.all_reduce(x, group=self.tp_group)
         return x
 
