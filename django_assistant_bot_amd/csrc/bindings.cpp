@@ -36,6 +36,13 @@ PYBIND11_MODULE(_native, m) {
                                long spin_limit, u s) {
     check(dab::custom_allreduce(bases, rank, VP(data), nbytes, half_bytes, spin_limit, ST(s)), "custom_allreduce");
   });
+  m.def("custom_allreduce_rmsnorm", [](const std::vector<uintptr_t>& bases, int rank, u slabs, int S, long slab_stride,
+                                       u x, u res_in, u res_out, u out, u w, int rows, int cols, float eps,
+                                       long half_bytes, long spin_limit, u s) {
+    check(dab::custom_allreduce_rmsnorm(bases, rank, (const float*)slabs, S, slab_stride, CVP(x), CVP(res_in),
+                                        VP(res_out), VP(out), CVP(w), rows, cols, eps, half_bytes, spin_limit, ST(s)),
+          "custom_allreduce_rmsnorm");
+  });
   m.def("allreduce_buffer_alloc", [](long bytes, bool uncached) {
     uintptr_t p = 0;
     check(dab::allreduce_buffer_alloc(bytes, uncached ? 1 : 0, &p), "allreduce_buffer_alloc");

@@ -144,6 +144,12 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
 
 // allreduce.hip: one-shot all-reduce over IPC-mapped peer buffers (TP decode on one node)
 size_t allreduce_signal_bytes();
+// TP decode: this rank's split-K slabs (S > 0) or bf16 partial (S == 0) -> all-reduce -> + residual
+// -> RMSNorm, one launch (bitwise slab_reduce + custom_allreduce + rmsnorm)
+int custom_allreduce_rmsnorm(const std::vector<uintptr_t>& bases, int rank, const float* slabs, int S,
+                             long slab_stride, const void* x, const void* res_in, void* res_out, void* out,
+                             const void* w, int rows, int cols, float eps, long half_bytes, long spin_limit,
+                             hipStream_t s);
 int custom_allreduce(const std::vector<uintptr_t>& bases, int rank, void* data, long nbytes, long half_bytes,
                      long spin_limit, hipStream_t s);
 int allreduce_buffer_alloc(long bytes, int uncached, uintptr_t* out);

@@ -60,6 +60,17 @@ class AttnMeta:
     # of the decode rows in a mixed step)
 
 
+class _Partial:
+    """This rank's un-reduced TP partial sum of a row-parallel projection (fp32 split-K slabs or
+    bf16): the all-reduce is still due and runs fused into the RMSNorm that consumes it
+    (``LlamaModel._norm``: one launch instead of slab_reduce + all-reduce + rmsnorm)."""
+
+    __slots__ = ("t",)
+
+    def __init__(self, t: torch.Tensor):
+        self.t = t
+
+
 class KVCache:
     """Paged KV cache: per layer [num_blocks, Hkv_local, block_size, D] for K and for V."""
 
@@ -344,7 +355,28 @@ class LlamaModel:
     def _final_norm(self, x, residual):
         if x is None:  # the residual stream holds the last layer's output
             return ops.rmsnorm(residual, self.final_norm, self.cfg.eps)[0]
-        return ops.rmsnorm(x, self.final_norm, self.cfg.eps, residual=residual)[0]
+        return self._norm(x, self.final_norm, residual)[0]
+
+    def _norm(self, x, w, residual):
+        """RMSNorm(x + residual) -> (normed, new residual); x may be a ``_Partial`` whose TP
+        all-reduce runs inside the same launch (``CustomAllReduce.all_reduce_rmsnorm``)."""
+        if isinstance(x, _Partial):
+            return self.custom_ar.all_reduce_rmsnorm(x.t, residual, w, self.cfg.eps)
+        return ops.rmsnorm(x, w, self.cfg.eps, residual=residual)
+
+    # TP decode all-reduce sites fused with their consumer RMSNorm (VERDICT r5 item 8); off: the
+    # separate slab_reduce / all-reduce / rmsnorm launches (A/B and the bit-exactness test)
+    tp_fused_norm = True
+
+    def _tp_partial(self, x, cols: int):
+        """A row-parallel projection's output under TP: a ``_Partial`` when the fused all-reduce +
+        norm can take it, else the all-reduced bf16 tensor."""
+        ar = self.custom_ar
+        if self.tp_fused_norm and ar is not None and x.is_cuda and ar.norm_eligible(x, cols):
+            return _Partial(x)
+        if x.dtype == torch.float32 and x.dim() == 3:
+            x = ops.slab_reduce(x)
+        return self._all_reduce(x)
 
     def _layer(self, li: int, L: DecoderLayer, x, residual, meta: AttnMeta, kv: KVCache, sk: bool):
         """One decoder layer: (layer input, residual stream) -> (next layer input, residual stream)."""
@@ -360,7 +392,7 @@ class LlamaModel:
             h, _ = ops.rmsnorm(x, L.attn_norm, cfg.eps)
             residual = x
         else:
-            h, residual = ops.rmsnorm(x, L.attn_norm, cfg.eps, residual=residual)
+            h, residual = self._norm(x, L.attn_norm, residual)
         qkv = self._proj(h, L.qkv_w, sk, name="qkv")
         if (not meta.decode and not meta.n_decode and qkv.is_cuda and qkv.dtype == torch.bfloat16
                 and ops.kernels.flash_rope_ok(D, kv.block_size)):
@@ -389,6 +421,10 @@ class LlamaModel:
         if fuse:
             residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual, shuffled=self.frag)
             h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)
+        elif sk and self.tp_size > 1:
+            # TP decode: the o partial (split-K slabs) meets its all-reduce inside the MLP norm's launch
+            o = self._tp_partial(self._proj(a.view(T, self.hq * D), L.o_w, sk, True, name="o"), cfg.hidden)
+            h, residual = self._norm(o, L.mlp_norm, residual)
         else:
             o = self._all_reduce(self._proj(a.view(T, self.hq * D), L.o_w, sk, slabs_ok, name="o"))
             h, residual = ops.rmsnorm(o, L.mlp_norm, cfg.eps, residual=residual)
@@ -399,6 +435,8 @@ class LlamaModel:
             act = ops.silu_mul(act)
         if fuse:
             return None, ops.gemm_bt(act, L.down_w, residual=residual, shuffled=self.frag)
+        if sk and self.tp_size > 1:  # reduced inside the next layer's (or the final) norm launch
+            return self._tp_partial(self._proj(act, L.down_w, sk, True, name="down"), cfg.hidden), residual
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))
         return x, residual
 

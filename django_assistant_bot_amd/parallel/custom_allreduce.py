@@ -94,6 +94,40 @@ class CustomAllReduce:
         if self._n.allreduce_error(self.base, 1):
             raise CustomAllReduceError("custom all-reduce: a peer did not arrive (group broken or desynchronised)")
 
+    def norm_eligible(self, partial: torch.Tensor, cols: int) -> bool:
+        """Whether ``all_reduce_rmsnorm`` takes this partial: fp32 slabs [S, rows, cols] or bf16
+        [rows, cols], contiguous, whose bf16 rows fit one staging half."""
+        if not partial.is_cuda or not partial.is_contiguous() or cols % 8 or cols > 16384:
+            return False
+        rows = partial.shape[-2]
+        ok_dtype = (partial.dtype == torch.float32 and partial.dim() == 3) or \
+                   (partial.dtype == torch.bfloat16 and partial.dim() == 2)
+        return ok_dtype and partial.shape[-1] == cols and rows * cols * 2 <= self.max_bytes
+
+    def all_reduce_rmsnorm(self, partial: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor, eps: float):
+        """One launch for a TP decode all-reduce site: sums this rank's split-K slabs (or takes its
+        bf16 partial), all-reduces over the group, adds the residual and applies the RMSNorm ->
+        (normed, new residual).  Bitwise ``slab_reduce`` + ``all_reduce`` + ``ops.rmsnorm``."""
+        cols = w.numel()
+        if not self.norm_eligible(partial, cols):
+            raise ValueError("all_reduce_rmsnorm: fp32 slabs [S, rows, cols] or bf16 [rows, cols] within max_bytes")
+        rows = partial.shape[-2]
+        out = torch.empty((rows, cols), dtype=torch.bfloat16, device=partial.device)
+        res_out = torch.empty_like(out) if residual is not None else None
+        if residual is not None and (residual.dtype != torch.bfloat16 or not residual.is_contiguous()
+                                     or tuple(residual.shape) != (rows, cols)):
+            raise ValueError("residual must be a contiguous bf16 [rows, cols]")
+        slabs = partial.dtype == torch.float32
+        if self.skip_next > 0:  # fault injection: this rank drops out of the collective
+            self.skip_next -= 1
+            return out.zero_(), (res_out.zero_() if res_out is not None else None)
+        self._n.custom_allreduce_rmsnorm(
+            self.bases, self.rank, partial.data_ptr() if slabs else 0, partial.shape[0] if slabs else 0,
+            rows * cols if slabs else 0, 0 if slabs else partial.data_ptr(),
+            residual.data_ptr() if residual is not None else 0, res_out.data_ptr() if res_out is not None else 0,
+            out.data_ptr(), w.data_ptr(), rows, cols, float(eps), self.max_bytes, self.spin_limit, stream(partial))
+        return out, res_out
+
     def enqueue_error_check(self, s: int | None = None) -> None:
         """Copies the error word to the pinned host word behind the work on stream ``s`` (default:
         the current stream).  Read it with ``raise_if_error`` after that stream is synchronised."""

@@ -78,6 +78,29 @@ def _body(rank, world, port, out_dir, uncached=True):
             if not torch.allclose(buf.cpu().float(), exp.float(), rtol=1e-2, atol=1e-2):
                 errors.append(f"graph replay {it}")
         ar.check_error()
+        # fused slab sum + all-reduce + residual + RMSNorm: bitwise the unfused sequence
+        from django_assistant_bot_amd import ops
+
+        for rows, cols, S in ((3, 4096, 8), (128, 8192, 4), (70, 1024, 1), (128, 4096, 0)):
+            def part(r):
+                g = torch.Generator().manual_seed(7000 + 31 * r + rows)
+                if S == 0:
+                    return torch.randn(rows, cols, generator=g).to(torch.bfloat16).to(dev)
+                return torch.randn(S, rows, cols, generator=g).to(dev)
+            g = torch.Generator().manual_seed(99 + rows)
+            res = torch.randn(rows, cols, generator=g).to(torch.bfloat16).to(dev)
+            w = (0.5 + torch.rand(cols, generator=g)).to(torch.bfloat16).to(dev)
+            out, res_out = ar.all_reduce_rmsnorm(part(rank), res, w, 1e-5)
+            torch.cuda.synchronize()
+            acc = None
+            for r in range(world):
+                p_r = part(r)
+                p_r = ops.slab_reduce(p_r) if S else p_r
+                acc = p_r.float() if acc is None else acc + p_r.float()
+            exp_out, exp_res = ops.rmsnorm(acc.to(torch.bfloat16), w, 1e-5, residual=res)
+            if not (torch.equal(out, exp_out) and torch.equal(res_out, exp_res)):
+                errors.append(f"fused norm rows={rows} cols={cols} S={S}")
+        ar.check_error()
     except Exception as exc:  # report, do not hang the other ranks' joins
         errors.append(repr(exc))
     finally:
@@ -103,3 +126,29 @@ def test_one_shot_allreduce_multi_process(world, uncached, tmp_path):
     assert not alive, "all-reduce ranks hung"
     res = [open(tmp_path / f"r{r}.txt").read() for r in range(world)]
     assert res == ["ok"] * world, res
+
+
+@pytest.mark.parametrize("rows,cols,S", [(1, 8192, 8), (7, 4096, 4), (128, 4096, 8), (128, 8192, 2), (200, 1024, 0)])
+def test_fused_allreduce_rmsnorm_is_the_unfused_sequence_at_tp1(rows, cols, S):
+    """one launch (slab sum -> one-shot all-reduce -> residual -> RMSNorm) is
+    bit-identical to slab_reduce + all_reduce + rmsnorm, here at W = 1 (one process)."""
+    from django_assistant_bot_amd import ops
+    from django_assistant_bot_amd.parallel.custom_allreduce import CustomAllReduce
+
+    dev = torch.device("cuda", 0)
+    ar = CustomAllReduce(None, dev, max_bytes=4 << 20)
+    try:
+        g = torch.Generator().manual_seed(rows * 7 + S)
+        part = (torch.randn(S, rows, cols, generator=g).to(dev) if S else
+                torch.randn(rows, cols, generator=g).to(torch.bfloat16).to(dev))
+        res = torch.randn(rows, cols, generator=g).to(torch.bfloat16).to(dev)
+        w = (0.5 + torch.rand(cols, generator=g)).to(torch.bfloat16).to(dev)
+        out, res_out = ar.all_reduce_rmsnorm(part, res, w, 1e-5)
+        x = ops.slab_reduce(part) if S else part.clone()
+        ar.all_reduce(x)
+        exp_out, exp_res = ops.rmsnorm(x, w, 1e-5, residual=res)
+        torch.cuda.synchronize()
+        assert torch.equal(out, exp_out) and torch.equal(res_out, exp_res)
+        ar.check_error()
+    finally:
+        ar.close()
