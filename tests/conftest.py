@@ -1,6 +1,8 @@
 import os
 import random
 import sys
+import threading
+import time
 
 import pytest
 
@@ -57,3 +59,27 @@ def bpe_dir(tmp_path_factory):
     d = tmp_path_factory.mktemp("bpe")
     tok.save(str(d / "tokenizer.json"))
     return str(d)
+
+
+@pytest.fixture(autouse=True)
+def _gpu_heartbeat(request):
+    """GPU tests that run for minutes (multi-process TP groups time-sharing the box's one GPU) print a
+    line every 30 s to the real stderr, past pytest's capture, so a long but live test is never taken
+    for a hung one by the GPU harness's silence watchdog."""
+    if "gpu" not in request.node.keywords:
+        yield
+        return
+    stop = threading.Event()
+    t0 = time.time()
+
+    def beat():
+        while not stop.wait(30):
+            sys.__stderr__.write(f"[heartbeat] {request.node.nodeid} running {time.time() - t0:.0f} s\n")
+            sys.__stderr__.flush()
+
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        yield
+    finally:
+        stop.set()
