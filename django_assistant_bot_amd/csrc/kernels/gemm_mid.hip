@@ -19,13 +19,17 @@
 //     L2 (groups are formed from blocks that share blockIdx % 8).  The iteration space
 //     tiles_n x (K / 64) is split evenly over the 8 x floor(32 / tiles_m) groups (stream-K in the
 //     N x K plane): every CU gets the same number of MFMAs whatever the tile count;
-//   * a tile whose K range spans several groups is combined in-launch by the last arriver: every
-//     segment stores its fp32 partial (write-through sc1 stores, 1 KB per wave-instruction), drains,
-//     and bumps the tile's arrival counter (agent-scope atomic); the workgroup that draws the last
-//     ticket reads the other partials with sc1 loads (no fence needed: cdna_hip_programming.md
-//     section 5 item 2), sums ALL segments in segment order (its own from registers: the result is
-//     the same whichever segment arrives last), resets the counter and runs the epilogue.  Nothing
-//     waits on another workgroup, so there is no spin and no residency requirement.
+//   * a tile whose K range spans several groups is combined in-launch by its OWNER, the group
+//     holding the tile's first K-steps: that segment ends the owner's range, so in time it finishes
+//     last.  The other segments store their fp32 partial (write-through sc1 stores, 1 KB per
+//     wave-instruction) and raise a per-slot ready flag two K-steps later, when the pipeline's own
+//     counted wait has retired the stores (no drain); the owner keeps its partial in registers,
+//     waits for each flag (bounded spin), adds the partials with sc1 loads in segment order (no
+//     fence needed: cdna_hip_programming.md section 5 item 2), clears the flags and runs the
+//     epilogue.  Only owners wait, on producers that never wait, so there is no deadlock (and the
+//     grid is at most one workgroup per CU).  Replaces a last-arriver combine (every segment stored
+//     and drained, then an atomic ticket) that cost 5-9 us per launch on the small projections
+//     (profiles/gemm_mid_r6.md).
 #include "common.h"
 #include "launchers.h"
 
@@ -41,7 +45,7 @@ struct GMid {
   bf16* C;
   const bf16* residual;
   float* slabs;  // [tiles_m][gn][2] partial tiles of 128 x 256 fp32 (in accumulator order)
-  int* cnt;      // [tiles_m * tiles_n] arrival counters, zero at rest
+  int* cnt;      // [tiles_m][gn][2] ready flags of the stored partial tiles, zero at rest
   int M, N, K;
   long lda, ldc, ldr;
   int tiles_m, tiles_n, kt;
@@ -89,6 +93,7 @@ struct MidGeo {
   static_assert(kSmem <= 163840, "LDS");
 };
 constexpr int kE = 8;                  // VMEM stores per wave in every epilogue variant
+constexpr int kSlabSt = 16;            // VMEM stores per wave of a published partial tile
 constexpr int kSlabFloats = 512 * 64;  // one partial tile: 512 threads x 16 f32x4
 
 // group start of the balanced split of the iteration space
@@ -220,8 +225,19 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
 
   int it = start;
   int b = 0;  // ring buffer of iteration `it`
-  bool after_epi = false;
+  // VMEM stores issued since the last phase's wait (younger than the DMA in flight): an epilogue's
+  // kE or a published partial's kSlabSt; the next phase's counted wait lets them stay in flight
+  int after_st = 0;
+  // a partial tile stored by this workgroup whose ready flag is not raised yet: raised at the
+  // second phase after the stores, when that phase's vmcnt(kDma) has retired them (no drain)
+  int pend_flag = -1, pend_phases = 0;
   const __amdgpu_buffer_rsrc_t rS = mk_rsrc(p.slabs, p.slab_bytes);
+  auto slab_off = [&](int jj, int side) { return (unsigned)(((mt * p.gn + jj) * 2 + side) * kSlabFloats) * 4u; };
+  auto flag_of = [&](int jj, int side) { return p.cnt + (mt * p.gn + jj) * 2 + side; };
+  auto raise_flag = [&]() {  // after every wave's stores retired and a barrier
+    if (tid == 0) __hip_atomic_store(p.cnt + pend_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pend_flag = -1;
+  };
   while (it < end) {
     const int nt = it / kt;
     const int k0 = it - nt * kt;
@@ -242,19 +258,21 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
       if (s_it < end) {
         stage(b == 0 ? kStages - 1 : b - 1, s_nt, s_kk);
         advance();
-        if (after_epi) wait_vmc<(kDist - 1) * kDma + kE>();
+        if (after_st == kSlabSt) wait_vmc<(kDist - 1) * kDma + kSlabSt>();
+        else if (after_st == kE) wait_vmc<(kDist - 1) * kDma + kE>();
         else wait_vmc<(kDist - 1) * kDma>();
       } else {
         // tail: the stages after `it + 1` that are still in flight may stay so
-        const int beyond = after_epi ? 0 : s_it - it - 2;
+        const int beyond = after_st ? 0 : s_it - it - 2;
         if (beyond >= 4) wait_vmc<4 * kDma>();
         else if (beyond == 3) wait_vmc<3 * kDma>();
         else if (beyond == 2) wait_vmc<2 * kDma>();
         else if (beyond == 1) wait_vmc<kDma>();
         else wait_vmc<0>();
       }
-      after_epi = false;
+      after_st = 0;
       mread_bar();
+      if (pend_flag >= 0 && ++pend_phases >= 2) raise_flag();  // this phase's wait retired the stores
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
@@ -267,65 +285,85 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
       b = b == kStages - 1 ? 0 : b + 1;
     }
     if (wr == 0) mbar();  // pairs with group 1's last K-loop barrier
+    if (pend_flag >= 0) {  // (a one-phase segment followed: drain and raise now)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      raise_flag();
+    }
 
-    // ---- segment end: a whole tile goes straight to the epilogue; a part is combined
+    // ---- segment end.  A whole tile goes straight to the epilogue.  A split tile's segments are
+    // held by groups j_lo .. j_hi in K order; its OWNER is j_lo, whose segment (the tile's first
+    // K-steps) ends its own range, so in time it finishes last.  The other segments store their
+    // fp32 partial (sc1, write-through) and raise a per-slot ready flag; the owner never stores its
+    // own, waits for each flag (bounded spin), adds the partials in segment order (its registers
+    // first), clears the flags and runs the epilogue.  Nobody else waits, so the owner's wait
+    // cannot deadlock (and the grid is <= one workgroup per CU anyway).
     const int n0 = nt * 256;
     bool write = true;
     if (k0 != 0 || k1 != kt) {
-      const int tile = mt * p.tiles_n + nt;
-      const int side = start >= nt * kt ? 0 : 1;
-      const unsigned own = (unsigned)(((mt * p.gn + j) * 2 + side) * kSlabFloats) * 4u;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int jn = 0; jn < 4; ++jn)
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][jn]), rS,
-                                                 own + (unsigned)(((i * 4 + jn) * 512 + tid) * 16), 0, 16);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains (R1)
-      __syncthreads();
       const int j_lo = grp_owner(nt * kt, p.q, p.r), j_hi = grp_owner(nt * kt + kt - 1, p.q, p.r);
-      // the broadcast word: the buffer of the stage just consumed (nothing in flight writes it)
-      int* flag = reinterpret_cast<int*>(smem + (b == 0 ? kStages - 1 : b - 1) * kStage);
-      if (tid == 0) *flag = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int old = __builtin_amdgcn_readfirstlane(*flag);
-      mread_bar();  // every wave has its copy before the next stage's DMA may overwrite the word
-      write = old == j_hi - j_lo && DIAG == 0;
-      if (old == j_hi - j_lo && tid == 0) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (write) {
-        f32x4 tot[4][4];
+      const int side = start >= nt * kt ? 0 : 1;
+      if (j != j_lo) {
+        const unsigned own = slab_off(j, side);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn) tot[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // every segment in segment order (its own from registers): the sum does not depend on
-        // which segment arrived last
-        for (int jj = j_lo; jj <= j_hi; ++jj) {
-          if (jj == j) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int jn = 0; jn < 4; ++jn) tot[i][jn] += acc[i][jn];
-          } else {
-            const int sd = grp_start(jj, p.q, p.r) >= nt * kt ? 0 : 1;
-            const unsigned off = (unsigned)(((mt * p.gn + jj) * 2 + sd) * kSlabFloats) * 4u;
-            u32x4 v[4][4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int jn = 0; jn < 4; ++jn)
-                v[i][jn] = __builtin_amdgcn_raw_buffer_load_b128(rS, off + (unsigned)(((i * 4 + jn) * 512 + tid) * 16),
-                                                                 0, 16);
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-              for (int jn = 0; jn < 4; ++jn) tot[i][jn] += __builtin_bit_cast(f32x4, v[i][jn]);
+          for (int jn = 0; jn < 4; ++jn)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][jn]), rS,
+                                                   own + (unsigned)(((i * 4 + jn) * 512 + tid) * 16), 0, 16);
+        after_st = kSlabSt;
+        if (!DIAG) {  // (DIAG: the owner reads nothing, so no flag may be left raised)
+          pend_flag = (int)(flag_of(j, side) - p.cnt);
+          pend_phases = 0;
+          if (it >= end) {  // nothing left to hide the drain behind
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            raise_flag();
           }
         }
+        write = false;
+      } else if (DIAG) {
+        write = false;
+      } else {
+        bool ok = true;
+        for (int jj = j_lo + 1; jj <= j_hi; ++jj) {
+          const int sd = grp_start(jj, p.q, p.r) >= nt * kt ? 0 : 1;
+          int* fl = flag_of(jj, sd);
+          if (tid == 0) {
+            long spins = 0;
+            while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+              if (++spins > (1L << 22)) {
+                ok = false;  // a producer never published (cannot happen in a healthy launch)
+                break;
+              }
+              __builtin_amdgcn_s_sleep(2);
+            }
+            if (ok) __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+          __syncthreads();  // every thread loads only after lane 0 saw the flag
+          const unsigned off = slab_off(jj, sd);
+          u32x4 v[4][4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn) acc[i][jn] = tot[i][jn];
+            for (int jn = 0; jn < 4; ++jn)
+              v[i][jn] = __builtin_amdgcn_raw_buffer_load_b128(rS, off + (unsigned)(((i * 4 + jn) * 512 + tid) * 16),
+                                                               0, 16);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) acc[i][jn] += __builtin_bit_cast(f32x4, v[i][jn]);
+        }
+        ok = __builtin_amdgcn_readfirstlane((int)ok) != 0 || tid != 0;
+        if (!__syncthreads_and(ok)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jn = 0; jn < 4; ++jn) {
+              const float nan = __builtin_nanf("");
+              acc[i][jn] = f32x4{nan, nan, nan, nan};
+            }
+        }
       }
     }
     if (write) {
@@ -401,7 +439,7 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
           }
         }
       }
-      after_epi = true;
+      after_st = kE;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -430,7 +468,12 @@ int gemm_mid_ok(int M, int N, int K, long lda) {
 
 // Workspace the launcher needs: partial slabs (bytes) and arrival counters (ints).
 long gemm_mid_slab_bytes() { return (long)cu_count() * 2 * kSlabFloats * 4; }
-int gemm_mid_counters(int M, int N) { return ((M + 127) / 128) * (N / 256); }
+// ready flags of the partial tiles: two per (row tile, group) <= two per workgroup
+int gemm_mid_counters(int M, int N) {
+  (void)M;
+  (void)N;
+  return 2 * (cu_count() & ~7);
+}
 
 // epilogue 0: C = A B^T (+ residual, bf16 add after rounding); 4: SwiGLU over 8-row [gate | up]
 // groups (C has N / 2 columns).  slabs: gemm_mid_slab_bytes() bytes; cnt: >= gemm_mid_counters()

@@ -456,9 +456,9 @@ _MID_WS: dict = {}
 
 
 def _mid_workspace(device: torch.device, s: int):
-    """Partial-tile slabs + arrival counters of ``gemm_mid``, one set per (device, stream): two
-    streams running the kernel at once must not share counters.  The counters are zero at rest (every
-    launch leaves them zero)."""
+    """Partial-tile slabs + ready flags of ``gemm_mid``, one set per (device, stream): two streams
+    running the kernel at once must not share them.  The flags are zero at rest (every launch leaves
+    them zero)."""
     key = (device.index, s)
     ws = _MID_WS.get(key)
     if ws is None:
@@ -476,7 +476,7 @@ def gemm_mid_ok(M: int, N: int, K: int, lda: int) -> bool:
 
 def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0):
     """C = A . B^T (+ residual) or SwiGLU over 8-row [gate | up] groups, B a ``shuffle_weights`` copy:
-    the mid-M kernel (``gemm_mid.hip``: grouped stream-K, 128 x 256 tiles, in-launch combine) for
+    the mid-M kernel (``gemm_mid.hip``: grouped stream-K, 128 x 256 tiles, in-launch owner combine) for
     M = 256..4096 (mixed serving steps, single prompts).  Bit-reproducible: the split-K partials are
     summed in a fixed order.  ``variant`` (A/B harness): 32 / 64 force the K-step; + 1000 leaves
     split tiles uncombined (timing only)."""
