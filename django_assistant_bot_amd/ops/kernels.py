@@ -348,14 +348,23 @@ GEMM_MID_MIN_M = 192
 GEMM_MID_FILL = 192  # gemm256 keeps a shape whose 256 x 256 tiles fill this many of the 256 CUs
 
 
+def _g256_fill(M: int, N: int) -> tuple[int, float]:
+    """(256 x 256 tiles, share of the last-wave-padded CU slots they fill) of gemm256 on 256 CUs."""
+    tiles = -(-M // 256) * (N // 256)
+    return tiles, tiles / (-(-tiles // 256) * 256)
+
+
 def use_gemm_mid(M: int, N: int, K: int, lda: int) -> bool:
     """Mid-M shapes on fragment-layout weights go to the stream-K kernel (gemm_mid.hip) where the
-    256 x 256 kernel would leave CUs idle: -(-M // 256) * (N / 256) < GEMM_MID_FILL tiles.  Measured
-    (profiles/gemm_mid_r6.md): Llama-3-8B qkv / o / down at M = 384..2048 run 1.2-2.3x faster than the
-    round-5 dispatch (the 128 x 128 kernel / underfilled gemm256); gate_up (112 tile columns) and
-    qkv at M >= 2048 stay on gemm256."""
-    return (M >= GEMM_MID_MIN_M and N % 256 == 0 and -(-M // 256) * (N // 256) < GEMM_MID_FILL
-            and gemm_mid_ok(M, N, K, lda))
+    256 x 256 kernel would leave CUs idle: fewer than GEMM_MID_FILL tiles, or a last wave that
+    leaves the chip under 70 % busy.  Measured (profiles/gemm_mid_r6.md): Llama-3-8B qkv / o / down
+    at M = 384..2048 run 1.2-2.5x faster than the round-5 dispatch, gate_up at M = 640 / 768 (336
+    tiles = 1.31 waves) 12 % faster than gemm256; gate_up at 384 / 512 / 1024 / 2048 and qkv at
+    2048 stay on gemm256."""
+    if M < GEMM_MID_MIN_M or N % 256 or not gemm_mid_ok(M, N, K, lda):
+        return False
+    tiles, fill = _g256_fill(M, N)
+    return tiles < GEMM_MID_FILL or fill < 0.7
 
 
 def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
