@@ -171,7 +171,7 @@ class LlamaModel:
         self.custom_ar = None  # parallel.custom_allreduce.CustomAllReduce (set by the engine)
         # TP all-reduces issued from Python: one-shot IPC vs the process group (RCCL / gloo); a call
         # captured into a decode graph counts once, at capture, not per replay
-        self.ar_counts = {"ipc": 0, "group": 0}
+        self.ar_counts = {"ipc": 0, "ipc_fused_norm": 0, "group": 0}
         inv = ref.llama3_inv_freq(cfg.head_dim, cfg.rope_theta, cfg.rope_scaling)
         self.cos_sin = ref.rope_cos_sin(inv, cfg.max_position).to(self.device)
 
@@ -361,6 +361,7 @@ class LlamaModel:
         """RMSNorm(x + residual) -> (normed, new residual); x may be a ``_Partial`` whose TP
         all-reduce runs inside the same launch (``CustomAllReduce.all_reduce_rmsnorm``)."""
         if isinstance(x, _Partial):
+            self.ar_counts["ipc_fused_norm"] += 1
             return self.custom_ar.all_reduce_rmsnorm(x.t, residual, w, self.cfg.eps)
         return ops.rmsnorm(x, w, self.cfg.eps, residual=residual)
 
