@@ -272,8 +272,8 @@ class VectorIndex:
         """Exact top-k without the [q, n] score matrix.  The k-th best score over a strided 1/64
         sample of the rows is a lower bound for the k-th best over all rows.  So the score GEMM
         appends only scores >= that bound (about 16k per query on unstructured data), and an exact
-        top-k runs over those.  Returns None when a candidate list overflowed; the caller then
-        takes the full path."""
+        top-k runs over those.  A chunk whose candidate list overflows is retried or scanned on its
+        own (``_threshold_chunk``)."""
         q = F.normalize(torch.as_tensor(queries).to(self.device, torch.float32), dim=-1).to(self.dtype)
         qg = None if q_groups is None else torch.as_tensor(q_groups, dtype=torch.int32).to(self.device)
         n4 = (self.n + 3) // 4 * 4
@@ -293,14 +293,36 @@ class VectorIndex:
         # at 512 queries asked for ~1 GB of candidate memory per search).
         cap = 2 * k * self.sample_stride + 4096
         per_chunk = max(1, self.CAND_BYTES // (8 * cap))
-        if q.shape[0] > per_chunk:
-            parts = [self._threshold_candidates(q[i:i + per_chunk], thr[i:i + per_chunk], k, cap, n4,
-                                                None if qg is None else qg[i:i + per_chunk])
-                     for i in range(0, q.shape[0], per_chunk)]
-            if any(p is None for p in parts):
-                return None
-            return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
-        return self._threshold_candidates(q, thr, k, cap, n4, qg)
+        parts = [self._threshold_chunk(queries, q, thr, k, cap, n4, qg, i, min(i + per_chunk, q.shape[0]), q_groups)
+                 for i in range(0, q.shape[0], per_chunk)]
+        if len(parts) == 1:
+            return parts[0]
+        return torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+
+    def _threshold_chunk(self, queries, q, thr, k: int, cap: int, n4: int, qg, i: int, j: int, q_groups):
+        """Queries i:j of a threshold search.  A list that overflows its capacity (clustered data:
+        far more rows than k x stride clear the sample's bound) is retried for THIS chunk with the
+        capacity it needed, and past the memory budget this chunk alone takes the full score path
+        -- never the whole batch."""
+        qgs = None if qg is None else qg[i:j]
+        got, cmax = self._threshold_candidates(q[i:j], thr[i:j], k, cap, n4, qgs)
+        if got is None:
+            cap2 = -(-cmax // 1024) * 1024
+            if (j - i) * cap2 * 8 <= 4 * self.CAND_BYTES:
+                self.stats["threshold_retries"] = self.stats.get("threshold_retries", 0) + 1
+                got, _ = self._threshold_candidates(q[i:j], thr[i:j], k, cap2, n4, qgs)
+        if got is None:  # this chunk through [chunk, n] score sub-batches
+            self.stats["threshold_chunk_full"] = self.stats.get("threshold_chunk_full", 0) + 1
+            step = max(1, (1 << 30) // (4 * max(1, self.n)))
+            vs, rs = [], []
+            for a in range(i, j, step):
+                b = min(j, a + step)
+                sc = self.scores(queries[a:b], None if q_groups is None else q_groups[a:b])
+                v, r = ops.topk_rows(sc, min(k, sc.shape[1], 1024))
+                vs.append(v)
+                rs.append(r)
+            got = (torch.cat(vs), torch.cat(rs))
+        return got
 
     CAND_BYTES = 256 << 20  # candidate-list memory of one threshold search
 
@@ -312,14 +334,14 @@ class VectorIndex:
         cmax = int(cnt.max())
         if cmax > cap:
             self.stats["threshold_overflows"] += 1
-            return None
+            return None, cmax
         self.stats["threshold_searches"] += 1
         # only the filled prefix of the lists (the longest one, ~16k of the 36k-entry capacity at
         # k = 250 on unstructured data) is ranked; shorter lists are -inf past their count
         n_use = min(cap, max(k, -(-cmax // 64) * 64))
         vals, pos = ops.topk_rows(cand_val[:, :n_use], min(k, n_use))
         rows = torch.gather(cand_idx, 1, pos.long())
-        return vals, rows.masked_fill(torch.isinf(vals), 0)
+        return (vals, rows.masked_fill(torch.isinf(vals), 0)), cmax
 
     def _sample_rows(self, ns: int) -> torch.Tensor:
         """The strided 1/64 row sample (row-major), cached until the next update."""

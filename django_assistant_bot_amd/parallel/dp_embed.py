@@ -64,7 +64,12 @@ def embed_corpus(engine, text_of: Callable[[int], str], n: int, rank: int = 0, w
         pool.shutdown()
     local = torch.cat(out_vecs) if out_vecs else None
     total = len(ids)
-    if dist.is_initialized():  # (also a world-1 group under DAB_FORCE_GROUP)
+    # the collectives run on the default group only when it IS this split's world of > 1 ranks (or a
+    # world-1 group under DAB_FORCE_GROUP): a caller passing world=1 inside a larger job (its own
+    # split) neither all-reduces with ranks that are not calling nor mis-sizes the gather
+    from .dist import force_group
+
+    if dist.is_initialized() and dist.get_world_size() == world and (world > 1 or force_group()):
         dev = engine.device if dist.get_backend() == "nccl" else torch.device("cpu")
         t = torch.tensor([total], dtype=torch.int64, device=dev)
         dist.all_reduce(t)

@@ -53,6 +53,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from .dist import force_group
 from . import wire
 
 logger = logging.getLogger(__name__)
@@ -459,7 +460,7 @@ class Node:
             mine = _words_texts(offs.numpy(), flat.numpy())
         eng = self.embeds[name]
         v = eng.embed(mine, normalize=norm, out_dtype=torch.float32)
-        if D == 1 and not self.grouped:
+        if D == 1 and not force_group():  # one embedder: its vectors are the answer (no gather)
             return v
         cdev = self._cdev(self.embed_group)
         rows = math.ceil(n / D)

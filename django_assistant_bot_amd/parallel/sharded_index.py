@@ -29,7 +29,13 @@ class ShardedIndex:
 
     def __init__(self, dim: int, device=None, group=None, capacity: int = 4096, dtype=torch.bfloat16):
         self.group = group
-        self.distributed = dist.is_available() and dist.is_initialized()
+        # the collective paths run on a group of > 1 ranks, or on any group under DAB_FORCE_GROUP;
+        # a 1-rank (sub)group in a larger job searches locally (no gloo staging of a
+        # world-1 collective)
+        from .dist import force_group
+
+        grouped = dist.is_available() and dist.is_initialized()
+        self.distributed = grouped and (dist.get_world_size(group) > 1 or force_group())
         self.rank = dist.get_rank(group) if self.distributed else 0
         self.world = dist.get_world_size(group) if self.distributed else 1
         self.local = VectorIndex(dim, device, capacity, dtype)

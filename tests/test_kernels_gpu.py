@@ -921,6 +921,29 @@ def test_index_threshold_search_overflow_falls_back():
     assert torch.allclose(v, torch.ones_like(v), atol=1e-2) and (i >= 0).all()
 
 
+def test_index_threshold_search_on_clustered_rows_retries_per_chunk():
+    """on clustered rows (real embeddings are) far more than k x stride rows clear the
+    sample's bound and a candidate list overflows; only the overflowing chunk is retried with the
+    capacity it needed (no whole-batch fallback to the [q, n] score matrix), and the result is the
+    exact top-k of the full scan."""
+    from django_assistant_bot_amd.engine.vector_index import VectorIndex
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    n, dim, nc = 300_000, 96, 12
+    centers = torch.nn.functional.normalize(torch.randn(nc, dim, device=DEV, generator=g), dim=-1)
+    lab = torch.randint(0, nc, (n,), device=DEV, generator=g)
+    vecs = centers[lab] + 0.02 * torch.randn(n, dim, device=DEV, generator=g)
+    idx = VectorIndex(dim, DEV, capacity=n)
+    idx.add(torch.arange(n).numpy(), vecs)
+    idx.CAND_BYTES = 8 << 20  # small budget: the 200 queries go through in several chunks
+    qs = centers[torch.arange(200, device=DEV) % nc] + 0.01 * torch.randn(200, dim, device=DEV, generator=g)
+    v, i, _ = idx.search(qs, 250)
+    ov = idx.stats["threshold_overflows"]
+    assert ov >= 1 and idx.stats.get("threshold_retries", 0) + idx.stats.get("threshold_chunk_full", 0) == ov
+    ev, _ = ops.topk_rows(idx.scores(qs), 250)
+    assert torch.allclose(v, ev, atol=1e-6), (v - ev).abs().max()
+
+
 def test_cu_masked_stream_runs_kernels():
     """_native.create_cu_masked_stream: a stream restricted to a CU subset (contiguous low CUs
     excluded) runs native kernels and library GEMMs with the same results (profiles/overlap_probe.md)."""
