@@ -222,6 +222,29 @@ def _dump_host_profile(prof):
         f.write(buf.getvalue())
 
 
+class _Heartbeat:
+    """Rank 0 writes '[bench] <phase> <elapsed>' to stderr when a phase starts and every 60 s
+    after, so a long setup (a 70B TP rehearsal builds 8 ranks' shards on one card) is visibly alive;
+    stdout keeps only the one JSON line."""
+
+    def __init__(self, rank: int):
+        import threading
+
+        self.rank, self.t0, self.name = rank, time.perf_counter(), ""
+        if rank == 0:
+            threading.Thread(target=self._beat, daemon=True).start()
+
+    def __call__(self, name: str) -> None:
+        self.name = name
+        if self.rank == 0:
+            print(f"[bench] {name} ({time.perf_counter() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+    def _beat(self):
+        while True:
+            time.sleep(60)
+            print(f"[bench] ... {self.name} ({time.perf_counter() - self.t0:.0f} s)", file=sys.stderr, flush=True)
+
+
 def _apply_config(args, ap) -> None:
     """BASELINE.json config presets.  Config 5 (Llama-3-70B TP=8 + bge-large at a fixed QPS) takes
     its TP degree from --gpus; flags given explicitly on the command line keep their value (a
@@ -313,6 +336,8 @@ def main():
         n_questions = n_steps * B
 
     t_setup = time.perf_counter()
+    phase = _Heartbeat(R)
+    phase("setup: engines")
     embedder = EmbeddingEngine(args.embed_model, dev, seed=args.seed)
     kv_gb = args.kv_gb if (args.kv_gb or not overlap) else 48.0  # two pools in overlap mode
     llm = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
@@ -324,6 +349,7 @@ def main():
         llm2 = LLMEngine(args.llm_model, dev, seed=args.seed + 17 * rep, max_batch=B, max_model_len=4096,
                          use_graphs=not args.no_graphs, kv_cache_gb=kv_gb, max_prefill_tokens=args.prefill_tokens,
                          shared_model=llm.model)
+    phase("setup: index")
     # ---- synthetic corpus: index rows (questions) grouped into documents
     n_rows = args.index_rows
     n_docs = max(1, n_rows // args.rows_per_doc)
@@ -383,6 +409,7 @@ def main():
     if dev.type == "cuda":
         torch.cuda.synchronize(dev)
     setup_s = time.perf_counter() - t_setup
+    phase("warm-up and timed steps")
 
     def sync_start():
         pdist.barrier(info)
