@@ -78,6 +78,9 @@ ARMS = {
     "warm96": {"_warm": 96},
     "warm160": {"_warm": 160},
     "warm96b128": {"_warm": 96, "_warm_blocks": 128},
+    # split-K launches with S % 8 == 0 (o / down at batch 128): K-slices grouped per XCD instead of
+    # tiles, so an XCD's L2 holds 1/8 of X
+    "slicexcd": {"_slice_xcd": 1},
 }
 
 
@@ -106,6 +109,7 @@ def main():
     ap.add_argument("--prompt", type=int, default=1100)
     ap.add_argument("--block-size", type=int, default=64, help="paged-KV block (tokens): one engine per value")
     args = ap.parse_args()
+    from django_assistant_bot_amd import ops
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
 
     torch.manual_seed(0)
@@ -150,6 +154,7 @@ def main():
             eng.model.l3_warm_mb = spec.get("_warm", type(eng.model).l3_warm_mb)
             eng.model.l3_warm_blocks = spec.get("_warm_blocks", type(eng.model).l3_warm_blocks)
             eng.model.STREAM_CFG_RES16 = spec.get("_res_cfg", type(eng.model).STREAM_CFG_RES16)
+            ops.native().stream_gemm_set_slice_xcd(spec.get("_slice_xcd", 0))
             eng._graphs.clear()
             for _ in range(4):
                 eng.step()

@@ -238,6 +238,8 @@ PYBIND11_MODULE(_native, m) {
      py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f);
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
+  m.def("stream_gemm_set_slice_xcd", &dab::stream_gemm_set_slice_xcd);
+  m.def("stream_gemm_slice_xcd", &dab::stream_gemm_slice_xcd);
   m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);
   m.def("slab_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
     check(dab::slab_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "slab_reduce");

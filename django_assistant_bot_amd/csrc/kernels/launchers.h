@@ -111,6 +111,8 @@ int stream_score_candidates_shuf(const void* X, long ldx, const void* W, int M, 
                                  const int* q_group, const float* thr, int* cnt, float* cand_val, int* cand_idx,
                                  int cap, hipStream_t s);
 int stream_gemm_max_m(int cfg);
+void stream_gemm_set_slice_xcd(int on);
+int stream_gemm_slice_xcd();
 int stream_gemm_shuffled(int cfg);  // 1: cfg reads weights in the ops.shuffle_weights layout
 
 // select.hip

@@ -50,6 +50,7 @@ struct StreamParams {
   // separate slab-summing RMSNorm launch disappears (its producer writes h with its residual add).
   int norm;
   float norm_eps;
+  int slice_xcd;  // block -> (tile, slice) with the K-slices (not the tiles) grouped per XCD
   // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
   // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -85,7 +86,7 @@ __device__ __forceinline__ bool static_for(F&& f) {
 }
 
 // ABL (benchmark ablations only): 1 no X staging, 2 no MFMA, 3 weight stream only (no X, no LDS
-// reads, no MFMA); results are garbage, timings bound the parts.
+// reads, no MFMA), 4 no split-K slab stores; results are garbage, timings bound the parts.
 //
 // NWC compute waves (waves NWC.. are the NL X loaders).  BN = 16 RT NWC / KG need not be a power of
 // two: 112 rows (7 waves) tile Llama-3-8B's 28672 gate_up rows onto exactly 256 workgroups, 96 rows
@@ -117,7 +118,10 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   const int bid = blockIdx.x;
   const int xcd = bid % 8, q8 = nwg / 8, r8 = nwg % 8;
   const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
-  const int tile = sid / p.S, slice = sid % p.S;
+  // slice_xcd (S a multiple of 8): the workgroups sharing an XCD share K-slices instead of tiles, so
+  // each XCD's L2 holds S / 8 slices of X rather than all of it
+  const int tile = p.slice_xcd ? bid / p.S : sid / p.S;
+  const int slice = p.slice_xcd ? (bid % 8) * (p.S / 8) + (bid / 8) % (p.S / 8) : sid % p.S;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int n0 = tile * BN;
   const int k_begin = slice * p.kc;
@@ -212,7 +216,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
           if constexpr (ABL != 3) bx[t] = *reinterpret_cast<const bf16x8*>(xb + (16 * t + li) * ROWB + 16 * (lc ^ li));
 #pragma unroll
         for (int a = 0; a < RT; ++a) {
-          if constexpr (ABL >= 2) {
+          if constexpr (ABL == 2 || ABL == 3) {
             asm volatile("" ::"v"(wr[h][a][c]));
             if constexpr (ABL == 2) {
 #pragma unroll
@@ -294,6 +298,7 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     return v;
   };
   if (p.S > 1) {
+    if constexpr (ABL == 4) return;
     float* slab = (float*)p.out + (size_t)slice * p.M * p.N;
     // write-through (sc1) 16-B stores: the slab lines leave this XCD's L2 as they are written
     // instead of sitting dirty until the kernel-end write-back, which the next kernel's start
@@ -427,6 +432,7 @@ static constexpr StreamCfg kStreamCfgs[] = {
     // wave (~134 registers), so one workgroup's pipeline fill / drain overlaps the other's stream
     {8, 1, 1, 2, 3, 2, true, 0, 4},  // 36: BN 64, 4 compute + 2 loader waves, 3-stage weight ring
     {8, 1, 1, 2, 4, 2, true, 0, 4},  // 37: = 36 with a 4-stage weight ring
+    {8, 2, 1, 4, 3, 4, true, 4},     // 38: = 10 without the slab stores (ablation, wrong results)
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
@@ -460,6 +466,14 @@ static void launch_any(int cfg, const StreamParams& p, hipStream_t s, bool nt) {
   }
 }
 
+// block -> (tile, slice) mapping of split-K launches with S % 8 == 0 (A/B; DAB_STREAM_SLICE_XCD)
+static int g_slice_xcd = [] {
+  const char* e = std::getenv("DAB_STREAM_SLICE_XCD");
+  return e ? std::atoi(e) : 0;
+}();
+void stream_gemm_set_slice_xcd(int on) { g_slice_xcd = on; }
+int stream_gemm_slice_xcd() { return g_slice_xcd; }
+
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps) {
   constexpr int KS = 128;
@@ -492,6 +506,7 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   // residual add (its output is not a normalised product)
   p.norm = norm_eps > 0.f;
   p.norm_eps = norm_eps;
+  p.slice_xcd = g_slice_xcd && S % 8 == 0;
   if (p.norm && (residual || K % 8 || M > stream_gemm_max_m(cfg))) return hipErrorInvalidValue;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();

@@ -495,6 +495,25 @@ def test_stream_gemm(cfg, M, N, K, S):
         close(ops.slab_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("cfg,S", [(10, 8), (10, 16), (14, 8), (9, 8)])
+def test_stream_gemm_slice_per_xcd_mapping(cfg, S):
+    """The A/B block mapping that groups K-slices (not tiles) per XCD (``stream_gemm_set_slice_xcd``):
+    every (tile, slice) pair is computed exactly once, so the slabs match the default mapping's."""
+    M, N, K = 128, 4096, 4096
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    ws = ops.shuffle_weights(w)
+    base = ops.stream_gemm(x, ws, splits=S, cfg=cfg, nt=True)
+    nat = ops.native()
+    nat.stream_gemm_set_slice_xcd(1)
+    try:
+        got = ops.stream_gemm(x, ws, splits=S, cfg=cfg, nt=True)
+    finally:
+        nat.stream_gemm_set_slice_xcd(0)
+    torch.cuda.synchronize()
+    assert torch.equal(got, base)
+    close(got.sum(0), ref.gemm_bt(x, w, out_f32=True), atol=1e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize("M", [1, 4, 16])
 @pytest.mark.parametrize("form", ["slabs", "swiglu8", "bf16"])
 def test_stream_gemm_consumer_rmsnorm(form, M):
