@@ -154,13 +154,15 @@ def attn_suite():
     # size; pair-g1 / pair-g4 force G)
     arms = {"base": {"DAB_FLASH_VPIPE": "0"}, "vpipe": {"DAB_FLASH_PAIR": "0"}, "pair": {},
             "pair-g1": {"DAB_FLASH_G": "1"}, "pair-g4": {"DAB_FLASH_G": "4"}, "pair-1bar": {"DAB_FLASH_1BAR": "1"}, "pair-sms": {"DAB_FLASH_SMS": "1"},
+            "pair-sgb": {"DAB_FLASH_SGB": "1"},
             "q64": {"DAB_FLASH_Q64": "1"}, "w8": {"DAB_FLASH_W8": "1"}}
     if os.environ.get("ATTN_ARMS"):  # e.g. ATTN_ARMS=vpipe,pair (a short run for PMC passes)
         arms = {a: arms[a] for a in os.environ["ATTN_ARMS"].split(",")}
 
     def with_env(env, fn):
         old = {k: os.environ.get(k) for k in ("DAB_FLASH_VPIPE", "DAB_FLASH_W8", "DAB_FLASH_PAIR", "DAB_FLASH_G",
-                                           "DAB_FLASH_1BAR", "DAB_FLASH_Q64", "DAB_FLASH_SMS")}
+                                           "DAB_FLASH_1BAR", "DAB_FLASH_Q64", "DAB_FLASH_SMS",
+                                           "DAB_FLASH_SGB")}
         for k in old:
             os.environ.pop(k, None)
         os.environ.update(env)

@@ -413,8 +413,12 @@ __device__ __forceinline__ unsigned lds_addr(const char* p) {
 // work of one slice runs beside the matrix cores instead of all of it before them (the
 // 'sm-split' of cdna_hip_programming.md Appendix B).  The row sum accumulates slice by slice (a
 // different fp32 summation order than the unsplit kernel: equal to within a bf16 rounding).
+//
+// SGB (A/B): the S^T phase's 16 K-fragment LDS reads and 16 MFMAs interleaved by
+// sched_group_barrier (4 reads ahead, then one MFMA per read) instead of hipcc's own order; same
+// instructions and accumulation order (bit-identical).
 template <bool CAUSAL, bool VPIPE = false, int NW = 4, bool STAG = false, bool PAIR = false, bool ONEBAR = false,
-          bool SMS = false>
+          bool SMS = false, bool SGB = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(FlashParams p) {
   static_assert(NW == 4 || NW == 8, "4 or 8 waves");
   static_assert(!STAG || NW == 8, "staggered groups: 8 waves");
@@ -624,6 +628,15 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
         s0 = mfma32(ka[i], qf[4 * half + i], s0);
         s1 = mfma32(kb2[i], qf[4 * half + i], s1);
       }
+    }
+    if constexpr (SGB) {  // masks: MFMA 0x8, DS_READ 0x100
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x8, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
     }
     // ---- online softmax on the raw scores (scale folded into the exponent's FMA): lane (q, hi)
     // holds keys k0 + crow(r, hi) (s0) and + 32 (s1)
@@ -1890,7 +1903,11 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       dim3 gp((npairs + G - 1) / G, Hq, batch);
       const char* ob = std::getenv("DAB_FLASH_1BAR");  // A/B: one barrier per tile
       const char* sm = std::getenv("DAB_FLASH_SMS");   // A/B: softmax split across the PV k-steps
-      if (sm && sm[0] == '1')
+      const char* sg = std::getenv("DAB_FLASH_SGB");   // A/B: sched_group_barrier S^T interleave
+      if (sg && sg[0] == '1')
+        hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, false, false, true>), gp, dim3(256), 0, s,
+                           prm);
+      else if (sm && sm[0] == '1')
         hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, false, true>), gp, dim3(256), 0, s, prm);
       else if (ob && ob[0] == '1')
         hipLaunchKernelGGL((flash_d128_kernel<true, true, 4, false, true, true>), gp, dim3(256), 0, s, prm);

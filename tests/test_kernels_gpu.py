@@ -1072,7 +1072,8 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
 
 @pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2"),
                                      ("DAB_FLASH_PAIR", "0"), ("DAB_FLASH_G", "3"), ("DAB_FLASH_1BAR", "1"),
-                                     ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1"), ("DAB_FLASH_SMS", "1")])
+                                     ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1"), ("DAB_FLASH_SMS", "1"),
+                                     ("DAB_FLASH_SGB", "1")])
 def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
