@@ -106,8 +106,9 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   constexpr int CPW = KW / 32;        // 32-deep MFMA chunks per wave per stage
   constexpr int RED = KG * MP * BNP * 4;
   static_assert(BN <= 256 && BN % 16 == 0, "tile rows");
-  // + per-row sums of squares / scales of the consumer RMSNorm (after the ring / reduction area)
-  constexpr int SMEM = (NB * XBUF > RED ? NB * XBUF : RED) + MP * 4;
+  // + per-row scales of the consumer RMSNorm and each wave's per-row sums of squares (after the ring
+  // / reduction area)
+  constexpr int SMEM = (NB * XBUF > RED ? NB * XBUF : RED) + MP * 4 * (1 + NWC + NL);
   static_assert(CPR >= 16 && CPW >= 1 && KW % 32 == 0, "stage shape");
   static_assert(NB >= 2 && (NB - 2) * GPL <= 63 && GPS % NL == 0, "loader vmcnt range");
   static_assert(NWC % KG == 0, "k groups");
@@ -264,12 +265,11 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
   // ---------------------------------------------------------------- epilogue (all 5 waves)
   constexpr int NT = 64 * (NWC + NL);
   float* rsq = reinterpret_cast<float*>(smem + (NB * XBUF > RED ? NB * XBUF : RED));
-  if (p.norm) {  // (uniform) sums of squares of the X rows, accumulated into LDS by every wave
-    for (int m = tid; m < MP; m += NT) rsq[m] = 0.f;
-  }
+  float* rsq_w = rsq + MP;  // [wave][MP] partial sums of squares
   wait_lgkm0();
   __builtin_amdgcn_s_barrier();
-  if (p.norm) {
+  if (p.norm) {  // (uniform) sums of squares of the X rows: one LDS slot per wave, summed in wave
+                 // order (run-to-run reproducible, no LDS atomics)
     const int vpr = p.K / 8;  // 16-B vectors per row
     for (int m = 0; m < p.M; ++m) {
       const bf16* xr = p.X + (size_t)m * p.ldx;
@@ -281,11 +281,16 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
         for (int j = 0; j < 8; ++j) ss = fmaf(f[j], f[j], ss);
       }
       ss = wave_sum(ss);
-      if (lane == 0) atomicAdd(rsq + m, ss);
+      if (lane == 0) rsq_w[w * MP + m] = ss;
     }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
-    for (int m = tid; m < p.M; m += NT) rsq[m] = rsqrtf(rsq[m] / (float)p.K + p.norm_eps);
+    for (int m = tid; m < p.M; m += NT) {
+      float ss = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWC + NL; ++q) ss += rsq_w[q * MP + m];
+      rsq[m] = rsqrtf(ss / (float)p.K + p.norm_eps);
+    }
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
   }
