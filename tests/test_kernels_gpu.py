@@ -964,7 +964,7 @@ def test_index_threshold_search_on_clustered_rows_retries_per_chunk():
     from django_assistant_bot_amd.engine.vector_index import VectorIndex
 
     g = torch.Generator(device=DEV).manual_seed(3)
-    n, dim = 300_000, 96
+    n, dim = 300_000, 128
     center = torch.nn.functional.normalize(torch.randn(dim, device=DEV, generator=g), dim=0)
     # the rows the 1/64 stride sample sees are scattered; every other row sits in the queries'
     # cluster, so nearly all of them clear the sample's k-th best
