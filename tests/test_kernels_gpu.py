@@ -973,6 +973,7 @@ def test_index_threshold_search_on_clustered_rows_retries_per_chunk():
     idx = VectorIndex(dim, DEV, capacity=n)
     idx.add(torch.arange(n).numpy(), vecs)
     idx.CAND_BYTES = 8 << 20  # small budget: the 200 queries go through in several chunks
+    idx.threshold_min_rows = 1 << 16  # the threshold path at this size (production: from 512k rows)
     qs = center + 0.02 * torch.randn(200, dim, device=DEV, generator=g)
     v, i, _ = idx.search(qs, 250)
     ov = idx.stats["threshold_overflows"]
