@@ -452,7 +452,9 @@ def test_engine_preemption_and_abort_on_gpu_graphs():
     """HIP-graph decode with a KV pool too small for the batch: preempted sequences are recomputed
     (prompt + generated tokens through the prefill path) and continue; an abort frees its blocks;
     every block is free at the end.  Against a pool that never runs dry, greedy tokens agree except
-    after a bf16 near-tie (prefill and decode kernels round differently on the recomputed rows)."""
+    after a bf16 near-tie (prefill and decode kernels round differently on the recomputed rows):
+    where a sequence diverges, its two candidate tokens are within bf16 noise of each other in the
+    model's own logits on the common prefix."""
     from django_assistant_bot_amd.engine.llm_engine import LLMEngine, SamplingParams
 
     shared = list(range(500, 628))
@@ -473,7 +475,7 @@ def test_engine_preemption_and_abort_on_gpu_graphs():
         assert eng.blocks.num_free_blocks() == eng.blocks.num_blocks()
         return eng, outs
 
-    _, ref = run(256)
+    ref_eng, ref = run(256)
     eng, outs = run(14, abort_idx=1)  # up to 6 x 6 blocks needed
     assert eng.stats["preemptions"] > 0 and eng.stats["graph_replays"] > 0
     assert outs[1].finish_reason == "abort"
@@ -482,5 +484,27 @@ def test_engine_preemption_and_abort_on_gpu_graphs():
         if i == 1:
             continue
         assert len(o.token_ids) == 100
-        same += o.token_ids == r.token_ids
-    assert same >= 4, same
+        if o.token_ids == r.token_ids:
+            same += 1
+            continue
+        # the first divergence must be a near-tie of the model's own logits on the common prefix
+        j = next(k for k, (a, b) in enumerate(zip(o.token_ids, r.token_ids)) if a != b)
+        lg = _prefix_logits(ref_eng.model, prompts[i] + r.token_ids[:j])
+        gap = abs(float(lg[o.token_ids[j]] - lg[r.token_ids[j]]))
+        assert gap <= 0.02 * float(lg.abs().max()), (i, j, gap, float(lg.abs().max()))
+    assert same >= 2, same
+
+
+def _prefix_logits(model, seq):
+    """Last-position logits of ``seq`` through one prefill forward of ``model`` (fresh KV cache)."""
+    from django_assistant_bot_amd.models.llama import AttnMeta, KVCache
+
+    cfg, S = model.cfg, len(seq)
+    nb = -(-S // 64)
+    kv = KVCache(cfg.layers, nb, cfg.kv_heads, 64, cfg.head_dim, DEV)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    meta = AttnMeta(decode=False, positions=torch.arange(S, **i32), slots=torch.arange(S, device=DEV),
+                    block_tables=torch.arange(nb, **i32)[None], ctx_lens=torch.tensor([S], **i32),
+                    cu_q=torch.tensor([0, S], **i32), max_q=S)
+    h = model.forward(torch.tensor(seq, **i32), meta, kv)
+    return model.logits(h[-1:].contiguous()).float()[0]
