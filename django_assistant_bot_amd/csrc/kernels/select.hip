@@ -13,6 +13,10 @@
 
 namespace dab {
 
+// float_key(-inf): keys at or below it are -inf logits (masked) or the 0 padding of candidate lists
+constexpr uint32_t kNegInfKey = 0x007FFFFFu;
+
+
 constexpr int SEL_NT = 1024;
 constexpr int SEL_MAXK = 1024;
 
@@ -109,7 +113,10 @@ __device__ int select_topk(KeyAt key_at, int n, int k, SelShared& sh) {
   uint32_t ties;
   const uint32_t kth = radix_kth(key_at, n, k, sh, ties);
   const uint32_t n_gt0 = (uint32_t)k - ties;
-  if (TIES_ALL) ties = (uint32_t)SEL_MAXK - n_gt0;  // capacity for the tied keys
+  // capacity for the tied keys -- unless the k-th value is -inf (a masked row with fewer than k
+  // allowed tokens): those ties carry probability 0, and extending over them would only sort and
+  // walk up to SEL_MAXK dead candidates
+  if (TIES_ALL && kth > kNegInfKey) ties = (uint32_t)SEL_MAXK - n_gt0;
   if (tid == 0) {
     sh.cnt_gt = 0;
     sh.cnt_eq = 0;
@@ -527,7 +534,7 @@ __global__ __launch_bounds__(SEL_NT) void sample_merge_kernel(const uint32_t* __
   }
   // HF TopKLogitsWarper: the candidates tied with the k-th value stay in (exact while no 8192-token
   // chunk holds more than 64 logits >= the k-th value: the chunk stage keeps 64 per chunk)
-  while (k < nc && skey[k] == skey[k - 1] && skey[k] != 0u) ++k;
+  while (k < nc && skey[k] == skey[k - 1] && skey[k] > kNegInfKey) ++k;  // (never over -inf / padding)
   const float P = top_p ? top_p[row] : 1.f;
   const float x0 = key_float(skey[0]) / T;
   float total = 0.f;

@@ -108,3 +108,19 @@ def test_greedy_takes_the_lowest_index_among_tied_maxima():
         cnt = torch.zeros(4, dtype=torch.int64, device=DEV)
         got = ops.sample_tokens(logits, z, k, p, 1, cnt, fast=fast)
         assert got.tolist() == [lo] * 4, (fast, got.tolist(), lo)
+
+
+@pytest.mark.parametrize("path", ["exact", "fast", "tp2"])
+def test_masked_row_with_fewer_allowed_tokens_than_top_k(path):
+    """A constrained-decoding row (mask_logits: -inf outside the allowed set) with 3 allowed tokens
+    and top-k 50: the -inf logits tie at the k-th value, carry probability 0 and are never drawn (nor
+    walked: the tie extension stops at -inf); the draw follows softmax over the 3 allowed logits."""
+    row = torch.full((V,), float("-inf"))
+    allowed = torch.tensor([17, 70_000, 128_000])
+    row[allowed] = torch.tensor([1.0, 0.5, 0.0])
+    row = row.to(torch.bfloat16)
+    want = torch.softmax(row.float()[allowed], 0)
+    tok = _draw(path, row, 1.0, 50, 1.0)
+    assert set(tok.unique().tolist()) <= set(allowed.tolist())
+    freq = torch.stack([(tok == a).double().mean() for a in allowed.tolist()])
+    assert float((freq - want.double()).abs().max()) < 0.01, (freq, want)
