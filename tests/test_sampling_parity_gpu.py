@@ -120,7 +120,7 @@ def test_masked_row_with_fewer_allowed_tokens_than_top_k(path):
     row[allowed] = torch.tensor([1.0, 0.5, 0.0])
     row = row.to(torch.bfloat16)
     want = torch.softmax(row.float()[allowed], 0)
-    tok = _draw(path, row, 1.0, 50, 1.0)
+    tok = _draw(path, row, 1.0, 50, 1.0).cpu()
     assert set(tok.unique().tolist()) <= set(allowed.tolist())
     freq = torch.stack([(tok == a).double().mean() for a in allowed.tolist()])
     assert float((freq - want.double()).abs().max()) < 0.01, (freq, want)
