@@ -86,7 +86,9 @@ __device__ __forceinline__ bool static_for(F&& f) {
 }
 
 // ABL (benchmark ablations only): 1 no X staging, 2 no MFMA, 3 weight stream only (no X, no LDS
-// reads, no MFMA), 4 no split-K slab stores; results are garbage, timings bound the parts.
+// reads, no MFMA), 4 no split-K slab stores, 5 the weight addressing of a tile-interleaved fragment
+// layout (the full kernel on the wrong bytes: what that layout's access pattern would cost); results
+// are garbage, timings bound the parts.
 //
 // NWC compute waves (waves NWC.. are the NL X loaders).  BN = 16 RT NWC / KG need not be a power of
 // two: 112 rows (7 waves) tile Llama-3-8B's 28672 gate_up rows onto exactly 256 workgroups, 96 rows
@@ -156,12 +158,12 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
         return true;
       });
     };
-    const int pre = (ABL & 1) ? 1 : min(NB - 1, nst);
+    const int pre = (ABL == 1 || ABL == 3) ? 1 : min(NB - 1, nst);
     for (int s = 0; s < pre; ++s) issue(s);
     retire(pre - 1);
     __builtin_amdgcn_s_barrier();
     for (int st = 0; st < nst; ++st) {
-      if (ABL & 1) {
+      if (ABL == 1 || ABL == 3) {
         __builtin_amdgcn_s_barrier();
         continue;
       }
@@ -187,9 +189,18 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     // clamped past the slice end: the ring keeps a branch-free load stream, so the compiler's
     // in-order vmcnt count stays exact (the spare loads re-read the last stage from L2)
     auto load_w = [&](int slot, int st, int a, int c) DAB_INLINE {
-      const int soff = min(st, nst - 1) * KS * (SHUF ? 32 : 2) + a * a_stride + w_rowtile0;
-      wr[slot][a][c] = __builtin_bit_cast(
-          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + (SHUF ? 1024 : 64) * c, soff, NT_W ? 2 : 0));
+      if constexpr (ABL == 5) {
+        // the addressing of a tile-interleaved fragment layout (fragment (row block b of the tile,
+        // k chunk) at chunk * BN/16 + b): every wave of the workgroup reads next to the others
+        // (profiles/decode_stream_layout_r6.md)
+        const int chunk = (k_begin + kg * KW) / 32 + min(st, nst - 1) * (KS / 32) + c;
+        const int off = (chunk * (BN / 16) + RT * rg + a) * 1024 + lane * 16;
+        wr[slot][a][c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, off, 0, NT_W ? 2 : 0));
+      } else {
+        const int soff = min(st, nst - 1) * KS * (SHUF ? 32 : 2) + a * a_stride + w_rowtile0;
+        wr[slot][a][c] = __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + (SHUF ? 1024 : 64) * c, soff, NT_W ? 2 : 0));
+      }
     };
     static_for<0, NWIN>([&](auto S_) DAB_INLINE {
       constexpr int s = decltype(S_)::value;
@@ -438,6 +449,8 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {8, 1, 1, 2, 3, 2, true, 0, 4},  // 36: BN 64, 4 compute + 2 loader waves, 3-stage weight ring
     {8, 1, 1, 2, 4, 2, true, 0, 4},  // 37: = 36 with a 4-stage weight ring
     {8, 2, 1, 4, 3, 4, true, 4},     // 38: = 10 without the slab stores (ablation, wrong results)
+    {8, 2, 1, 4, 3, 4, true, 5},     // 39: = 10 reading a tile-interleaved layout (ablation, wrong results)
+    {8, 1, 1, 4, 4, 2, true, 5, 7},  // 40: = 20 reading a tile-interleaved layout (ablation, wrong results)
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 
