@@ -81,6 +81,9 @@ ARMS = {
     # split-K launches with S % 8 == 0 (o / down at batch 128): K-slices grouped per XCD instead of
     # tiles, so an XCD's L2 holds 1/8 of X
     "slicexcd": {"_slice_xcd": 1},
+    # bf16 split-K slabs (LlamaModel.slab_bf16) against fp32
+    "slab16": {"_slab16": True},
+    "slab32": {"_slab16": False},
 }
 
 
@@ -155,6 +158,7 @@ def main():
             eng.model.l3_warm_blocks = spec.get("_warm_blocks", type(eng.model).l3_warm_blocks)
             eng.model.STREAM_CFG_RES16 = spec.get("_res_cfg", type(eng.model).STREAM_CFG_RES16)
             ops.native().stream_gemm_set_slice_xcd(spec.get("_slice_xcd", 0))
+            eng.model.slab_bf16 = spec.get("_slab16", type(eng.model).slab_bf16)
             eng._graphs.clear()
             for _ in range(4):
                 eng.step()

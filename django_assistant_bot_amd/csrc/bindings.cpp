@@ -96,20 +96,23 @@ PYBIND11_MODULE(_native, m) {
     check(dab::silu_mul(VP(out), CVP(x), rows, F, ST(s), interleaved), "silu_mul");
   }, py::arg("out"), py::arg("x"), py::arg("rows"), py::arg("F"), py::arg("s"), py::arg("interleaved") = 0);
   m.def("rope_kv_write", [](u qkv, int ld, u positions, u cos_sin, u q_out, u k_cache, u v_cache, u slots, int T,
-                            int Hq, int Hkv, int D, int block_size, u s, u slabs, int S, long slab_stride) {
+                            int Hq, int Hkv, int D, int block_size, u s, u slabs, int S, long slab_stride,
+                            int slab_bf16) {
     check(dab::rope_kv_write(CVP(qkv), ld, (const int*)positions, CVP(cos_sin), VP(q_out), VP(k_cache), VP(v_cache),
-                             (const int64_t*)slots, T, Hq, Hkv, D, block_size, ST(s), (const float*)slabs, S,
-                             slab_stride),
+                             (const int64_t*)slots, T, Hq, Hkv, D, block_size, ST(s), CVP(slabs), S, slab_stride,
+                             slab_bf16),
           "rope_kv_write");
   }, py::arg("qkv"), py::arg("ld"), py::arg("positions"), py::arg("cos_sin"), py::arg("q_out"), py::arg("k_cache"),
      py::arg("v_cache"), py::arg("slots"), py::arg("T"), py::arg("Hq"), py::arg("Hkv"), py::arg("D"),
-     py::arg("block_size"), py::arg("s"), py::arg("slabs") = 0, py::arg("S") = 0, py::arg("slab_stride") = 0);
+     py::arg("block_size"), py::arg("s"), py::arg("slabs") = 0, py::arg("S") = 0, py::arg("slab_stride") = 0,
+     py::arg("slab_bf16") = 0);
   m.def("rmsnorm_slabs", [](u out, u res_out, u slabs, int S, long slab_stride, u res_in, u w, int rows, int cols,
-                            float eps, u s) {
-    check(dab::rmsnorm_slabs(VP(out), VP(res_out), (const float*)slabs, S, slab_stride, CVP(res_in), CVP(w), rows, cols,
-                             eps, ST(s)),
+                            float eps, u s, int slab_bf16) {
+    check(dab::rmsnorm_slabs(VP(out), VP(res_out), CVP(slabs), S, slab_stride, CVP(res_in), CVP(w), rows, cols, eps,
+                             ST(s), slab_bf16),
           "rmsnorm_slabs");
-  });
+  }, py::arg("out"), py::arg("res_out"), py::arg("slabs"), py::arg("S"), py::arg("slab_stride"), py::arg("res_in"),
+     py::arg("w"), py::arg("rows"), py::arg("cols"), py::arg("eps"), py::arg("s"), py::arg("slab_bf16") = 0);
   m.def("flash_attention",
         [](u q, long qst, long qsh, u k, u v, long kvst, long kvsh, u kc, u vc, u bt, int max_blocks, int bs, u out,
            long ost, long osh, u cu_q, u cu_k, u ctx_k, int batch, int max_sq, int Hq, int Hkv, int D, int causal,
@@ -229,21 +232,22 @@ PYBIND11_MODULE(_native, m) {
      py::arg("q_group"), py::arg("thr"), py::arg("cnt"), py::arg("cand_val"), py::arg("cand_idx"), py::arg("cap"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("stream_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
-                          int S, int epilogue, u s, int nt, int cfg, float norm_eps) {
+                          int S, int epilogue, u s, int nt, int cfg, float norm_eps, int slab_bf16) {
     check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
-                           cfg, norm_eps),
+                           cfg, norm_eps, slab_bf16),
           "stream_gemm");
   }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
      py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
-     py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f);
+     py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f, py::arg("slab_bf16") = 0);
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
   m.def("stream_gemm_set_slice_xcd", &dab::stream_gemm_set_slice_xcd);
   m.def("stream_gemm_slice_xcd", &dab::stream_gemm_slice_xcd);
   m.def("stream_gemm_shuffled", &dab::stream_gemm_shuffled);
-  m.def("slab_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s) {
-    check(dab::slab_reduce(VP(out), ldo, (const float*)slabs, S, M, N, CVP(residual), ldr, ST(s)), "slab_reduce");
-  });
+  m.def("slab_reduce", [](u out, long ldo, u slabs, int S, int M, int N, u residual, long ldr, u s, int slab_bf16) {
+    check(dab::slab_reduce(VP(out), ldo, CVP(slabs), S, M, N, CVP(residual), ldr, ST(s), slab_bf16), "slab_reduce");
+  }, py::arg("out"), py::arg("ldo"), py::arg("slabs"), py::arg("S"), py::arg("M"), py::arg("N"), py::arg("residual"),
+     py::arg("ldr"), py::arg("s"), py::arg("slab_bf16") = 0);
   m.def("sample_tokens", [](u logits, int f32, long ld, int rows, int vocab, u temp, u top_k, u top_p,
                             unsigned long long seed, u counters, u out_tokens, u out_logprobs, u s) {
     check(dab::sample_tokens(CVP(logits), f32, ld, rows, vocab, (const float*)temp, (const int*)top_k,

@@ -175,54 +175,74 @@ __device__ __forceinline__ void rope_rot(float& x1, float& x2, const float2 cs) 
   x2 = o2;
 }
 
+// 8 consecutive elements of one split-K slab, loaded raw (fp32: two 16-B loads; bf16: one) so every
+// load of a round can be issued before the first add, then added in fp32 to an accumulator.
+template <typename ST>
+struct SlabVec8;
+template <>
+struct SlabVec8<float> {
+  f32x4 a, b;
+  __device__ __forceinline__ void load(const float* p) {
+    a = *reinterpret_cast<const f32x4*>(p);
+    b = *reinterpret_cast<const f32x4*>(p + 4);
+  }
+  __device__ __forceinline__ void add_to(float (&v)[8]) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] += a[j];
+      v[4 + j] += b[j];
+    }
+  }
+};
+template <>
+struct SlabVec8<bf16> {
+  u32x4 r;
+  __device__ __forceinline__ void load(const bf16* p) { r = *reinterpret_cast<const u32x4*>(p); }
+  __device__ __forceinline__ void add_to(float (&v)[8]) const {
+    float f[8];
+    unpack8(r, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += f[j];
+  }
+};
+
 // One 8-dim chunk pair (dims i0..i0+7 and i0+D/2..) of head `h` of token `t` of a QKV projection,
 // with rotate-half RoPE applied when `rotate`: the shared body of rope_kv_kernel and of the fused
 // decode-attention prologue (bitwise the same result in both).  The projection is either bf16 rows
-// (`qkv`, row stride `ld`) or S fp32 split-K slabs (`slabs`, row stride `ld`, slab stride
+// (`qkv`, row stride `ld`) or S fp32 / bf16 split-K slabs (`slabs`, row stride `ld`, slab stride
 // `slab_stride`) summed in slab order and rounded like a bf16 GEMM output.  `cs` holds the 8
 // (cos, sin) pairs of the token's position for dims i0..i0+7.  U slabs' loads are in flight per
 // round (the per-element add order is slab order for any U).
-template <int U = 4>
-__device__ __forceinline__ void rope_chunk(const bf16* __restrict__ qkv, const float* __restrict__ slabs, int S,
+template <int U = 4, typename ST = float>
+__device__ __forceinline__ void rope_chunk(const bf16* __restrict__ qkv, const ST* __restrict__ slabs, int S,
                                            long slab_stride, int ld, int t, int h, int D, int i0,
                                            const float2 (&cs)[8], bool rotate, float (&x1)[8], float (&x2)[8]) {
   const int half = D >> 1;
   if (slabs) {
-    const float* src = slabs + (size_t)t * ld + (size_t)h * D;
+    const ST* src = slabs + (size_t)t * ld + (size_t)h * D;
 #pragma unroll
     for (int j = 0; j < 8; ++j) x1[j] = x2[j] = 0.f;
     int sl = 0;
     for (; sl + U <= S; sl += U, src += U * slab_stride) {
-      f32x4 a0[U], a1[U], b0[U], b1[U];
+      SlabVec8<ST> a[U], b[U];
 #pragma unroll
       for (int q = 0; q < U; ++q) {
-        const float* sq = src + q * slab_stride;
-        a0[q] = *reinterpret_cast<const f32x4*>(sq + i0);
-        a1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + 4);
-        b0[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half);
-        b1[q] = *reinterpret_cast<const f32x4*>(sq + i0 + half + 4);
+        const ST* sq = src + q * slab_stride;
+        a[q].load(sq + i0);
+        b[q].load(sq + i0 + half);
       }
 #pragma unroll
-      for (int q = 0; q < U; ++q)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x1[j] += a0[q][j];
-          x1[4 + j] += a1[q][j];
-          x2[j] += b0[q][j];
-          x2[4 + j] += b1[q][j];
-        }
+      for (int q = 0; q < U; ++q) {
+        a[q].add_to(x1);
+        b[q].add_to(x2);
+      }
     }
     for (; sl < S; ++sl, src += slab_stride) {
-      const f32x4 a0 = *reinterpret_cast<const f32x4*>(src + i0), a1 = *reinterpret_cast<const f32x4*>(src + i0 + 4);
-      const f32x4 b0 = *reinterpret_cast<const f32x4*>(src + i0 + half);
-      const f32x4 b1 = *reinterpret_cast<const f32x4*>(src + i0 + half + 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        x1[j] += a0[j];
-        x1[4 + j] += a1[j];
-        x2[j] += b0[j];
-        x2[4 + j] += b1[j];
-      }
+      SlabVec8<ST> a, b;
+      a.load(src + i0);
+      b.load(src + i0 + half);
+      a.add_to(x1);
+      b.add_to(x2);
     }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {

@@ -54,12 +54,13 @@ __global__ __launch_bounds__(256) void silu_mul_kernel(bf16* __restrict__ out, c
 // k heads are rotated and written to the paged cache, v heads copied to the paged cache.
 // cos_sin: [max_pos, D/2] float2 (cos, sin); slots[t] = block * block_size + offset (or < 0: skip).
 // Cache layout: [num_blocks, Hkv, block_size, D].
+template <typename ST>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv, int ld,
                                                       const int* __restrict__ positions,
                                                       const float2* __restrict__ cos_sin, bf16* __restrict__ q_out,
                                                       bf16* __restrict__ k_cache, bf16* __restrict__ v_cache,
                                                       const int64_t* __restrict__ slots, int T, int Hq, int Hkv, int D,
-                                                      int block_size, const float* __restrict__ slabs, int S,
+                                                      int block_size, const ST* __restrict__ slabs, int S,
                                                       long slab_stride) {
   const int per_head = D >> 4;  // threads per head
   const int heads = Hq + 2 * Hkv;
@@ -122,13 +123,19 @@ int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s, int in
 
 int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos_sin, void* q_out, void* k_cache,
                   void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s,
-                  const float* slabs, int S, long slab_stride) {
+                  const void* slabs, int S, long slab_stride, int slab_bf16) {
   if (T <= 0) return 0;
-  if (D % 16 || ld % 8 || (slabs && (S < 1 || slab_stride % 4))) return hipErrorInvalidValue;
+  if (D % 16 || ld % 8 || (slabs && (S < 1 || slab_stride % 8))) return hipErrorInvalidValue;
   const size_t total = (size_t)T * (q_out ? Hq + 2 * Hkv : 2 * Hkv) * (D / 16);
-  hipLaunchKernelGGL(rope_kv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, (const bf16*)qkv, ld,
-                     positions, (const float2*)cos_sin, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, slots, T, Hq,
-                     Hkv, D, block_size, slabs, S, slab_stride);
+  const dim3 grid((unsigned)((total + 255) / 256));
+  if (slabs && slab_bf16)
+    hipLaunchKernelGGL(rope_kv_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)qkv, ld, positions,
+                       (const float2*)cos_sin, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, slots, T, Hq, Hkv, D,
+                       block_size, (const bf16*)slabs, S, slab_stride);
+  else
+    hipLaunchKernelGGL(rope_kv_kernel<float>, grid, dim3(256), 0, s, (const bf16*)qkv, ld, positions,
+                       (const float2*)cos_sin, (bf16*)q_out, (bf16*)k_cache, (bf16*)v_cache, slots, T, Hq, Hkv, D,
+                       block_size, (const float*)slabs, S, slab_stride);
   return hipGetLastError();
 }
 

@@ -24,8 +24,8 @@ struct L3Warm {
 // norm.hip
 int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const void* w, int rows, int cols, float eps,
             hipStream_t s);
-int rmsnorm_slabs(void* out, void* res_out, const float* slabs, int S, long slab_stride, const void* res_in,
-                  const void* w, int rows, int cols, float eps, hipStream_t s);
+int rmsnorm_slabs(void* out, void* res_out, const void* slabs, int S, long slab_stride, const void* res_in,
+                  const void* w, int rows, int cols, float eps, hipStream_t s, int slab_bf16 = 0);
 int layernorm(void* out, const void* x, const void* res_in, const void* gamma, const void* beta, int rows, int cols,
               float eps, hipStream_t s);
 int bert_embed(void* out, const int* ids, const int* pos_ids, const int* type_ids, const void* word, const void* pos,
@@ -39,7 +39,7 @@ int gelu(void* out, const void* x, const void* bias, size_t rows, int cols, hipS
 int silu_mul(void* out, const void* x, size_t rows, int F, hipStream_t s, int interleaved = 0);
 int rope_kv_write(const void* qkv, int ld, const int* positions, const void* cos_sin, void* q_out, void* k_cache,
                   void* v_cache, const int64_t* slots, int T, int Hq, int Hkv, int D, int block_size, hipStream_t s,
-                  const float* slabs = nullptr, int S = 0, long slab_stride = 0);
+                  const void* slabs = nullptr, int S = 0, long slab_stride = 0, int slab_bf16 = 0);
 
 // attention.hip
 int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const void* k, const void* v,
@@ -90,11 +90,12 @@ int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const vo
 // stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
-                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps = 0.f);
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps = 0.f,
+                int slab_bf16 = 0);
 int stream_gemm_bn(int cfg);
-// fp32 split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
-int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
-                hipStream_t s);
+// fp32 (or bf16: slab_bf16) split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
+int slab_reduce(void* out, long ldo, const void* slabs, int S, int M, int N, const void* residual, long ldr,
+                hipStream_t s, int slab_bf16 = 0);
 // index_scan.hip: persistent scan for 1..64 queries at K <= 1024, 65..96 at K <= 768 (queries staged in
 // LDS once), K % 256 == 0
 int index_scan_candidates(const void* X, long ldx, const void* W, long ldw, int M, int N, int K, const int* row_group,

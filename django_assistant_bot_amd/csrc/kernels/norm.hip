@@ -62,9 +62,9 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(bf16* __restrict__ out, bf1
 // residual, gain and the slab chunks of KG vectors at once -- is issued before the first add, so the
 // kernel waits out one memory round trip instead of one per slab group plus one for the gain after
 // the row reduction.  Out-of-range vectors load a clamped (valid) address and are masked.
-template <int NT, int VPT>
+template <int NT, int VPT, typename ST = float>
 __global__ __launch_bounds__(NT) void rmsnorm_slab_kernel(bf16* __restrict__ out, bf16* __restrict__ res_out,
-                                                          const float* __restrict__ slabs, int S, long slab_stride,
+                                                          const ST* __restrict__ slabs, int S, long slab_stride,
                                                           const bf16* __restrict__ res_in, const bf16* __restrict__ w,
                                                           int cols, float eps) {
   constexpr int KG = VPT < 2 ? VPT : 2;  // vectors whose slab loads are in flight together
@@ -89,67 +89,40 @@ __global__ __launch_bounds__(NT) void rmsnorm_slab_kernel(bf16* __restrict__ out
   for (int k = 0; k < VPT; ++k)
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
-  const float* base = slabs + row * cols;
+  const ST* base = slabs + row * cols;
 #pragma unroll
   for (int k0 = 0; k0 < VPT; k0 += KG) {
     int sl = 0;
     for (; sl + 8 <= S; sl += 8) {
-      f32x4 a[KG][8], b[KG][8];
+      SlabVec8<ST> a[KG][8];
 #pragma unroll
       for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float* src = base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8;
-          a[kk][q] = *reinterpret_cast<const f32x4*>(src);
-          b[kk][q] = *reinterpret_cast<const f32x4*>(src + 4);
-        }
+        for (int q = 0; q < 8; ++q) a[kk][q].load(base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8);
       __builtin_amdgcn_sched_barrier(0);  // keep every load of the round ahead of the adds
 #pragma unroll
       for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[k0 + kk][j] += a[kk][q][j];
-            v[k0 + kk][4 + j] += b[kk][q][j];
-          }
+        for (int q = 0; q < 8; ++q) a[kk][q].add_to(v[k0 + kk]);
     }
     for (; sl + 4 <= S; sl += 4) {
-      f32x4 a[KG][4], b[KG][4];
+      SlabVec8<ST> a[KG][4];
 #pragma unroll
       for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float* src = base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8;
-          a[kk][q] = *reinterpret_cast<const f32x4*>(src);
-          b[kk][q] = *reinterpret_cast<const f32x4*>(src + 4);
-        }
+        for (int q = 0; q < 4; ++q) a[kk][q].load(base + (size_t)(sl + q) * slab_stride + (size_t)iv[k0 + kk] * 8);
       __builtin_amdgcn_sched_barrier(0);  // keep every load of the round ahead of the adds
 #pragma unroll
       for (int kk = 0; kk < KG; ++kk)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            v[k0 + kk][j] += a[kk][q][j];
-            v[k0 + kk][4 + j] += b[kk][q][j];
-          }
+        for (int q = 0; q < 4; ++q) a[kk][q].add_to(v[k0 + kk]);
     }
     for (; sl < S; ++sl) {
-      f32x4 a[KG], b[KG];
+      SlabVec8<ST> a[KG];
 #pragma unroll
-      for (int kk = 0; kk < KG; ++kk) {
-        const float* src = base + (size_t)sl * slab_stride + (size_t)iv[k0 + kk] * 8;
-        a[kk] = *reinterpret_cast<const f32x4*>(src);
-        b[kk] = *reinterpret_cast<const f32x4*>(src + 4);
-      }
+      for (int kk = 0; kk < KG; ++kk) a[kk].load(base + (size_t)sl * slab_stride + (size_t)iv[k0 + kk] * 8);
 #pragma unroll
-      for (int kk = 0; kk < KG; ++kk)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[k0 + kk][j] += a[kk][j];
-          v[k0 + kk][4 + j] += b[kk][j];
-        }
+      for (int kk = 0; kk < KG; ++kk) a[kk].add_to(v[k0 + kk]);
     }
   }
   float ss = 0.f;
@@ -481,20 +454,47 @@ int rmsnorm(void* out, void* res_out, const void* x, const void* res_in, const v
   return hipGetLastError();
 }
 
-int rmsnorm_slabs(void* out, void* res_out, const float* slabs, int S, long slab_stride, const void* res_in,
-                  const void* w, int rows, int cols, float eps, hipStream_t s) {
-  if (rows <= 0) return 0;
-  if (cols % 8 || cols > 16384 || S < 1 || slab_stride % 4) return hipErrorInvalidValue;
+// DAB_ROW_DISPATCH for a kernel templated <NT, VPT, T>
+#define DAB_ROW_DISPATCH_T(KERNEL, T, ROWS, COLS, STREAM, ...)                                   \
+  do {                                                                                          \
+    const int nvec_ = (COLS) / 8;                                                               \
+    if (nvec_ <= 64)                                                                            \
+      hipLaunchKernelGGL((KERNEL<64, 1, T>), dim3(ROWS), dim3(64), 0, STREAM, __VA_ARGS__);     \
+    else if (nvec_ <= 128)                                                                      \
+      hipLaunchKernelGGL((KERNEL<128, 1, T>), dim3(ROWS), dim3(128), 0, STREAM, __VA_ARGS__);   \
+    else if (nvec_ <= 256)                                                                      \
+      hipLaunchKernelGGL((KERNEL<256, 1, T>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);   \
+    else if (nvec_ <= 512)                                                                      \
+      hipLaunchKernelGGL((KERNEL<256, 2, T>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);   \
+    else if (nvec_ <= 1024)                                                                     \
+      hipLaunchKernelGGL((KERNEL<256, 4, T>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);   \
+    else                                                                                        \
+      hipLaunchKernelGGL((KERNEL<256, 8, T>), dim3(ROWS), dim3(256), 0, STREAM, __VA_ARGS__);   \
+  } while (0)
+
+template <typename ST>
+static int rmsnorm_slabs_t(void* out, void* res_out, const ST* slabs, int S, long slab_stride, const void* res_in,
+                           const void* w, int rows, int cols, float eps, hipStream_t s) {
   // 4096-wide rows (Llama-3-8B decode, 8 slabs): 512 threads x 1 vector instead of 256 x 2 -- twice
   // the waves issuing the slab loads: 4.97 vs 5.52 us per call at 128 rows (benchmarks/slab_norm_bench.py)
   if (cols / 8 > 256 && cols / 8 <= 512) {
-    hipLaunchKernelGGL((rmsnorm_slab_kernel<512, 1>), dim3(rows), dim3(512), 0, s, (bf16*)out, (bf16*)res_out, slabs,
-                       S, slab_stride, (const bf16*)res_in, (const bf16*)w, cols, eps);
+    hipLaunchKernelGGL((rmsnorm_slab_kernel<512, 1, ST>), dim3(rows), dim3(512), 0, s, (bf16*)out, (bf16*)res_out,
+                       slabs, S, slab_stride, (const bf16*)res_in, (const bf16*)w, cols, eps);
     return hipGetLastError();
   }
-  DAB_ROW_DISPATCH(rmsnorm_slab_kernel, rows, cols, s, (bf16*)out, (bf16*)res_out, slabs, S, slab_stride,
-                   (const bf16*)res_in, (const bf16*)w, cols, eps);
+  DAB_ROW_DISPATCH_T(rmsnorm_slab_kernel, ST, rows, cols, s, (bf16*)out, (bf16*)res_out, slabs, S, slab_stride,
+                     (const bf16*)res_in, (const bf16*)w, cols, eps);
   return hipGetLastError();
+}
+
+// slab_bf16: bf16 slabs (stream_gemm(..., slab_bf16)), else fp32
+int rmsnorm_slabs(void* out, void* res_out, const void* slabs, int S, long slab_stride, const void* res_in,
+                  const void* w, int rows, int cols, float eps, hipStream_t s, int slab_bf16) {
+  if (rows <= 0) return 0;
+  if (cols % 8 || cols > 16384 || S < 1 || slab_stride % 8) return hipErrorInvalidValue;
+  if (slab_bf16)
+    return rmsnorm_slabs_t(out, res_out, (const bf16*)slabs, S, slab_stride, res_in, w, rows, cols, eps, s);
+  return rmsnorm_slabs_t(out, res_out, (const float*)slabs, S, slab_stride, res_in, w, rows, cols, eps, s);
 }
 
 int layernorm(void* out, const void* x, const void* res_in, const void* gamma, const void* beta, int rows, int cols,

@@ -51,6 +51,7 @@ struct StreamParams {
   int norm;
   float norm_eps;
   int slice_xcd;  // block -> (tile, slice) with the K-slices (not the tiles) grouped per XCD
+  int slab_bf16;  // S > 1: bf16 K-slice slabs instead of fp32
   // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
   // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -321,6 +322,21 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     // would wait for (MI355X_MICROARCH.md price list: +2.8-3.8 us behind 12.6-16.8 MB of fp32
     // partials; o 14.6 -> 13.2 us, qkv 18.0 -> 16.6 us in the decode layer, profiles/decode_round2.md);
     // the consumer reads them once from the Infinity Cache either way
+    if (p.slab_bf16) {
+      // bf16 slabs (the partial sums rounded to bf16, as the TP path hands them to the all-reduce):
+      // half the bytes for the producer's stores and the consumer's reads
+      bf16* bslab = (bf16*)p.out + (size_t)slice * p.M * p.N;
+      const auto brd = __builtin_amdgcn_make_buffer_rsrc(bslab + n0, 0, (p.M - 1) * p.N * 2 + BN * 2, 0x00020000);
+      for (int e = tid; e < MP * (BN / 8); e += NT) {
+        const int m = e / (BN / 8), c8 = (e % (BN / 8)) * 8;
+        if (m < p.M) {
+          const f32x4 lo = tile4(m, c8), hi = tile4(m, c8 + 4);
+          float o[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          __builtin_amdgcn_raw_buffer_store_b128(pack8(o), brd, (m * p.N + c8) * 2, 0, 16);
+        }
+      }
+      return;
+    }
     const auto srd = __builtin_amdgcn_make_buffer_rsrc(slab + n0, 0, (p.M - 1) * p.N * 4 + BN * 4, 0x00020000);
     for (int e = tid; e < MP * (BN / 4); e += NT) {
       const int m = e / (BN / 4), c4 = (e % (BN / 4)) * 4;
@@ -493,7 +509,8 @@ void stream_gemm_set_slice_xcd(int on) { g_slice_xcd = on; }
 int stream_gemm_slice_xcd() { return g_slice_xcd; }
 
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
-                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps) {
+                int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps,
+                int slab_bf16) {
   constexpr int KS = 128;
   if (M <= 0 || N <= 0) return 0;
   const int bn = stream_gemm_bn(cfg);
@@ -525,14 +542,16 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   p.norm = norm_eps > 0.f;
   p.norm_eps = norm_eps;
   p.slice_xcd = g_slice_xcd && S % 8 == 0;
+  p.slab_bf16 = S > 1 && slab_bf16;
   if (p.norm && (residual || K % 8 || M > stream_gemm_max_m(cfg))) return hipErrorInvalidValue;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();
 }
 
-// Sum S fp32 slabs -> bf16 (optionally + residual), rounded like a bf16 GEMM output before the add:
-// the TP path hands bf16 partial sums to the all-reduce.
-__global__ __launch_bounds__(256) void slab_reduce_kernel(bf16* out, long ldo, const float* slabs, int S, int M, int N,
+// Sum S fp32 / bf16 slabs -> bf16 (optionally + residual), rounded like a bf16 GEMM output before the
+// add: the TP path hands bf16 partial sums to the all-reduce.
+template <typename ST>
+__global__ __launch_bounds__(256) void slab_reduce_kernel(bf16* out, long ldo, const ST* slabs, int S, int M, int N,
                                                           const bf16* residual, long ldr) {
   const size_t e = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8;
   const size_t total = (size_t)M * N;
@@ -540,13 +559,9 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(bf16* out, long ldo, c
   const int m = (int)(e / N), n = (int)(e % N);
   float o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int s = 0; s < S; ++s) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(slabs + (size_t)s * total + e);
-    const f32x4 a = src[0], b = src[1];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[j] += a[j];
-      o[4 + j] += b[j];
-    }
+    SlabVec8<ST> v;
+    v.load(slabs + (size_t)s * total + e);
+    v.add_to(o);
   }
   if (residual) {
     float r[8];
@@ -557,13 +572,18 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(bf16* out, long ldo, c
   *reinterpret_cast<u32x4*>(out + (size_t)m * ldo + n) = pack8(o);
 }
 
-int slab_reduce(void* out, long ldo, const float* slabs, int S, int M, int N, const void* residual, long ldr,
-                hipStream_t s) {
+int slab_reduce(void* out, long ldo, const void* slabs, int S, int M, int N, const void* residual, long ldr,
+                hipStream_t s, int slab_bf16) {
   if (M <= 0 || N <= 0) return 0;
   if (N % 8 || ldo % 8 || (residual && ldr % 8)) return hipErrorInvalidValue;
   const size_t total8 = (size_t)M * N / 8;
-  hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)((total8 + 255) / 256)), dim3(256), 0, s, (bf16*)out, ldo,
-                     slabs, S, M, N, (const bf16*)residual, ldr);
+  const dim3 grid((unsigned)((total8 + 255) / 256));
+  if (slab_bf16)
+    hipLaunchKernelGGL(slab_reduce_kernel<bf16>, grid, dim3(256), 0, s, (bf16*)out, ldo, (const bf16*)slabs, S, M, N,
+                       (const bf16*)residual, ldr);
+  else
+    hipLaunchKernelGGL(slab_reduce_kernel<float>, grid, dim3(256), 0, s, (bf16*)out, ldo, (const float*)slabs, S, M,
+                       N, (const bf16*)residual, ldr);
   return hipGetLastError();
 }
 

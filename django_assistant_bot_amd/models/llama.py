@@ -269,6 +269,13 @@ class LlamaModel:
             return -1, 1
         return cfg, self._stream_splits(N, K, ops.native().stream_gemm_bn(cfg))
 
+    # Split-K slabs of the decode projections as bf16 (the partial sums rounded once, as the TP path
+    # hands them to its all-reduce) instead of fp32: half the bytes the producer writes and the
+    # RMSNorm / RoPE consumers read; batch-128 decode step 7.503 -> 7.351 ms (benchmarks/decode_ab.py
+    # slab32,slab16; profiles/decode_slab_r6.md).  TP keeps fp32: its fused all-reduce + norm sums
+    # fp32 slabs.
+    slab_bf16 = True
+
     def _proj(self, x, w, dec: bool, allow_slabs: bool = True, name: str = "", epilogue=ops.EPI_NONE):
         """One projection.  Decode-sized batches (``dec``) stream the fragment-layout weights
         through stream_gemm, as fp32 split-K slabs when a consumer sums them (RMSNorm, the decode
@@ -284,7 +291,8 @@ class LlamaModel:
             if cfg >= 0:
                 if epilogue != ops.EPI_NONE:
                     return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg)
-                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True)
+                sd = torch.bfloat16 if (self.slab_bf16 and self.tp_size == 1) else torch.float32
+                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True, slab_dtype=sd)
                 return ops.slab_reduce(out) if (s > 1 and not allow_slabs) else out
         return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag)
 

@@ -31,12 +31,13 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     """RMSNorm over the last dim; with ``residual`` the input is ``x + residual`` and the sum is
     also returned (fused residual stream).  Returns (out, residual_out).
 
-    ``x`` may also be fp32 split-K slabs [S, rows, cols] of the producing projection
-    (``stream_gemm(..., splits=S)``): they are summed (and rounded to bf16) inside the kernel."""
-    slabs = x.dtype == torch.float32 and x.dim() == 3
+    ``x`` may also be split-K slabs [S, rows, cols] (fp32, or bf16: ``slab_dtype``) of the producing
+    projection (``stream_gemm(..., splits=S)``): they are summed in fp32 (and rounded to bf16) inside
+    the kernel."""
+    slabs = x.dim() == 3 and x.dtype in (torch.float32, torch.bfloat16)
     if not x.is_cuda:
         if slabs:
-            x = x.sum(0).to(torch.bfloat16)
+            x = x.float().sum(0).to(torch.bfloat16)
         return ref.rmsnorm(x, w, eps, residual)
     expect_bf16_contig(w, residual)
     same_device(x, w, residual)
@@ -55,7 +56,7 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, residual: torch.Tensor
     res_out = torch.empty(shape, dtype=torch.bfloat16, device=x.device) if residual is not None else None
     if slabs:
         native().rmsnorm_slabs(ptr(out), ptr(res_out), ptr(x), S, rows * cols, ptr(residual), ptr(w), rows, cols,
-                               float(eps), stream(x))
+                               float(eps), stream(x), int(x.dtype == torch.bfloat16))
     else:
         native().rmsnorm(ptr(out), ptr(res_out), ptr(x), ptr(residual), ptr(w), rows, cols, float(eps), stream(x))
     return out, res_out
@@ -155,14 +156,14 @@ def silu_mul(x, interleaved=False, group: int | None = None):
 def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, write_q=True):
     """Applies RoPE to the q/k heads of ``qkv`` [T, (Hq+2Hkv)*D]; writes k, v into the paged caches
     [num_blocks, Hkv, block_size, D] at ``slots`` (int64, <0 skipped); returns q [T, Hq, D].
-    ``qkv`` may also be fp32 split-K slabs [S, T, (Hq+2Hkv)*D], summed inside the kernel.
+    ``qkv`` may also be split-K slabs [S, T, (Hq+2Hkv)*D] (fp32 or bf16), summed inside the kernel.
     ``write_q=False`` (bf16 ``qkv``): k / v only, returns None (the prefill attention rotates q on
     load: ``flash_attention_paged(..., rope=...)``)."""
     block_size = k_cache.shape[2]
-    slabs = qkv.dtype == torch.float32 and qkv.dim() == 3
+    slabs = qkv.dim() == 3 and qkv.dtype in (torch.float32, torch.bfloat16)
     if not qkv.is_cuda:
         if slabs:
-            qkv = qkv.sum(0).to(torch.bfloat16)
+            qkv = qkv.float().sum(0).to(torch.bfloat16)
         return ref.rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, block_size)
     expect_bf16_contig(k_cache, v_cache)
     _i32(positions)
@@ -184,7 +185,7 @@ def rope_kv_write(qkv, positions, cos_sin, k_cache, v_cache, slots, Hq, Hkv, D, 
         expect(qkv.is_contiguous(), "slabs must be contiguous")
         native().rope_kv_write(0, qkv.shape[-1], ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache), ptr(v_cache),
                                ptr(slots), T, Hq, Hkv, D, block_size, stream(qkv), ptr(qkv), qkv.shape[0],
-                               T * qkv.shape[-1])
+                               T * qkv.shape[-1], int(qkv.dtype == torch.bfloat16))
     else:
         expect_bf16_contig(qkv)
         native().rope_kv_write(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(q), ptr(k_cache),
@@ -621,7 +622,8 @@ def unshuffle_weights(w: torch.Tensor) -> torch.Tensor:
 
 
 
-def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0, norm_eps: float = 0.0):
+def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0, norm_eps: float = 0.0,
+                slab_dtype=torch.float32):
     """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): bf16
     [M, N] (optional residual add), SwiGLU [M, N/2] over 16- / 8-row interleaved [gate | up] rows, or
     fp32 K-slice slabs [S, M, N] (their sum is the product; consumers sum them in their prologue or
@@ -629,9 +631,12 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
     (``native().stream_gemm_bn(cfg)`` weight rows per workgroup); ``nt`` streams the weights with
     non-temporal loads.  ``norm_eps`` > 0: x is an un-normalised residual stream and w carries the
     RMSNorm gains in its columns; the kernel scales row m by rsqrt(mean(x[m]^2) + eps) (the
-    consumer-side RMSNorm of small decode batches).  On the CPU ``w`` is row-major."""
+    consumer-side RMSNorm of small decode batches).  ``slab_dtype`` bf16: the split-K slabs are the
+    partial sums rounded to bf16 (half the bytes for the producer and its consumer; the rounding the TP
+    path's all-reduce input has).  On the CPU ``w`` is row-major."""
     if not x.is_cuda:
-        return _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual, norm_eps=norm_eps)
+        y = _ref_stream_gemm(x, w, splits=splits, epilogue=epilogue, residual=residual, norm_eps=norm_eps)
+        return y.to(slab_dtype) if splits > 1 else y
     expect(norm_eps <= 0 or residual is None, "the consumer RMSNorm takes no residual add")
     expect(x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16, "bf16 operands required")
     expect(x.stride(-1) == 1 and w.stride(-1) == 1, "operands must be K-contiguous")
@@ -646,9 +651,10 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
         expect(w.is_contiguous(), "shuffled-layout configurations take a contiguous shuffle_weights() tensor")
     if splits > 1:
         expect(epilogue == EPI_NONE and residual is None, "split-K writes raw slabs")
+        expect(slab_dtype in (torch.float32, torch.bfloat16), "slabs are fp32 or bf16")
         if out is None:
-            out = torch.empty((splits, M, N), dtype=torch.float32, device=x.device)
-        expect(out.dtype == torch.float32 and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
+            out = torch.empty((splits, M, N), dtype=slab_dtype, device=x.device)
+        expect(out.dtype == slab_dtype and out.is_contiguous() and tuple(out.shape) == (splits, M, N), "bad slabs")
         ldo = N
     else:
         n_out = N // 2 if epilogue in (EPI_SWIGLU, EPI_SWIGLU8) else N
@@ -663,24 +669,25 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
         ldo = out.stride(0)
     native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
                          residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
-                         int(bool(nt)), int(cfg), float(norm_eps))
+                         int(bool(nt)), int(cfg), float(norm_eps), int(splits > 1 and out.dtype == torch.bfloat16))
     return out
 
 
 def slab_reduce(slabs, residual=None, out=None):
-    """fp32 slabs [S, M, N] -> bf16 [M, N] (sum rounded to bf16, then + residual)."""
+    """fp32 / bf16 slabs [S, M, N] -> bf16 [M, N] (fp32 sum rounded to bf16, then + residual)."""
     if not slabs.is_cuda:
-        y = slabs.sum(0).to(torch.bfloat16)
+        y = slabs.float().sum(0).to(torch.bfloat16)
         return y if residual is None else (y.float() + residual.float()).to(torch.bfloat16)
     S, M, N = slabs.shape
-    expect(slabs.dtype == torch.float32 and slabs.is_contiguous() and N % 8 == 0, "bad slabs")
+    expect(slabs.dtype in (torch.float32, torch.bfloat16) and slabs.is_contiguous() and N % 8 == 0, "bad slabs")
     if out is None:
         out = torch.empty((M, N), dtype=torch.bfloat16, device=slabs.device)
     if residual is not None:
         expect(residual.dtype == torch.bfloat16 and tuple(residual.shape) == (M, N) and residual.stride(-1) == 1,
                "residual must be bf16 [M, N]")
     native().slab_reduce(ptr(out), out.stride(0), ptr(slabs), S, M, N, ptr(residual),
-                         residual.stride(0) if residual is not None else 0, stream(slabs))
+                         residual.stride(0) if residual is not None else 0, stream(slabs),
+                         int(slabs.dtype == torch.bfloat16))
     return out
 
 

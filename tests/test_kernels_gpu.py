@@ -508,6 +508,36 @@ def test_stream_gemm(cfg, M, N, K, S):
         close(ops.slab_reduce(slabs, res), ref.gemm_bt(x, w, residual=res), atol=5e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("cfg,M,S", [(10, 128, 8), (10, 100, 4), (13, 64, 8), (30, 5, 4), (27, 200, 8), (20, 128, 2)])
+def test_bf16_split_k_slabs_and_their_consumers(cfg, M, S):
+    """bf16 split-K slabs (``slab_dtype=bf16``) are the fp32 slabs rounded to bf16, bit for bit; the
+    consumers (slab RMSNorm, RoPE / KV write, slab_reduce) sum bf16 slabs exactly as they sum the same
+    values held in fp32 (slab order, fp32 adds): bitwise equal outputs."""
+    N, K = (1792, 2048) if cfg == 20 else (1024, 2048)
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    ws = ops.shuffle_weights(w)
+    s32 = ops.stream_gemm(x, ws, splits=S, cfg=cfg, nt=True)
+    s16 = ops.stream_gemm(x, ws, splits=S, cfg=cfg, nt=True, slab_dtype=torch.bfloat16)
+    assert s16.dtype == torch.bfloat16 and s16.shape == s32.shape
+    assert torch.equal(s16, s32.to(torch.bfloat16))
+    up = s16.float()  # the bf16 values in fp32 slabs
+    g, r = bf(N), bf(M, N)
+    a = ops.rmsnorm(s16, g, 1e-5, residual=r)
+    b = ops.rmsnorm(up, g, 1e-5, residual=r)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    assert torch.equal(ops.slab_reduce(s16, r), ops.slab_reduce(up, r))
+    # RoPE / KV write over a [S, T, (Hq + 2 Hkv) D] slab stack (8 + 2 x 4 heads of 64)
+    Hq, Hkv, D, bs, nb = 8, 4, 64, 64, 4
+    qs = s16[:, :, :(Hq + 2 * Hkv) * D].contiguous()
+    cs = ref.rope_cos_sin(ref.llama3_inv_freq(D, 500000.0, None), 1024).to(DEV)
+    pos = torch.randint(0, 1000, (M,), device=DEV, dtype=torch.int32)
+    slots = torch.randperm(nb * bs, device=DEV)[:M].to(torch.int64)
+    caches = [torch.zeros(nb, Hkv, bs, D, device=DEV, dtype=torch.bfloat16) for _ in range(4)]
+    q16 = ops.rope_kv_write(qs, pos, cs, caches[0], caches[1], slots, Hq, Hkv, D)
+    q32 = ops.rope_kv_write(qs.float().contiguous(), pos, cs, caches[2], caches[3], slots, Hq, Hkv, D)
+    assert torch.equal(q16, q32) and torch.equal(caches[0], caches[2]) and torch.equal(caches[1], caches[3])
+
+
 @pytest.mark.parametrize("cfg,S", [(10, 8), (10, 16), (14, 8), (9, 8)])
 def test_stream_gemm_slice_per_xcd_mapping(cfg, S):
     """The A/B block mapping that groups K-slices (not tiles) per XCD (``stream_gemm_set_slice_xcd``):

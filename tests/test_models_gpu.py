@@ -58,6 +58,29 @@ def test_decode_stream_matches_row_major_path_and_reference(B):
     assert err < 0.15, err
 
 
+@pytest.mark.parametrize("B", [20, 128, 200])
+def test_bf16_decode_slabs_match_fp32_slabs_and_reference(B):
+    """``LlamaModel.slab_bf16``: the decode projections' split-K slabs stored as bf16 -- within bf16
+    noise of the fp32-slab decode and of the fp32 CPU reference."""
+    cfg = decoder_config("tiny-llama")
+    w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=5, interleave_mlp=True)
+    gen = torch.Generator().manual_seed(B)
+    prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
+               for n in torch.randint(10, 150, (B,), generator=gen)]
+    wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
+    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+    m.slab_bf16 = False
+    h32, lg32 = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    m.slab_bf16 = True
+    h16, lg16 = _run(m, cfg, prompts, DEV, torch.bfloat16)
+    torch.testing.assert_close(h16.float(), h32.float(), atol=6e-2, rtol=5e-2)
+    torch.testing.assert_close(lg16.float(), lg32.float(), atol=6e-2, rtol=5e-2)
+    m_ref = LlamaModel(cfg, {k: v.bfloat16().float() for k, v in w32.items()}, "cpu", interleaved_mlp=True)
+    h_ref, _ = _run(m_ref, cfg, prompts, "cpu", torch.float32)
+    err = (h16.float().cpu() - h_ref).abs().max().item()
+    assert err < 0.15, err
+
+
 @pytest.mark.parametrize("B", [4, 128])
 def test_default_path_keeps_unfolded_norm_gains(B):
     """the default GPU model does NOT fold the RMSNorm gains into the projections (one
