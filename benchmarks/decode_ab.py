@@ -83,6 +83,10 @@ ARMS = {
     "slicexcd": {"_slice_xcd": 1},
     # bf16 split-K slabs (LlamaModel.slab_bf16) against fp32
     "slab16": {"_slab16": True},
+    # split counts re-tuned for bf16 slabs
+    "qkv8": {"qkv": (10, 8)},
+    "down16": {"down": (10, 16)},
+    "o4b": {"o": (10, 4)},
     "slab32": {"_slab16": False},
 }
 
