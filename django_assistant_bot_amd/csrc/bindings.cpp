@@ -157,25 +157,27 @@ PYBIND11_MODULE(_native, m) {
      py::arg("order") = 0, py::arg("w0") = 0, py::arg("w0_bytes") = 0, py::arg("w1") = 0, py::arg("w1_bytes") = 0,
      py::arg("w_blocks") = 0);
   m.def("gemm_bt", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
-                      int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s, int b_rows) {
+                      int epilogue, int out_f32, u row_group, u q_group, u allow, int allow_words, u s, int b_rows,
+                      int b_group) {
     check(dab::gemm_bt(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, out_f32,
-                       (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s), b_rows),
+                       (const int*)row_group, (const int*)q_group, (const uint32_t*)allow, allow_words, ST(s), b_rows,
+                       b_group),
           "gemm_bt");
   }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
      py::arg("residual"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"),
      py::arg("out_f32"), py::arg("row_group"), py::arg("q_group"), py::arg("allow"), py::arg("allow_words"),
-     py::arg("s"), py::arg("b_rows") = 0);
+     py::arg("s"), py::arg("b_rows") = 0, py::arg("b_group") = 1);
   m.def("gemm_mid_ok", &dab::gemm_mid_ok);
   m.def("gemm_mid_slab_bytes", &dab::gemm_mid_slab_bytes);
   m.def("gemm_mid_counters", &dab::gemm_mid_counters);
   m.def("gemm_mid", [](u A, long lda, u B, u C, long ldc, u residual, long ldr, int M, int N, int K, int epilogue,
-                       u slabs, long slab_bytes, u cnt, int n_cnt, u s, int variant) {
+                       u slabs, long slab_bytes, u cnt, int n_cnt, u s, int variant, int b_group) {
     check(dab::gemm_mid(CVP(A), lda, CVP(B), VP(C), ldc, CVP(residual), ldr, M, N, K, epilogue, VP(slabs), slab_bytes,
-                        (int*)cnt, n_cnt, ST(s), variant),
+                        (int*)cnt, n_cnt, ST(s), variant, b_group),
           "gemm_mid");
   }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("C"), py::arg("ldc"), py::arg("residual"), py::arg("ldr"),
      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("slabs"), py::arg("slab_bytes"),
-     py::arg("cnt"), py::arg("n_cnt"), py::arg("s"), py::arg("variant") = 0);
+     py::arg("cnt"), py::arg("n_cnt"), py::arg("s"), py::arg("variant") = 0, py::arg("b_group") = 1);
   m.def("gemm256_ok", &dab::gemm256_ok);
   m.def("gemm256_stamped", [](u A, long lda, u B, u C, u bias, u residual, int M, int N, int K, int epilogue,
                               int b_shuf, u stamps, int stamp_tiles, u s, int store_aux) {
@@ -194,13 +196,13 @@ PYBIND11_MODULE(_native, m) {
     return r;
   });
   m.def("gemm256", [](u A, long lda, u B, long ldb, u C, long ldc, u bias, u residual, long ldr, int M, int N, int K,
-                      int epilogue, u s, int b_shuf) {
+                      int epilogue, u s, int b_shuf, int b_group) {
     check(dab::gemm256(CVP(A), lda, CVP(B), ldb, VP(C), ldc, CVP(bias), CVP(residual), ldr, M, N, K, epilogue, ST(s),
-                       b_shuf),
+                       b_shuf, b_group),
           "gemm256");
   }, py::arg("A"), py::arg("lda"), py::arg("B"), py::arg("ldb"), py::arg("C"), py::arg("ldc"), py::arg("bias"),
      py::arg("residual"), py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("epilogue"), py::arg("s"),
-     py::arg("b_shuf") = 0);
+     py::arg("b_shuf") = 0, py::arg("b_group") = 1);
   m.def("gemm_score_candidates", [](u A, long lda, u B, long ldb, int M, int N, int K, u row_group, u q_group, u thr,
                                     u cnt, u cand_val, u cand_idx, int cap, u s) {
     check(dab::gemm_score_candidates(CVP(A), lda, CVP(B), ldb, M, N, K, reinterpret_cast<const int*>(row_group),
@@ -232,13 +234,13 @@ PYBIND11_MODULE(_native, m) {
      py::arg("q_group"), py::arg("thr"), py::arg("cnt"), py::arg("cand_val"), py::arg("cand_idx"), py::arg("cap"),
      py::arg("s"), py::arg("b_rows") = 0);
   m.def("stream_gemm", [](u X, long ldx, u W, long ldw, u out, long ldo, u residual, long ldr, int M, int N, int K,
-                          int S, int epilogue, u s, int nt, int cfg, float norm_eps, int slab_bf16) {
+                          int S, int epilogue, u s, int nt, int cfg, float norm_eps, int slab_bf16, int w_group) {
     check(dab::stream_gemm(CVP(X), ldx, CVP(W), ldw, VP(out), ldo, CVP(residual), ldr, M, N, K, S, epilogue, ST(s), nt,
-                           cfg, norm_eps, slab_bf16),
+                           cfg, norm_eps, slab_bf16, w_group),
           "stream_gemm");
   }, py::arg("X"), py::arg("ldx"), py::arg("W"), py::arg("ldw"), py::arg("out"), py::arg("ldo"), py::arg("residual"),
      py::arg("ldr"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("S"), py::arg("epilogue"), py::arg("s"),
-     py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f, py::arg("slab_bf16") = 0);
+     py::arg("nt"), py::arg("cfg"), py::arg("norm_eps") = 0.f, py::arg("slab_bf16") = 0, py::arg("w_group") = 1);
   m.def("stream_gemm_bn", &dab::stream_gemm_bn);
   m.def("stream_gemm_max_m", &dab::stream_gemm_max_m);
   m.def("stream_gemm_set_slice_xcd", &dab::stream_gemm_set_slice_xcd);

@@ -48,6 +48,7 @@ struct GemmParams {
   int* cand_idx;     // [M, cap] column n
   int cap;
   int rows_b;  // SHUF: rows of the B copy (>= N, multiple of 16)
+  int bgrp;    // SHUF: row blocks per group of the copy (shuffle_weights(w, group)), 1 = plain
 };
 
 __device__ __forceinline__ int gsw(int r) { return 2 * ((r >> 1) & 3); }
@@ -93,7 +94,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_bt_kernel(GemmParams p) {
       const bf16* gb;
       if constexpr (SHUF) {  // piece idx = 16-row block idx / 2, 32-k block idx % 2 (clamped past the copy)
         const int blk = min(n0 / 16 + (idx >> 1), p.rows_b / 16 - 1);
-        gb = p.B + ((size_t)blk * (p.K / 32) + k0 / 32 + (idx & 1)) * 512 + lane * 8;
+        const int G = p.bgrp;  // fragment (blk, chunk) at ((blk / G) K/32 + chunk) G + blk % G
+        gb = p.B + (((size_t)(blk / G) * (p.K / 32) + k0 / 32 + (idx & 1)) * G + blk % G) * 512 + lane * 8;
       } else {
         const int e = idx * 64 + lane;
         const int r = e >> 3, pos = e & 7;
@@ -280,9 +282,10 @@ static int launch_gemm(const GemmParams& p, bool big, hipStream_t s, bool shuf) 
 
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
-            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows) {
+            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows, int b_group) {
   if (M <= 0 || N <= 0) return 0;
   if (K % 64 || N % 4 || lda % 8 || ldb % 8) return hipErrorInvalidValue;
+  if (b_group < 1 || (b_group > 1 && (b_rows <= 0 || b_rows % (16 * b_group)))) return hipErrorInvalidValue;
   if (epilogue == EPI_SWIGLU && (N % 32 || out_f32)) return hipErrorInvalidValue;
   if (epilogue == EPI_SWIGLU8 && (N % 32 || out_f32 || bias || residual)) return hipErrorInvalidValue;
   if (b_rows > 0 && (b_rows < N || b_rows % 16 || ldb != K)) return hipErrorInvalidValue;
@@ -305,6 +308,7 @@ int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   p.allow_words = allow_words;
   p.out_f32 = out_f32;
   p.rows_b = b_rows;
+  p.bgrp = b_group;
   const bool sh = b_rows > 0;
   // large problems: 256x256 tiles, 8 waves of 128x64 (half the LDS fragment traffic per MFMA of the
   // 64x64 wave tile); small M or N: 128x128 tiles, 4 waves (less padding, more workgroups)
@@ -342,6 +346,7 @@ int gemm_score_candidates(const void* A, long lda, const void* B, long ldb, int 
   if (b_rows == 0 && M >= 32 && M <= 64 && K % 128 == 0)
     return stream_score_candidates(A, lda, B, ldb, M, N, K, row_group, q_group, thr, cnt, cand_val, cand_idx, cap, s);
   GemmParams p{};
+  p.bgrp = 1;
   p.A = (const bf16*)A;
   p.B = (const bf16*)B;
   p.row_group = row_group;

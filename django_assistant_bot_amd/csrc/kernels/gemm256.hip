@@ -57,6 +57,7 @@ struct G256 {
   long lda, ldb, ldc, ldr;
   int gm;  // tile rows per group of the grouped tile order
   int rows_b;  // SHUF: rows of the B copy (>= N)
+  int bgrp;    // SHUF: row blocks per group of the B copy, 1 or 8 (shuffle_weights(w, 8))
   // G_CAND (index threshold search, see gemm.hip EPI_CANDIDATES): filtered scores >= thr[m] are
   // appended to row m's candidate list; no C is written and N need not be a multiple of 256
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -223,10 +224,15 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   // SHUF: wave w copies 16-row block w of each 128-row half, both 32-k blocks of the K-tile
   // (1 KB each, lane-linear); block (rb, kb) of a K-tile sits at byte (K / 32 rb + kb) 1 KB
   const unsigned kblk = (unsigned)(p.K / 32) * 1024u;
-  const unsigned vB0 = SHUF ? (unsigned)(lane * 16) + (unsigned)w * kblk : (unsigned)((srow * p.ldb + 8 * cc) * 2);
-  const unsigned vB1 = SHUF ? vB0 + 1024u : vB0 + (unsigned)(64 * p.ldb * 2);
+  // SHUF grouped copy (p.bgrp = 8, shuffle_weights(w, 8)): the 8 blocks of a 128-row half are
+  // adjacent per k chunk -- block w of the half w KB in, a k chunk 8 KB on
+  const bool bgrp = SHUF && p.bgrp == 8;
+  const unsigned cb = bgrp ? 8192u : 1024u;
+  const unsigned vB0 = SHUF ? (unsigned)(lane * 16) + (unsigned)w * (bgrp ? 1024u : kblk)
+                            : (unsigned)((srow * p.ldb + 8 * cc) * 2);
+  const unsigned vB1 = SHUF ? vB0 + cb : vB0 + (unsigned)(64 * p.ldb * 2);
   const unsigned vB2 = SHUF ? vB0 + 8u * kblk : vB0 + (unsigned)(128 * p.ldb * 2);
-  const unsigned vB3 = SHUF ? vB2 + 1024u : vB0 + (unsigned)(192 * p.ldb * 2);
+  const unsigned vB3 = SHUF ? vB2 + cb : vB0 + (unsigned)(192 * p.ldb * 2);
   auto rsrc_a = [&](int mm) {
     const long rows = min(256, p.M - mm);
     return make_rsrc(p.A + (size_t)mm * p.lda, (unsigned)(((rows - 1) * p.lda + p.K) * 2));
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(G256 p) {
   auto stage = [&](int buf, int slot, int kt, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb) {
     const bool shb = SHUF && slot >= 2;  // (slot is a compile-time constant at every call)
     char* dst = smem + buf * kBuf + slot * kHalf + w * (shb ? 2048 : 1024);
-    const unsigned so = (unsigned)kt * (shb ? 2048u : 128u);
+    const unsigned so = (unsigned)kt * (shb ? 2u * cb : 128u);
     const __amdgpu_buffer_rsrc_t r = slot < 2 ? ra : rb;
     const unsigned v0 = slot == 0 ? vA0 : slot == 1 ? vA2 : slot == 2 ? vB0 : vB2;
     const unsigned v1 = slot == 0 ? vA1 : slot == 1 ? vA3 : slot == 2 ? vB1 : vB3;
@@ -837,8 +843,10 @@ int gemm256_ok(int M, int N, int K, long lda, long ldb) {
 // b_shuf: B is in the shuffle_weights layout (ldb == K).  Epilogues: 0 none, 1 GELU, 2 SwiGLU over
 // 16-row [gate | up] groups, 4 SwiGLU over 8-row groups (no bias); bias / residual optional.
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf) {
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf,
+            int b_group) {
   if (!gemm256_ok(M, N, K, lda, ldb)) return hipErrorInvalidValue;
+  if (b_group != 1 && !(b_group == 8 && b_shuf)) return hipErrorInvalidValue;  // (N % 256: whole groups)
   if ((epilogue == G_SWIGLU || epilogue == G_SWIGLU8) && residual) return hipErrorInvalidValue;
   if (epilogue == G_SWIGLU8 && bias) return hipErrorInvalidValue;
   if (b_shuf && ldb != K) return hipErrorInvalidValue;
@@ -856,6 +864,7 @@ int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc,
   p.ldc = ldc;
   p.ldr = ldr;
   p.rows_b = N;
+  p.bgrp = b_group;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const int tiles = ((M + 255) / 256) * (N / 256);

@@ -54,6 +54,7 @@ struct GMid {
   int gn;   // groups = 8 * gpx
   int q, r;  // tiles_n * kt = q * gn + r iterations: group j owns q (+1 for j < r)
   unsigned b_bytes, slab_bytes;
+  int bgrp;  // row blocks per group of the B copy: 1 (plain) or 8 (shuffle_weights(w, 8))
 };
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -151,7 +152,12 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
     vA0 = (unsigned)((srow * p.lda + 8 * cc) * 2);
   }
   const unsigned kblk = (unsigned)(p.K / 32) * 1024u;  // bytes of one 16-row block over all of K
-  const unsigned vB0 = (unsigned)(lane * 16) + (unsigned)w * kblk, vB2 = vB0 + 8u * kblk;
+  // grouped copy (p.bgrp = 8, shuffle_weights(w, 8)): the 8 blocks of a 128-row half adjacent per k
+  // chunk, so block w of a half is w KB in and a k chunk is 8 KB on (the half itself starts where
+  // the plain layout's does)
+  const bool bgrp = p.bgrp == 8;
+  const unsigned cb = bgrp ? 8192u : 1024u;  // bytes per 32-deep k chunk of a block
+  const unsigned vB0 = (unsigned)(lane * 16) + (unsigned)w * (bgrp ? 1024u : kblk), vB2 = vB0 + 8u * kblk;
   const long a_rows = min(128, p.M - m0);
   const __amdgpu_buffer_rsrc_t rA = mk_rsrc(p.A + (size_t)m0 * p.lda, (unsigned)(((a_rows - 1) * p.lda + p.K) * 2));
   const __amdgpu_buffer_rsrc_t rB = mk_rsrc(p.B, p.b_bytes);
@@ -159,14 +165,14 @@ __global__ __launch_bounds__(512) void gemm_mid_kernel(GMid p) {
   auto stage = [&](int buf, int nt, int kk) {
     char* dst = smem + buf * kStage;
     const unsigned sa = (unsigned)kk * (unsigned)(BK * 2);
-    const unsigned sb = (unsigned)nt * 16u * kblk + (unsigned)kk * (unsigned)(BK * 32);
+    const unsigned sb = (unsigned)nt * 16u * kblk + (unsigned)kk * (unsigned)(BK / 32) * cb;
     if constexpr (BK == 64) {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + 8192 + w * 1024), 16, vA1, sa, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 2048), 16, vB0, sb, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 2048 + 1024), 16, vB0 + 1024u, sb, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + w * 2048 + 1024), 16, vB0 + cb, sb, 0, 0);
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 16384 + w * 2048), 16, vB2, sb, 0, 0);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 16384 + w * 2048 + 1024), 16, vB2 + 1024u, sb,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rB, (lds_void*)(dst + kA + 16384 + w * 2048 + 1024), 16, vB2 + cb, sb,
                                                0, 0);
     } else {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rA, (lds_void*)(dst + w * 1024), 16, vA0, sa, 0, 0);
@@ -482,8 +488,10 @@ int gemm_mid_counters(int M, int N) {
 // BK 32 (6-stage ring) measured 5-20 % slower than BK 64 on every mid shape, with LDS bank
 // conflicts on its 64-B A rows (profiles/gemm_mid_r6.md): kept as an A/B arm only.
 int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
-             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant) {
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant,
+             int b_group) {
   if (!gemm_mid_ok(M, N, K, lda)) return hipErrorInvalidValue;
+  if (b_group != 1 && b_group != 8) return hipErrorInvalidValue;
   if (epilogue != MID_NONE && epilogue != MID_SWIGLU8) return hipErrorInvalidValue;
   if (epilogue == MID_SWIGLU8 && residual) return hipErrorInvalidValue;
   if (!slabs || !cnt || slab_bytes < gemm_mid_slab_bytes() || n_cnt < gemm_mid_counters(M, N) ||
@@ -516,6 +524,7 @@ int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const vo
   p.r = iters % p.gn;
   p.b_bytes = (unsigned)((long)N * K * 2);
   p.slab_bytes = (unsigned)slab_bytes;
+  p.bgrp = b_group;
 #define MID_LAUNCH(E, R, BKV, D) hipLaunchKernelGGL((gemm_mid_kernel<E, R, BKV, D>), dim3(grid), dim3(512), 0, s, p)
 #define MID_BK(E, R)                       \
   do {                                     \

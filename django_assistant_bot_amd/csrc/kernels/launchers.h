@@ -59,7 +59,7 @@ int paged_decode_attention(const void* q, const void* k_cache, const void* v_cac
 // [gate | up] groups
 int gemm_bt(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias, const void* residual,
             long ldr, int M, int N, int K, int epilogue, int out_f32, const int* row_group, const int* q_group,
-            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows = 0);
+            const uint32_t* allow, int allow_words, hipStream_t s, int b_rows = 0, int b_group = 1);
 
 // gemm256.hip (large-M prefill / encoder GEMM, 256x256 phased schedule; epilogue 0 none, 1 GELU,
 // 2 SwiGLU on [gate 16 | up 16]-interleaved weight rows; bias / residual optional)
@@ -76,7 +76,8 @@ int gemm256_candidates_stamped(const void* A, long lda, const void* B, int M, in
 int gemm256_stamped(const void* A, long lda, const void* B, void* C, const void* bias, const void* residual, int M,
                     int N, int K, int epilogue, int b_shuf, void* stamps, int stamp_tiles, hipStream_t s, int store_aux);
 int gemm256(const void* A, long lda, const void* B, long ldb, void* C, long ldc, const void* bias,
-            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0);
+            const void* residual, long ldr, int M, int N, int K, int epilogue, hipStream_t s, int b_shuf = 0,
+            int b_group = 1);
 
 // gemm_mid.hip (M = 256..4096: mixed serving steps / single prompts; grouped stream-K over the N x K
 // plane, 128 x 256 tiles, in-launch last-arriver combine; B in the shuffle_weights layout;
@@ -85,13 +86,14 @@ int gemm_mid_ok(int M, int N, int K, long lda);
 long gemm_mid_slab_bytes();
 int gemm_mid_counters(int M, int N);
 int gemm_mid(const void* A, long lda, const void* B, void* C, long ldc, const void* residual, long ldr, int M, int N,
-             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant = 0);
+             int K, int epilogue, void* slabs, long slab_bytes, int* cnt, int n_cnt, hipStream_t s, int variant = 0,
+             int b_group = 1);
 
 // stream_gemm.hip (warp-specialised decode GEMM, M <= 256: bf16 / SwiGLU / fp32 split-K slabs; cfg selects
 // the tile / ring configuration, stream_gemm_bn(cfg) = weight rows per workgroup)
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps = 0.f,
-                int slab_bf16 = 0);
+                int slab_bf16 = 0, int w_group = 1);
 int stream_gemm_bn(int cfg);
 // fp32 (or bf16: slab_bf16) split-K slabs [S][M][N] -> bf16 [M, N] (+ residual)
 int slab_reduce(void* out, long ldo, const void* slabs, int S, int M, int N, const void* residual, long ldr,

@@ -52,6 +52,7 @@ struct StreamParams {
   float norm_eps;
   int slice_xcd;  // block -> (tile, slice) with the K-slices (not the tiles) grouped per XCD
   int slab_bf16;  // S > 1: bf16 K-slice slabs instead of fp32
+  int wgrp;       // SHUF: row blocks per group of the weight copy (shuffle_weights(w, group)), 1 = plain
   // ST_EPI_CAND (index threshold search over W = index rows, X = queries): filtered scores
   // >= thr[m] are appended to query m's list (gemm.hip EPI_CANDIDATES); N need not divide BN
   const int* row_group;  // [N] (<0 = deleted) or null
@@ -178,14 +179,31 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
     // SHUF: whole 16-row blocks (a block's rows are interleaved in every 1 KB fragment; the rows
     // past N of a partial block exist in the copy and are dropped by the epilogues)
     const int w_rows = SHUF ? min(BN, (p.N - n0 + 15) / 16 * 16) : min(BN, p.N - n0);
-    const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (size_t)n0 * p.ldw), 0,
-                                                        (int)(w_rows * p.ldw * 2), 0x00020000);
+    // grouped fragment layout (p.wgrp = G > 1, shuffle_weights(w, group=G)): the G row blocks of a
+    // group are adjacent per 32-deep k chunk, fragment (b, c) at ((b / G) K/32 + c) G + b % G KB;
+    // block offsets are then absolute (descriptor over the whole copy) and a k chunk is G KB on
+    const bool grp = SHUF && p.wgrp > 1;
+    const auto wres = __builtin_amdgcn_make_buffer_rsrc((void*)(p.W + (grp ? 0 : (size_t)n0 * p.ldw)), 0,
+                                                        grp ? (int)((long)p.N * p.K * 2) : (int)(w_rows * p.ldw * 2),
+                                                        0x00020000);
+    const int cstride = SHUF ? (grp ? p.wgrp : 1) * 1024 : 0;  // bytes per 32-deep k chunk (SHUF)
     // row-major W: lane (li, g) reads row li, k 8g..8g+7 of a 16 x 32 chunk (16 rows x 64 B per load);
     // SHUF (shuffle_weights layout [N/16][K/32][64 lanes][8]): every load is 1 KB contiguous
-    const int w_voff = SHUF ? lane * 16 + ((k_begin + kg * KW) / 32) * 1024
+    const int w_voff = SHUF ? lane * 16 + ((k_begin + kg * KW) / 32) * cstride
                             : (int)(((16 * RT * rg + li) * p.ldw + k_begin + kg * KW + 8 * g) * 2);
     const int a_stride = SHUF ? p.K * 32 : 16 * (int)p.ldw * 2;
     const int w_rowtile0 = SHUF ? RT * rg * p.K * 32 : 0;
+    // SHUF: byte offset of row block (RT rg + a) of the tile at k chunk 0
+    int wblk[RT];
+#pragma unroll
+    for (int a = 0; a < RT; ++a) {
+      if (grp) {
+        const int b = n0 / 16 + RT * rg + a;
+        wblk[a] = ((b / p.wgrp) * (p.K / 32) * p.wgrp + b % p.wgrp) * 1024;
+      } else {
+        wblk[a] = a * a_stride + w_rowtile0;
+      }
+    }
     bf16x8 wr[NWIN][RT][CPW];
     // clamped past the slice end: the ring keeps a branch-free load stream, so the compiler's
     // in-order vmcnt count stays exact (the spare loads re-read the last stage from L2)
@@ -197,10 +215,14 @@ __global__ __launch_bounds__(64 * (NWC + NL), 1) void stream_gemm_kernel(StreamP
         const int chunk = (k_begin + kg * KW) / 32 + min(st, nst - 1) * (KS / 32) + c;
         const int off = (chunk * (BN / 16) + RT * rg + a) * 1024 + lane * 16;
         wr[slot][a][c] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, off, 0, NT_W ? 2 : 0));
-      } else {
-        const int soff = min(st, nst - 1) * KS * (SHUF ? 32 : 2) + a * a_stride + w_rowtile0;
+      } else if constexpr (SHUF) {
+        const int soff = min(st, nst - 1) * (KS / 32) * cstride + wblk[a];
         wr[slot][a][c] = __builtin_bit_cast(
-            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + (SHUF ? 1024 : 64) * c, soff, NT_W ? 2 : 0));
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + cstride * c, soff, NT_W ? 2 : 0));
+      } else {
+        const int soff = min(st, nst - 1) * KS * 2 + a * a_stride + w_rowtile0;
+        wr[slot][a][c] = __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wres, w_voff + 64 * c, soff, NT_W ? 2 : 0));
       }
     };
     static_for<0, NWIN>([&](auto S_) DAB_INLINE {
@@ -510,7 +532,7 @@ int stream_gemm_slice_xcd() { return g_slice_xcd; }
 
 int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, long ldo, const void* residual, long ldr,
                 int M, int N, int K, int S, int epilogue, hipStream_t s, int nt_weights, int cfg, float norm_eps,
-                int slab_bf16) {
+                int slab_bf16, int w_group) {
   constexpr int KS = 128;
   if (M <= 0 || N <= 0) return 0;
   const int bn = stream_gemm_bn(cfg);
@@ -543,6 +565,9 @@ int stream_gemm(const void* X, long ldx, const void* W, long ldw, void* out, lon
   p.norm_eps = norm_eps;
   p.slice_xcd = g_slice_xcd && S % 8 == 0;
   p.slab_bf16 = S > 1 && slab_bf16;
+  p.wgrp = w_group < 1 ? 1 : w_group;
+  if (p.wgrp > 1 && (!kStreamCfgs[cfg].shuf || N % (16 * p.wgrp) || (long)N * K * 2 >= (1L << 31)))
+    return hipErrorInvalidValue;
   if (p.norm && (residual || K % 8 || M > stream_gemm_max_m(cfg))) return hipErrorInvalidValue;
   launch_any(cfg, p, s, nt_weights != 0);
   return hipGetLastError();

@@ -163,7 +163,11 @@ class LlamaModel:
                 qkv_w, an = self._fold(qkv_w, an), torch.ones_like(an)
                 gu_w, mn = self._fold(gu_w, mn), torch.ones_like(mn)
             fmt = ops.shuffle_weights if self.frag else (lambda t: t)
-            self.layers.append(DecoderLayer(an, fmt(qkv_w), proj(f"l{i}.o_w"), mn, fmt(gu_w), proj(f"l{i}.down_w")))
+            if i == 0:
+                self.gate_up_group = 8 if (self.frag and self.gate_up_grouped and gu_w.shape[0] % 128 == 0
+                                           and gu_w.numel() * 2 < (1 << 31)) else 1
+            gu = ops.shuffle_weights(gu_w, self.gate_up_group) if self.frag else gu_w
+            self.layers.append(DecoderLayer(an, fmt(qkv_w), proj(f"l{i}.o_w"), mn, gu, proj(f"l{i}.down_w")))
             del qkv_w, gu_w
         if self.frag and consume:
             torch.cuda.empty_cache()
@@ -196,6 +200,15 @@ class LlamaModel:
         parts = [torch.empty_like(src) for _ in range(self.tp_size)]
         dist.all_gather(parts, src, group=self.tp_group)
         return torch.cat(parts, 1).to(local.device)
+
+    def set_gate_up_group(self, group: int) -> None:
+        """Re-lay every layer's gate_up copy as ``shuffle_weights(w, group)``, in place (captured
+        graphs keep their pointers but bake the group in: re-capture after a change).  A/B harness."""
+        if not self.frag or group == self.gate_up_group:
+            return
+        for L in self.layers:
+            L.gate_up_w.copy_(ops.shuffle_weights(ops.unshuffle_weights(L.gate_up_w, self.gate_up_group), group))
+        self.gate_up_group = group
 
     def _fragment_ok(self, weights: dict) -> bool:
         keys = ["lm_head" if "lm_head" in weights else "embed"] + [
@@ -269,6 +282,13 @@ class LlamaModel:
             return -1, 1
         return cfg, self._stream_splits(N, K, ops.native().stream_gemm_bn(cfg))
 
+    # gate_up in the grouped fragment layout (shuffle_weights(w, 8): the 8 row blocks of each 128-row
+    # group adjacent per 32-deep k chunk): the decode GEMM's 7 compute waves (one block each) then
+    # stream neighbouring bytes -- gate_up at batch 128 51.9 -> 47.9 us cold
+    # (profiles/decode_stream_layout_r6.md); every GEMM reading the copy takes the group size
+    gate_up_grouped = True
+    gate_up_group = 1
+
     # Split-K slabs of the decode projections as bf16 (the partial sums rounded once, as the TP path
     # hands them to its all-reduce) instead of fp32: half the bytes the producer writes and the
     # RMSNorm / RoPE consumers read; batch-128 decode step 7.503 -> 7.351 ms (benchmarks/decode_ab.py
@@ -286,15 +306,16 @@ class LlamaModel:
                 y = ops.linear(x, w)
                 return ops.silu_mul(y, group=8 if self.interleaved_mlp else 0)
             return ops.linear(x, w)
+        grp = self.gate_up_group if name == "gate_up" else 1
         if dec and self.frag:
             cfg, s = self._stream_choice(name, x.shape[0], w.shape[0], w.shape[1])
             if cfg >= 0:
                 if epilogue != ops.EPI_NONE:
-                    return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg)
+                    return ops.stream_gemm(x, w, epilogue=epilogue, nt=True, cfg=cfg, w_group=grp)
                 sd = torch.bfloat16 if (self.slab_bf16 and self.tp_size == 1) else torch.float32
-                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True, slab_dtype=sd)
+                out = ops.stream_gemm(x, w, splits=s, cfg=cfg, nt=True, slab_dtype=sd, w_group=grp)
                 return ops.slab_reduce(out) if (s > 1 and not allow_slabs) else out
-        return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag)
+        return ops.gemm_bt(x, w, epilogue=epilogue, shuffled=self.frag, b_group=grp)
 
     def forward(self, ids: torch.Tensor, meta: AttnMeta, kv: KVCache) -> torch.Tensor:
         """ids int32 [T] -> final hidden states [T, H] (after the last RMSNorm)."""
@@ -338,7 +359,8 @@ class LlamaModel:
                              meta.workspace, order=meta.order)
         h1 = ops.stream_gemm(a.view(T, self.hq * D), L.o_w, residual=h, cfg=self.STREAM_CFG_RES16, nt=True)
         gc, _ = self._stream_choice("gate_up", T, L.gate_up_w.shape[0], L.gate_up_w.shape[1])
-        act = ops.stream_gemm(h1, L.gate_up_w, epilogue=ops.EPI_SWIGLU8, cfg=gc, nt=True, norm_eps=cfg.eps)
+        act = ops.stream_gemm(h1, L.gate_up_w, epilogue=ops.EPI_SWIGLU8, cfg=gc, nt=True, norm_eps=cfg.eps,
+                              w_group=self.gate_up_group)
         return ops.stream_gemm(act, L.down_w, residual=h1, cfg=self.STREAM_CFG_RES16, nt=True)
 
     # Small decode batches: the paged attention is a chain of dependent memory round trips on a few

@@ -377,19 +377,20 @@ def use_gemm256(M: int, N: int, K: int, lda: int, ldb: int) -> bool:
 
 
 def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, row_group=None, q_group=None,
-            allow=None, out=None, shuffled=False, n=None):
+            allow=None, out=None, shuffled=False, n=None, b_group: int = 1):
     """C = A . B^T (+bias) (+act) (+residual) on MFMA; A [M, K], B [N, K] (K-contiguous rows).
 
     ``shuffled``: B is a ``shuffle_weights`` copy (the layout the decode GEMM streams, so a model
     keeps ONE copy of every projection) of ``B.shape[0]`` rows, of which the first ``n`` (default:
-    all) are the matrix."""
+    all) are the matrix; ``b_group`` 8: a ``shuffle_weights(w, 8)`` copy."""
+    expect(b_group == 1 or (shuffled and b_group == 8), "b_group: 1, or 8 with a shuffled copy")
     if shuffled:
         R = B.shape[0]
         N = R if n is None else int(n)
-        expect(R % 16 == 0 and B.shape[1] % 32 == 0 and B.is_contiguous() and R >= N,
-               "shuffled B: contiguous [R, K] copy, R % 16 == 0, K % 32 == 0, R >= n")
+        expect(R % (16 * b_group) == 0 and B.shape[1] % 32 == 0 and B.is_contiguous() and R >= N,
+               "shuffled B: contiguous [R, K] copy, R % (16 b_group) == 0, K % 32 == 0, R >= n")
         if not A.is_cuda:
-            Bu = unshuffle_weights(B)[:N]
+            Bu = unshuffle_weights(B, b_group)[:N]
             return ref.gemm_bt(A, Bu, bias, residual, epilogue, out_f32, row_group, q_group, allow)
     if not A.is_cuda:
         return ref.gemm_bt(A, B, bias, residual, epilogue, out_f32, row_group, q_group, allow)
@@ -430,26 +431,26 @@ def gemm_bt(A, B, bias=None, residual=None, epilogue=EPI_NONE, out_f32=False, ro
     plain = not out_f32 and row_group is None and q_group is None and allow is None
     if (plain and shuffled and N == B.shape[0] and bias is None and epilogue in (EPI_NONE, EPI_SWIGLU8)
             and use_gemm_mid(M, N, K, A.stride(0))):
-        return gemm_mid(A, B, residual=residual, epilogue=epilogue, out=out)
+        return gemm_mid(A, B, residual=residual, epilogue=epilogue, out=out, b_group=b_group)
     if (epilogue in (EPI_NONE, EPI_GELU, EPI_SWIGLU, EPI_SWIGLU8) and plain and (not shuffled or N == B.shape[0])
             and use_gemm256(M, N, K, A.stride(0), B.stride(0))):
-        return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
+        return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled, b_group)
     native().gemm_bt(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
                      residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), int(out_f32),
                      ptr(row_group), ptr(q_group), ptr(allow), allow_words, stream(A),
-                     B.shape[0] if shuffled else 0)
+                     B.shape[0] if shuffled else 0, int(b_group))
     return out
 
 
-def _gemm256_into(A, B, out, bias, residual, epilogue, shuffled):
+def _gemm256_into(A, B, out, bias, residual, epilogue, shuffled, b_group=1):
     M, K = A.shape
     native().gemm256(ptr(A), A.stride(0), ptr(B), B.stride(0), ptr(out), out.stride(0), ptr(bias), ptr(residual),
                      residual.stride(0) if residual is not None else 0, M, B.shape[0], K, int(epilogue), stream(A),
-                     int(shuffled))
+                     int(shuffled), int(b_group))
     return out
 
 
-def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
+def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False, b_group: int = 1):
     """The phased 256x256 kernel directly, for any M (``gemm_bt`` takes it from M >= 1024):
     tests and benchmarks.  N % 256 == 0, K % 128 == 0."""
     M, K = A.shape
@@ -459,7 +460,7 @@ def gemm256(A, B, bias=None, residual=None, epilogue=EPI_NONE, shuffled=False):
     expect(not shuffled or (B.is_contiguous() and B.shape[1] == K), "shuffled B must be a contiguous [N, K] copy")
     n_out = N // 2 if epilogue in (EPI_SWIGLU, EPI_SWIGLU8) else N
     out = torch.empty((M, n_out), dtype=torch.bfloat16, device=A.device)
-    return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled)
+    return _gemm256_into(A, B, out, bias, residual, epilogue, shuffled, b_group)
 
 
 _MID_WS: dict = {}
@@ -484,7 +485,7 @@ def gemm_mid_ok(M: int, N: int, K: int, lda: int) -> bool:
     return bool(native().gemm_mid_ok(M, N, K, lda)) and -(-M // 128) * (N // 256) <= (1 << 16)
 
 
-def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0):
+def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0, b_group: int = 1):
     """C = A . B^T (+ residual) or SwiGLU over 8-row [gate | up] groups, B a ``shuffle_weights`` copy:
     the mid-M kernel (``gemm_mid.hip``: grouped stream-K, 128 x 256 tiles, in-launch owner combine) for
     M = 256..4096 (mixed serving steps, single prompts).  Bit-reproducible: the split-K partials are
@@ -496,6 +497,7 @@ def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0)
     expect(A.stride(-1) == 1 and B.is_contiguous() and B.shape[1] == K, "A K-contiguous, B a contiguous [N, K] copy")
     expect(epilogue in (EPI_NONE, EPI_SWIGLU8), "gemm_mid epilogues: none (+residual) or SwiGLU8")
     expect(gemm_mid_ok(M, N, K, A.stride(0)), "gemm_mid: N % 256, K % 64, M <= 4096, 16-B rows")
+    expect(b_group in (1, 8), "gemm_mid: b_group 1 or 8")
     n_out = N // 2 if epilogue == EPI_SWIGLU8 else N
     if residual is not None:
         expect(epilogue == EPI_NONE and residual.dtype == torch.bfloat16 and residual.stride(-1) == 1
@@ -507,7 +509,7 @@ def gemm_mid(A, B, residual=None, epilogue=EPI_NONE, out=None, variant: int = 0)
     slabs, cnt = _mid_workspace(A.device, s)
     native().gemm_mid(ptr(A), A.stride(0), ptr(B), ptr(out), out.stride(0), ptr(residual),
                       residual.stride(0) if residual is not None else 0, M, N, K, int(epilogue), ptr(slabs),
-                      slabs.numel() * 4, ptr(cnt), cnt.numel(), s, int(variant))
+                      slabs.numel() * 4, ptr(cnt), cnt.numel(), s, int(variant), int(b_group))
     return out
 
 
@@ -603,27 +605,33 @@ STREAM_KS = 128
 STREAM_MAX_M = 256  # decode batches / prefill last-token LM heads up to this many rows stream the weights
 
 
-def shuffle_weights(w: torch.Tensor) -> torch.Tensor:
+def shuffle_weights(w: torch.Tensor, group: int = 1) -> torch.Tensor:
     """[N, K] row-major -> the same values in the fragment layout [N/16][K/32][64 lanes][8]: the
     16 x 32 tile an MFMA A fragment covers is 1 KB contiguous, in lane order (lane l = row l & 15,
     k 8 (l >> 4) .. + 8), so every weight load of the streaming kernel is one fully coalesced 1 KB
     read, and the prefill GEMMs' LDS-DMA copies whole blocks (gemm256 / gemm_bt ``shuffled``).
-    Returned with shape [N, K] (only the memory order changes)."""
+    ``group`` G > 1: the grouped form [N/(16G)][K/32][G][1 KB] -- the fragments of G consecutive
+    16-row blocks adjacent for each 32-deep k chunk, so the decode GEMM's waves (one block each)
+    stream neighbouring bytes (profiles/decode_stream_layout_r6.md); the kernels take it with
+    ``w_group`` / ``b_group`` = G.  Returned with shape [N, K] (only the memory order changes)."""
     N, K = w.shape
-    expect(N % 16 == 0 and K % 32 == 0, "shuffle_weights needs N % 16 == 0 and K % 32 == 0")
-    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous().view(N, K)
+    expect(N % (16 * group) == 0 and K % 32 == 0, "shuffle_weights needs N % (16 group) == 0 and K % 32 == 0")
+    f = w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4)
+    if group > 1:
+        f = f.reshape(N // (16 * group), group, K // 32, 512).permute(0, 2, 1, 3)
+    return f.contiguous().view(N, K)
 
 
-def unshuffle_weights(w: torch.Tensor) -> torch.Tensor:
+def unshuffle_weights(w: torch.Tensor, group: int = 1) -> torch.Tensor:
     """Inverse of ``shuffle_weights``."""
     N, K = w.shape
+    if group > 1:
+        w = w.reshape(N // (16 * group), K // 32, group, 512).permute(0, 2, 1, 3)
     return w.reshape(N // 16, K // 32, 4, 16, 8).permute(0, 3, 1, 2, 4).contiguous().view(N, K)
 
 
-
-
 def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=False, cfg=0, norm_eps: float = 0.0,
-                slab_dtype=torch.float32):
+                slab_dtype=torch.float32, w_group: int = 1):
     """Decode GEMM y = x w^T on the warp-specialised streaming kernel (``stream_gemm.hip``): bf16
     [M, N] (optional residual add), SwiGLU [M, N/2] over 16- / 8-row interleaved [gate | up] rows, or
     fp32 K-slice slabs [S, M, N] (their sum is the product; consumers sum them in their prologue or
@@ -669,7 +677,8 @@ def stream_gemm(x, w, splits=1, epilogue=EPI_NONE, residual=None, out=None, nt=F
         ldo = out.stride(0)
     native().stream_gemm(ptr(x), x.stride(0), ptr(w), w.stride(0), ptr(out), ldo, ptr(residual),
                          residual.stride(0) if residual is not None else 0, M, N, K, splits, int(epilogue), stream(x),
-                         int(bool(nt)), int(cfg), float(norm_eps), int(splits > 1 and out.dtype == torch.bfloat16))
+                         int(bool(nt)), int(cfg), float(norm_eps), int(splits > 1 and out.dtype == torch.bfloat16),
+                         int(w_group))
     return out
 
 

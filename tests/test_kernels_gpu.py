@@ -538,6 +538,62 @@ def test_bf16_split_k_slabs_and_their_consumers(cfg, M, S):
     assert torch.equal(q16, q32) and torch.equal(caches[0], caches[2]) and torch.equal(caches[1], caches[3])
 
 
+@pytest.mark.parametrize("cfg,M,N,K,S,epi", [(10, 128, 4096, 4096, 8, "none"), (20, 128, 2688, 1024, 1, "swiglu8"),
+                                              (20, 100, 28672 // 8, 1024, 1, "swiglu8"), (13, 64, 1792, 2048, 8, "none"),
+                                              (30, 5, 1792, 2048, 4, "none"), (30, 16, 2688, 1024, 1, "swiglu8"),
+                                              (27, 200, 1792, 2048, 8, "none")])
+def test_stream_gemm_grouped_weight_layout(cfg, M, N, K, S, epi):
+    """``shuffle_weights(w, G)`` (the G row blocks of a 16 G-row group adjacent per 32-deep k chunk)
+    read with ``w_group=G``: the same fragments in a different order, so the output is bit-identical
+    to the plain layout's (G = 8, the model's gate_up copy, and G = 7, one per compute wave)."""
+    x, w = bf(M, K), bf(N, K, scale=0.05)
+    kw = dict(cfg=cfg, nt=True, slab_dtype=torch.bfloat16)
+    if epi == "swiglu8":
+        kw["epilogue"] = ops.EPI_SWIGLU8
+    else:
+        kw["splits"] = S
+    base = ops.stream_gemm(x, ops.shuffle_weights(w), **kw)
+    ran = 0
+    for G in (7, 8):
+        if N % (16 * G):
+            continue
+        wg = ops.shuffle_weights(w, G)
+        assert torch.equal(ops.unshuffle_weights(wg, G), w)
+        assert torch.equal(ops.stream_gemm(x, wg, w_group=G, **kw), base), G
+        ran += 1
+    assert ran
+    if epi == "none":
+        close(base.float().sum(0), ref.gemm_bt(x, w, out_f32=True), atol=3e-2, rtol=2e-2)
+    if N % 112:
+        with pytest.raises(Exception):  # N not a whole number of 7-block groups: refused, not misread
+            ops.stream_gemm(x, ops.shuffle_weights(w), w_group=7, **kw)
+
+
+@pytest.mark.parametrize("M,N,K,path", [(77, 1152, 512, "bt"), (3000, 1152, 768, "bt"), (384, 28672, 4096, "mid"),
+                                        (700, 1024, 512, "mid"), (1100, 512, 4096, "256"), (2048, 2304, 1024, "256")])
+def test_prefill_gemms_on_the_grouped_weight_layout(M, N, K, path):
+    """The prefill GEMMs that read the model's grouped gate_up copy (``shuffle_weights(w, 8)``,
+    ``b_group=8``): gemm.hip's 128 / 256 tiles (N % 256 != 0 keeps gemm_mid / gemm256 off), gemm_mid and
+    gemm256 -- bit-identical to the same kernel on the plain fragment layout, plain and SwiGLU8."""
+    A, B = bf(M, K), bf(N, K, scale=0.05)
+    plain, grp = ops.shuffle_weights(B), ops.shuffle_weights(B, 8)
+    for epi in (ops.EPI_NONE, ops.EPI_SWIGLU8):
+        if path == "bt":
+            run = lambda w, g: ops.gemm_bt(A, w, epilogue=epi, shuffled=True, b_group=g)  # noqa: E731
+        elif path == "mid":
+            run = lambda w, g: ops.kernels.gemm_mid(A, w, epilogue=epi, b_group=g)  # noqa: E731
+        else:
+            run = lambda w, g: ops.kernels.gemm256(A, w, epilogue=epi, shuffled=True, b_group=g)  # noqa: E731
+        got = run(grp, 8)
+        assert torch.equal(got, run(plain, 1)), epi
+        if epi == ops.EPI_NONE:
+            close(got, ref.gemm_bt(A, B), atol=3e-2, rtol=2e-2)
+    if path == "bt":
+        res = bf(M, N)
+        assert torch.equal(ops.gemm_bt(A, grp, residual=res, shuffled=True, b_group=8),
+                           ops.gemm_bt(A, plain, residual=res, shuffled=True))
+
+
 @pytest.mark.parametrize("cfg,S", [(10, 8), (10, 16), (14, 8), (9, 8)])
 def test_stream_gemm_slice_per_xcd_mapping(cfg, S):
     """The A/B block mapping that groups K-slices (not tiles) per XCD (``stream_gemm_set_slice_xcd``):

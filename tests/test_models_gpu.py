@@ -81,6 +81,29 @@ def test_bf16_decode_slabs_match_fp32_slabs_and_reference(B):
     assert err < 0.15, err
 
 
+@pytest.mark.parametrize("B", [3, 128])
+def test_grouped_gate_up_layout_is_bit_identical(B):
+    """``LlamaModel.gate_up_grouped``: gate_up held as ``shuffle_weights(w, 8)`` (prefill through
+    gemm.hip / gemm_mid / gemm256, decode through stream_gemm) gives the same hidden states and logits,
+    bit for bit, as the plain fragment copy."""
+    cfg = decoder_config("tiny-llama")
+    wbf = {k: v.to(torch.bfloat16) for k, v in random_decoder_weights(cfg, dtype=torch.float32, seed=7,
+                                                                       interleave_mlp=True).items()}
+    gen = torch.Generator().manual_seed(B)
+    prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
+               for n in torch.randint(10, 250, (B,), generator=gen)]
+    out = []
+    for grouped in (False, True):
+        LlamaModel.gate_up_grouped = grouped
+        try:
+            m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+        finally:
+            LlamaModel.gate_up_grouped = True
+        assert m.gate_up_group == (8 if grouped else 1)
+        out.append(_run(m, cfg, prompts, DEV, torch.bfloat16))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("B", [4, 128])
 def test_default_path_keeps_unfolded_norm_gains(B):
     """the default GPU model does NOT fold the RMSNorm gains into the projections (one
