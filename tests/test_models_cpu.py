@@ -238,3 +238,24 @@ def test_tp_checkpoint_load_reads_only_the_rank_slices(tmp_path):
             assert st.bytes_read <= repl + proj / tp * 1.001, (tp, st.bytes_read, repl, proj)
 
 
+
+
+@pytest.mark.parametrize("group", [1, 7, 8])
+def test_grouped_fragment_layout_round_trip_and_addressing(group):
+    """``shuffle_weights(w, G)``: a permutation of the rows' 1-KB fragments -- fragment (block b, k
+    chunk c) of the plain layout sits at 1-KB slot ((b / G) K/32 + c) G + b % G, the address the
+    kernels compute (stream_gemm.hip ``wblk``, gemm_mid / gemm256 / gemm.hip ``bgrp``); the inverse
+    restores the matrix and the CPU gemm_bt fallback reads it with ``b_group``."""
+    from django_assistant_bot_amd import ops
+    N, K = 16 * group * 3, 128
+    w = torch.randn(N, K).to(torch.bfloat16)
+    plain, grp = ops.shuffle_weights(w).view(-1, 512), ops.shuffle_weights(w, group).view(-1, 512)
+    nck = K // 32
+    for b in range(N // 16):
+        for c in range(nck):
+            assert torch.equal(grp[((b // group) * nck + c) * group + b % group], plain[b * nck + c])
+    assert torch.equal(ops.unshuffle_weights(ops.shuffle_weights(w, group), group), w)
+    if group == 8:
+        x = torch.randn(5, K).to(torch.bfloat16)
+        assert torch.equal(ops.gemm_bt(x, ops.shuffle_weights(w, 8), shuffled=True, b_group=8),
+                           ops.gemm_bt(x, w))
