@@ -88,8 +88,11 @@ ARMS = {
     "down16": {"down": (10, 16)},
     "o4b": {"o": (10, 4)},
     "slab32": {"_slab16": False},
-    # gate_up in the plain fragment layout instead of the grouped one (shuffle_weights(w, 8))
-    "gu_g1": {"_gu_group": 1},
+    # projection copies in the plain / grouped fragment layout (shuffle_weights(w, G), LlamaModel.PROJ_GROUPS)
+    "gu_g1": {"_groups": {"gate_up": 1}},
+    "all_g8": {"_groups": {"qkv": 8, "o": 8, "down": 8}},
+    "down_g8": {"_groups": {"down": 8}},
+    "qkvo_g8": {"_groups": {"qkv": 8, "o": 8}},
 }
 
 
@@ -143,7 +146,7 @@ def main():
             eng.step()
 
     base_part, base_spart = eng.long_part_size, eng.part_size
-    base_group = eng.model.gate_up_group
+    base_groups = dict(eng.model.proj_group)
     arms = args.arms.split(",")
     res = {a: [] for a in arms}
     for r in range(args.rounds):
@@ -166,7 +169,8 @@ def main():
             eng.model.STREAM_CFG_RES16 = spec.get("_res_cfg", type(eng.model).STREAM_CFG_RES16)
             ops.native().stream_gemm_set_slice_xcd(spec.get("_slice_xcd", 0))
             eng.model.slab_bf16 = spec.get("_slab16", type(eng.model).slab_bf16)
-            eng.model.set_gate_up_group(spec.get("_gu_group", base_group))
+            for n, g in {**base_groups, **spec.get("_groups", {})}.items():
+                eng.model.set_proj_group(n, g)
             eng._graphs.clear()
             for _ in range(4):
                 eng.step()

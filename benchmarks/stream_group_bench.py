@@ -43,15 +43,15 @@ def main():
     N, K = 28672, 4096
     w = (torch.randn(N, K, device="cuda") * 0.02).to(torch.bfloat16)
     plain, grp = ops.shuffle_weights(w), ops.shuffle_weights(w, 8)
-    for M in (512, 2048, 8192, 32768):
-        x = (torch.randn(M, K, device="cuda") * 0.5).to(torch.bfloat16)
-        res = {"op": "gate_up_prefill", "M": M}
+    for Mp in (512, 2048, 8192, 32768):
+        x = (torch.randn(Mp, K, device="cuda") * 0.5).to(torch.bfloat16)
+        res = {"op": "gate_up_prefill", "M": Mp}
         y1 = ops.gemm_bt(x, plain, epilogue=ops.EPI_SWIGLU8, shuffled=True)
-        assert torch.equal(ops.gemm_bt(x, grp, epilogue=ops.EPI_SWIGLU8, shuffled=True, b_group=8), y1), M
+        assert torch.equal(ops.gemm_bt(x, grp, epilogue=ops.EPI_SWIGLU8, shuffled=True, b_group=8), y1), Mp
         for G, wk in ((1, plain), (8, grp)):
             t = graph_time([lambda: ops.gemm_bt(x, wk, epilogue=ops.EPI_SWIGLU8, shuffled=True, b_group=G)])
             res[f"g{G}_us"] = round(t * 1e6, 1)
-            res[f"g{G}_tflops"] = round(2 * M * N * K / t / 1e12, 1)
+            res[f"g{G}_tflops"] = round(2 * Mp * N * K / t / 1e12, 1)
         print(json.dumps(res), flush=True)
 
 

@@ -130,9 +130,17 @@ class LlamaModel:
         self.frag = fragment_layout and self.device.type == "cuda" and self._fragment_ok(weights)
         take = weights.pop if consume else weights.__getitem__
 
-        def proj(key):
-            t = take(key).to(self.device)
-            return ops.shuffle_weights(t) if self.frag else t
+        self.proj_group = {}
+
+        def fmt(name, t):
+            """The decoder's one copy of projection ``name``: the fragment layout, grouped per
+            ``PROJ_GROUPS`` where the shape allows (layer 0 decides for every layer)."""
+            if not self.frag:
+                return t
+            if name not in self.proj_group:
+                g = self.PROJ_GROUPS.get(name, 1)
+                self.proj_group[name] = g if (t.shape[0] % (16 * g) == 0 and t.numel() * 2 < (1 << 31)) else 1
+            return ops.shuffle_weights(t, self.proj_group[name])
 
         self.embed = take("embed").to(self.device)
         self.final_norm = take("final_norm").to(self.device)
@@ -162,12 +170,10 @@ class LlamaModel:
             if self.fold_norms:
                 qkv_w, an = self._fold(qkv_w, an), torch.ones_like(an)
                 gu_w, mn = self._fold(gu_w, mn), torch.ones_like(mn)
-            fmt = ops.shuffle_weights if self.frag else (lambda t: t)
-            if i == 0:
-                self.gate_up_group = 8 if (self.frag and self.gate_up_grouped and gu_w.shape[0] % 128 == 0
-                                           and gu_w.numel() * 2 < (1 << 31)) else 1
-            gu = ops.shuffle_weights(gu_w, self.gate_up_group) if self.frag else gu_w
-            self.layers.append(DecoderLayer(an, fmt(qkv_w), proj(f"l{i}.o_w"), mn, gu, proj(f"l{i}.down_w")))
+            o_w, down_w = take(f"l{i}.o_w").to(self.device), take(f"l{i}.down_w").to(self.device)
+            self.layers.append(DecoderLayer(an, fmt("qkv", qkv_w), fmt("o", o_w), mn, fmt("gate_up", gu_w),
+                                            fmt("down", down_w)))
+            del o_w, down_w
             del qkv_w, gu_w
         if self.frag and consume:
             torch.cuda.empty_cache()
@@ -201,14 +207,19 @@ class LlamaModel:
         dist.all_gather(parts, src, group=self.tp_group)
         return torch.cat(parts, 1).to(local.device)
 
-    def set_gate_up_group(self, group: int) -> None:
-        """Re-lay every layer's gate_up copy as ``shuffle_weights(w, group)``, in place (captured
-        graphs keep their pointers but bake the group in: re-capture after a change).  A/B harness."""
-        if not self.frag or group == self.gate_up_group:
+    def set_proj_group(self, name: str, group: int) -> None:
+        """Re-lay every layer's copy of projection ``name`` (qkv / o / gate_up / down) as
+        ``shuffle_weights(w, group)``, in place (captured graphs keep their pointers but bake the group
+        in: re-capture after a change).  A/B harness."""
+        old = self.proj_group.get(name, 1)
+        if not self.frag or group == old:
             return
         for L in self.layers:
-            L.gate_up_w.copy_(ops.shuffle_weights(ops.unshuffle_weights(L.gate_up_w, self.gate_up_group), group))
-        self.gate_up_group = group
+            w = getattr(L, name + "_w")
+            if w.shape[0] % (16 * group):
+                raise ValueError(f"{name}: {w.shape[0]} rows are not whole groups of {group}")
+            w.copy_(ops.shuffle_weights(ops.unshuffle_weights(w, old), group))
+        self.proj_group[name] = group
 
     def _fragment_ok(self, weights: dict) -> bool:
         keys = ["lm_head" if "lm_head" in weights else "embed"] + [
@@ -282,12 +293,11 @@ class LlamaModel:
             return -1, 1
         return cfg, self._stream_splits(N, K, ops.native().stream_gemm_bn(cfg))
 
-    # gate_up in the grouped fragment layout (shuffle_weights(w, 8): the 8 row blocks of each 128-row
-    # group adjacent per 32-deep k chunk): the decode GEMM's 7 compute waves (one block each) then
-    # stream neighbouring bytes -- gate_up at batch 128 51.9 -> 47.9 us cold
-    # (profiles/decode_stream_layout_r6.md); every GEMM reading the copy takes the group size
-    gate_up_grouped = True
-    gate_up_group = 1
+    # Projections held in the grouped fragment layout (shuffle_weights(w, G): the G row blocks of
+    # each 16 G-row group adjacent per 32-deep k chunk), so the decode GEMM's waves (one block each)
+    # stream neighbouring bytes; every GEMM reading a copy takes its group (``proj_group``).  gate_up
+    # at 8: batch-128 decode step 7.31 -> 7.23 ms (profiles/decode_stream_layout_r6.md)
+    PROJ_GROUPS = {"gate_up": 8}
 
     # Split-K slabs of the decode projections as bf16 (the partial sums rounded once, as the TP path
     # hands them to its all-reduce) instead of fp32: half the bytes the producer writes and the
@@ -306,7 +316,7 @@ class LlamaModel:
                 y = ops.linear(x, w)
                 return ops.silu_mul(y, group=8 if self.interleaved_mlp else 0)
             return ops.linear(x, w)
-        grp = self.gate_up_group if name == "gate_up" else 1
+        grp = self.proj_group.get(name, 1)
         if dec and self.frag:
             cfg, s = self._stream_choice(name, x.shape[0], w.shape[0], w.shape[1])
             if cfg >= 0:
@@ -353,15 +363,18 @@ class LlamaModel:
         cfg, D = self.cfg, self.cfg.head_dim
         T = h.shape[0]
         c, s = self._stream_choice("qkv", T, L.qkv_w.shape[0], L.qkv_w.shape[1])
-        qkv = ops.stream_gemm(h, L.qkv_w, splits=s, cfg=c, nt=True, norm_eps=cfg.eps)
+        pg = self.proj_group
+        qkv = ops.stream_gemm(h, L.qkv_w, splits=s, cfg=c, nt=True, norm_eps=cfg.eps, w_group=pg.get("qkv", 1))
         q = ops.rope_kv_write(qkv, meta.positions, self.cos_sin, kv.k[li], kv.v[li], meta.slots, self.hq, self.hkv, D)
         a = ops.paged_decode(q, kv.k[li], kv.v[li], meta.block_tables, meta.ctx_lens, meta.part_size,
                              meta.workspace, order=meta.order)
-        h1 = ops.stream_gemm(a.view(T, self.hq * D), L.o_w, residual=h, cfg=self.STREAM_CFG_RES16, nt=True)
+        h1 = ops.stream_gemm(a.view(T, self.hq * D), L.o_w, residual=h, cfg=self.STREAM_CFG_RES16, nt=True,
+                             w_group=pg.get("o", 1))
         gc, _ = self._stream_choice("gate_up", T, L.gate_up_w.shape[0], L.gate_up_w.shape[1])
         act = ops.stream_gemm(h1, L.gate_up_w, epilogue=ops.EPI_SWIGLU8, cfg=gc, nt=True, norm_eps=cfg.eps,
-                              w_group=self.gate_up_group)
-        return ops.stream_gemm(act, L.down_w, residual=h1, cfg=self.STREAM_CFG_RES16, nt=True)
+                              w_group=pg.get("gate_up", 1))
+        return ops.stream_gemm(act, L.down_w, residual=h1, cfg=self.STREAM_CFG_RES16, nt=True,
+                               w_group=pg.get("down", 1))
 
     # Small decode batches: the paged attention is a chain of dependent memory round trips on a few
     # dozen CUs (~15 us per layer at batch 1 while HBM idles).  ``l3_warm_mb`` > 0 appends
@@ -450,7 +463,8 @@ class LlamaModel:
         """o projection, MLP norm, gate_up (+SwiGLU), down: -> (next layer input, residual stream)."""
         cfg = self.cfg
         if fuse:
-            residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual, shuffled=self.frag)
+            residual = ops.gemm_bt(a.view(T, self.hq * D), L.o_w, residual=residual, shuffled=self.frag,
+                                   b_group=self.proj_group.get("o", 1))
             h, _ = ops.rmsnorm(residual, L.mlp_norm, cfg.eps)
         elif sk and self.tp_size > 1:
             # TP decode: the o partial (split-K slabs) meets its all-reduce inside the MLP norm's launch
@@ -465,7 +479,8 @@ class LlamaModel:
         if h.is_cuda and epi == ops.EPI_NONE:
             act = ops.silu_mul(act)
         if fuse:
-            return None, ops.gemm_bt(act, L.down_w, residual=residual, shuffled=self.frag)
+            return None, ops.gemm_bt(act, L.down_w, residual=residual, shuffled=self.frag,
+                                     b_group=self.proj_group.get("down", 1))
         if sk and self.tp_size > 1:  # reduced inside the next layer's (or the final) norm launch
             return self._tp_partial(self._proj(act, L.down_w, sk, True, name="down"), cfg.hidden), residual
         x = self._all_reduce(self._proj(act, L.down_w, sk, slabs_ok, name="down"))

@@ -83,9 +83,9 @@ def test_bf16_decode_slabs_match_fp32_slabs_and_reference(B):
 
 @pytest.mark.parametrize("B", [3, 128])
 def test_grouped_gate_up_layout_is_bit_identical(B):
-    """``LlamaModel.gate_up_grouped``: gate_up held as ``shuffle_weights(w, 8)`` (prefill through
-    gemm.hip / gemm_mid / gemm256, decode through stream_gemm) gives the same hidden states and logits,
-    bit for bit, as the plain fragment copy."""
+    """``LlamaModel.PROJ_GROUPS``: projections held as ``shuffle_weights(w, 8)`` (prefill through
+    gemm.hip / gemm_mid / gemm256, decode through stream_gemm) give the same hidden states and logits,
+    bit for bit, as the plain fragment copies; ``set_proj_group`` re-lays a copy in place."""
     cfg = decoder_config("tiny-llama")
     wbf = {k: v.to(torch.bfloat16) for k, v in random_decoder_weights(cfg, dtype=torch.float32, seed=7,
                                                                        interleave_mlp=True).items()}
@@ -93,15 +93,29 @@ def test_grouped_gate_up_layout_is_bit_identical(B):
     prompts = [torch.randint(0, cfg.vocab_size, (int(n),), generator=gen).tolist()
                for n in torch.randint(10, 250, (B,), generator=gen)]
     out = []
-    for grouped in (False, True):
-        LlamaModel.gate_up_grouped = grouped
+    default = LlamaModel.PROJ_GROUPS
+    for groups in ({}, default, {"qkv": 8, "o": 8, "gate_up": 8, "down": 8}):
+        LlamaModel.PROJ_GROUPS = groups
         try:
             m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
         finally:
-            LlamaModel.gate_up_grouped = True
-        assert m.gate_up_group == (8 if grouped else 1)
+            LlamaModel.PROJ_GROUPS = default
+        assert all(m.proj_group[n] == groups.get(n, 1) for n in ("qkv", "o", "gate_up", "down"))
         out.append(_run(m, cfg, prompts, DEV, torch.bfloat16))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+        if groups:
+            assert torch.equal(out[0][0], out[-1][0]) and torch.equal(out[0][1], out[-1][1]), groups
+    m.set_proj_group("qkv", 1)  # re-laid in place: the same bits again
+    assert torch.equal(_run(m, cfg, prompts, DEV, torch.bfloat16)[1], out[0][1])
+    if B <= 16:  # the small-batch path (consumer RMSNorm, residual producers) on grouped copies
+        fused = []
+        for groups in ({}, {"qkv": 8, "o": 8, "gate_up": 8, "down": 8}):
+            LlamaModel.PROJ_GROUPS = groups
+            try:
+                m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True, small_norm_fused=True)
+            finally:
+                LlamaModel.PROJ_GROUPS = default
+            fused.append(_run(m, cfg, prompts, DEV, torch.bfloat16))
+        assert torch.equal(fused[0][0], fused[1][0]) and torch.equal(fused[0][1], fused[1][1])
 
 
 @pytest.mark.parametrize("B", [4, 128])
