@@ -93,6 +93,8 @@ ARMS = {
     "all_g8": {"_groups": {"qkv": 8, "o": 8, "down": 8}},
     "down_g8": {"_groups": {"down": 8}},
     "qkvo_g8": {"_groups": {"qkv": 8, "o": 8}},
+    "gu41": {"gate_up": (41, 1)},
+    "gu42": {"gate_up": (42, 1)},
 }
 
 

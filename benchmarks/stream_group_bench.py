@@ -13,7 +13,9 @@ from benchmarks.kernel_bench import graph_time  # noqa: E402
 from django_assistant_bot_amd import ops  # noqa: E402
 
 M = 128
-SHAPES = (("gate_up", 28672, 4096, 20, 1, ops.EPI_SWIGLU8), ("qkv", 6144, 4096, 10, 4, ops.EPI_NONE),
+SHAPES = (("gate_up", 28672, 4096, 20, 1, ops.EPI_SWIGLU8), ("gate_up", 28672, 4096, 22, 1, ops.EPI_SWIGLU8),
+          ("gate_up", 28672, 4096, 41, 1, ops.EPI_SWIGLU8), ("gate_up", 28672, 4096, 42, 1, ops.EPI_SWIGLU8),
+          ("qkv", 6144, 4096, 10, 4, ops.EPI_NONE),
           ("o", 4096, 4096, 10, 8, ops.EPI_NONE), ("down", 4096, 14336, 10, 8, ops.EPI_NONE))
 
 
@@ -25,7 +27,7 @@ def main():
         res = {"op": name, "M": M, "N": N, "K": K, "cfg": cfg, "S": S}
         kw = dict(splits=S, cfg=cfg, nt=True, epilogue=epi, slab_dtype=torch.bfloat16)
         base = None
-        for G in (1, 7, 8):
+        for G in (1, 7, 8) if cfg == 20 else (1, 8):
             if N % (16 * G):
                 continue
             wl = [ops.shuffle_weights(w, G) for w in ws]

@@ -489,6 +489,9 @@ static constexpr StreamCfg kStreamCfgs[] = {
     {8, 2, 1, 4, 3, 4, true, 4},     // 38: = 10 without the slab stores (ablation, wrong results)
     {8, 2, 1, 4, 3, 4, true, 5},     // 39: = 10 reading a tile-interleaved layout (ablation, wrong results)
     {8, 1, 1, 4, 4, 2, true, 5, 7},  // 40: = 20 reading a tile-interleaved layout (ablation, wrong results)
+    // gate_up on the grouped copy (shuffle_weights(w, 8)): = 20 with deeper weight rings
+    {8, 1, 1, 4, 6, 2, true, 0, 7},  // 41: 6-stage weight ring
+    {8, 1, 1, 3, 8, 1, true, 0, 7},  // 42: 8-stage weight ring, 1 loader wave
 };
 constexpr int kNumStreamCfgs = sizeof(kStreamCfgs) / sizeof(kStreamCfgs[0]);
 

@@ -541,7 +541,8 @@ def test_bf16_split_k_slabs_and_their_consumers(cfg, M, S):
 @pytest.mark.parametrize("cfg,M,N,K,S,epi", [(10, 128, 4096, 4096, 8, "none"), (20, 128, 2688, 1024, 1, "swiglu8"),
                                               (20, 100, 28672 // 8, 1024, 1, "swiglu8"), (13, 64, 1792, 2048, 8, "none"),
                                               (30, 5, 1792, 2048, 4, "none"), (30, 16, 2688, 1024, 1, "swiglu8"),
-                                              (27, 200, 1792, 2048, 8, "none")])
+                                              (27, 200, 1792, 2048, 8, "none"), (41, 128, 2688, 1024, 1, "swiglu8"),
+                                              (42, 77, 2688, 1024, 1, "swiglu8"), (41, 128, 1792, 2048, 4, "none")])
 def test_stream_gemm_grouped_weight_layout(cfg, M, N, K, S, epi):
     """``shuffle_weights(w, G)`` (the G row blocks of a 16 G-row group adjacent per 32-deep k chunk)
     read with ``w_group=G``: the same fragments in a different order, so the output is bit-identical
@@ -663,7 +664,8 @@ def test_stream_swiglu_and_strided_x(cfg, M):
     close(got, exp, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([10, 13, 20, 21, 22, 23, 30, 31], [5, 30, 64, 128])])
+@pytest.mark.parametrize("cfg,M", [c[:2] for c in _stream_cases([10, 13, 20, 21, 22, 23, 30, 31, 41, 42],
+                                                                 [5, 30, 64, 128])])
 def test_stream_swiglu8(cfg, M):
     """8-row [gate | up] groups (EPI_SWIGLU8, the decode copy of gate_up): BN 96 / 112 / 128 tiles."""
     F, K = 1344, 1024
