@@ -1,0 +1,89 @@
+"""Prefill attention at the headline's prefill-step shape: ~30 prompts of 989-1189 tokens (1089 mean,
+the bench's RAG prompts) packed into one 32k-token step, causal, q read from the strided qkv
+projection with RoPE on load (the model's call, models/llama.py _layer prefill path).  Against
+uniform 1024-token sequences, so the loss from ragged lengths (partial 128-row query blocks) is
+visible.  One JSON line per case: us, exact causal TF/s."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from benchmarks.kernel_bench import timeit  # noqa: E402
+from django_assistant_bot_amd import ops  # noqa: E402
+
+Hq, Hkv, D, bs = 32, 8, 128, 64
+
+
+def case(name, lens):
+    B = len(lens)
+    T = int(sum(lens))
+    nbl = [-(-n // bs) for n in lens]
+    nb = sum(nbl)
+    kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
+    vc = torch.randn_like(kc)
+    bt = torch.zeros((B, max(nbl)), dtype=torch.int32)
+    o = 0
+    for i, n in enumerate(nbl):
+        bt[i, :n] = torch.arange(o, o + n, dtype=torch.int32)
+        o += n
+    bt = bt.cuda()
+    cu = torch.zeros(B + 1, dtype=torch.int32)
+    cu[1:] = torch.cumsum(torch.tensor(lens), 0)
+    cu = cu.cuda()
+    ctx = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
+    q = qkv[:, :Hq * D].view(T, Hq, D)
+    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).cuda()
+    cs = ops.reference.rope_cos_sin(ops.reference.llama3_inv_freq(D, 500000.0, None), 8192).cuda()
+    mx = int(max(lens))
+    flop = sum(4.0 * Hq * D * n * (n + 1) / 2 for n in lens)
+    res = {"case": name, "seqs": B, "tokens": T}
+    times = {a: [] for a in ARMS}
+    base = None
+    for _ in range(ROUNDS):  # interleaved rounds: no arm is always the first one timed
+        for arm, env in ARMS.items():
+            for k in ("DAB_FLASH_G", "DAB_FLASH_PAIR", "DAB_FLASH_LPT"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            run = lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctx, mx, causal=True, rope=(pos, cs))  # noqa: E731
+            out = run()
+            if base is None:
+                base = out
+            else:
+                assert torch.equal(out, base), arm
+            times[arm].append(timeit(run))
+    for k in ("DAB_FLASH_G", "DAB_FLASH_PAIR", "DAB_FLASH_LPT"):
+        os.environ.pop(k, None)
+    for arm, ts in times.items():
+        t = sorted(ts)[len(ts) // 2]
+        res[f"{arm}_us"] = round(t * 1e6, 1)
+        res[f"{arm}_tflops"] = round(flop / t / 1e12, 1)
+    print(json.dumps(res), flush=True)
+
+
+# default = heaviest-first walk with the fill-based G; "fifo" = the round-5 alternating walk with the
+# same G; gN = heaviest-first with G forced to N
+ARMS = {"default": {}, "fifo": {"DAB_FLASH_LPT": "0"}, "g1": {"DAB_FLASH_G": "1"}, "g2": {"DAB_FLASH_G": "2"},
+        "g4": {"DAB_FLASH_G": "4"}, "nopair": {"DAB_FLASH_PAIR": "0"}}
+ROUNDS = 3
+
+
+def main():
+    g = torch.Generator().manual_seed(0)
+    case("uniform-16x1024", [1024] * 16)
+    case("uniform-32x1024", [1024] * 32)
+    case("uniform-30x1088", [1088] * 30)
+    case("uniform-30x1089", [1089] * 30)
+    case("uniform-30x1152", [1152] * 30)
+    case("uniform-8x4096", [4096] * 8)
+    case("uniform-2x8192", [8192] * 2)
+    case("uniform-4x300", [300] * 4)
+    lens = torch.randint(989, 1190, (30,), generator=g).tolist()
+    case("ragged-30x989..1189", lens)
+    case("ragged-sorted", sorted(lens, reverse=True))
+
+
+if __name__ == "__main__":
+    main()

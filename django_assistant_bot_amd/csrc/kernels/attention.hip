@@ -61,6 +61,9 @@ struct FlashParams {
   const int* rope_pos;
   const float2* rope_cs;
   int pairs_per_wg;  // flash_d128 PAIR: causal query-block pairs walked by one workgroup (>= 1)
+  // flash_d128 PAIR: heaviest-first walk -- each XCD runs the first pair group (the longest blocks)
+  // of all its (sequence, head) units before any later group (lighter), instead of alternating
+  int lpt;
 };
 
 // One workgroup = 16 QT NW queries (NW waves x QT 16-query sub-tiles) of one (sequence, head);
@@ -435,7 +438,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void flash_d128_kernel(Fl
   const int nwg = nqb * gridDim.y * gridDim.z;
   const int lin = blockIdx.x + nqb * (blockIdx.y + gridDim.y * blockIdx.z);
   const int xcd = lin % 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+  int sid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + lin / 8;
+  if (PAIR && p.lpt) {
+    // the (sequence, head) units split evenly over the XCDs (units % 8 == 0, checked by the host);
+    // on each XCD, pair group 0 of every unit, then group 1, ...: the mixed-duration workgroups of
+    // a ragged pair split no longer alternate, so greedy dispatch cannot strand a long one at the end
+    const int nu = gridDim.y * gridDim.z / 8, k = lin / 8;
+    sid = (xcd * nu + k % nu) * nqb + k / nu;
+  }
   const int h = (sid / nqb) % gridDim.y;
   const int b = sid / (nqb * gridDim.y);
   // the sequence's block ids are requested first: they depend on b alone, so their round trip runs
@@ -1837,7 +1847,7 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
                     const int* rope_pos, const void* rope_cs) {
   if (batch <= 0 || max_seqlen_q <= 0) return 0;
   if (Hq % Hkv || (paged && block_size % 64)) return hipErrorInvalidValue;
-  FlashParams prm;
+  FlashParams prm{};
   prm.rope_pos = rope_pos;
   prm.rope_cs = (const float2*)rope_cs;
   prm.q = (const bf16*)q;
@@ -1893,14 +1903,20 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     const char* pe = std::getenv("DAB_FLASH_PAIR");
     if (causal && vpipe && !(pe && pe[0] == '0')) {
       // G pairs per workgroup: enough workgroups for ~2 rounds of the chip's 512 slots (2 per CU),
-      // fewer start-ups beyond that; DAB_FLASH_G overrides (A/B)
+      // fewer start-ups beyond that.  The workgroups are walked heaviest-first (lpt): the groups of
+      // a (sequence, head) differ in work whenever G does not divide its pair count (9 query blocks
+      // = 5 pairs at G = 4), and greedy dispatch of alternating long / short workgroups stranded
+      // long ones at the end -- the headline's ~1.1k-token prompts ran at 350 TF/s on the
+      // alternating walk, ~575 TF/s on this one (profiles/attn_prefill_shape_r6.md).
+      // DAB_FLASH_G / DAB_FLASH_LPT=0 override (A/B)
       const int npairs = ((max_seqlen_q + 127) / 128 + 1) / 2;
-      const long wg1 = (long)npairs * Hq * batch;
-      int G = (int)(wg1 / 1024);
+      int G = (int)((long)npairs * Hq * batch / 1024);
       if (const char* ge = std::getenv("DAB_FLASH_G")) G = std::atoi(ge);
       G = G < 1 ? 1 : (G > npairs ? npairs : G);
       prm.pairs_per_wg = G;
       dim3 gp((npairs + G - 1) / G, Hq, batch);
+      const char* lp = std::getenv("DAB_FLASH_LPT");
+      prm.lpt = !(lp && lp[0] == '0') && ((long)Hq * batch) % 8 == 0;
       const char* ob = std::getenv("DAB_FLASH_1BAR");  // A/B: one barrier per tile
       const char* sm = std::getenv("DAB_FLASH_SMS");   // A/B: softmax split across the PV k-steps
       const char* sg = std::getenv("DAB_FLASH_SGB");   // A/B: sched_group_barrier S^T interleave

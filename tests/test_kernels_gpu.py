@@ -1178,7 +1178,7 @@ def test_paged_decode_l3_warm_leaves_the_output_unchanged(B, blocks):
 @pytest.mark.parametrize("env,val", [("DAB_ENC_W5", "1"), ("DAB_FLASH_W8", "1"), ("DAB_FLASH_W8", "2"),
                                      ("DAB_FLASH_PAIR", "0"), ("DAB_FLASH_G", "3"), ("DAB_FLASH_1BAR", "1"),
                                      ("DAB_FLASH_Q64", "1"), ("DAB_ENC_PERSIST", "1"), ("DAB_FLASH_SMS", "1"),
-                                     ("DAB_FLASH_SGB", "1")])
+                                     ("DAB_FLASH_SGB", "1"), ("DAB_FLASH_LPT", "0"), ("DAB_FLASH_G", "5")])
 def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
     """Occupancy / pipeline variants of the attention kernels selected per launch by environment
     switch (the A/B arms of benchmarks/kernel_bench.py attn) produce the default kernel's output:
@@ -1207,8 +1207,9 @@ def test_attention_variants_match_the_default_kernel(env, val, monkeypatch):
         cu, ctxt = cu.to(DEV), torch.tensor(ctx, dtype=torch.int32, device=DEV)
         run = lambda: ops.flash_attention_paged(q, kc, vc, bt, cu, ctxt, max(ctx), causal=True)  # noqa: E731
         exp = None
-    # (PAIR is the default: its arm turns it off; DAB_FLASH_G=3 walks 3 pairs per workgroup against 1)
-    monkeypatch.setenv(env, {"0": "1", "3": "1"}.get(val, "0"))
+    # (PAIR and the heaviest-first walk are the default: their arms turn them off; DAB_FLASH_G=3 / 5
+    # walk 3 / 5 pairs per workgroup against 1)
+    monkeypatch.setenv(env, {"0": "1", "3": "1", "5": "1"}.get(val, "0"))
     base = run()
     monkeypatch.setenv(env, val)
     out = run()
