@@ -16,29 +16,36 @@ from django_assistant_bot_amd import ops  # noqa: E402
 Hq, Hkv, D, bs = 32, 8, 128, 64
 
 
-def case(name, lens):
+def case(name, lens, prefix=0, pool_blocks=0):
+    """lens: query tokens per sequence; prefix: cached tokens before them (the prompt's system block
+    comes from the prefix cache, so the engine's queries start at position 64)."""
     B = len(lens)
+    ctx_l = [n + prefix for n in lens]
     T = int(sum(lens))
-    nbl = [-(-n // bs) for n in lens]
-    nb = sum(nbl)
+    nbl = [-(-n // bs) for n in ctx_l]
+    nb = max(sum(nbl), pool_blocks)
     kc = torch.randn(nb, Hkv, bs, D, device="cuda").to(torch.bfloat16)
     vc = torch.randn_like(kc)
     bt = torch.zeros((B, max(nbl)), dtype=torch.int32)
+    # pool_blocks: the blocks scattered at random over a pool that large (the engine's per-layer KV
+    # pool after many batches), else packed in order
+    ids = torch.randperm(nb, generator=torch.Generator().manual_seed(1)).to(torch.int32) if pool_blocks else \
+        torch.arange(nb, dtype=torch.int32)
     o = 0
     for i, n in enumerate(nbl):
-        bt[i, :n] = torch.arange(o, o + n, dtype=torch.int32)
+        bt[i, :n] = ids[o:o + n]
         o += n
     bt = bt.cuda()
     cu = torch.zeros(B + 1, dtype=torch.int32)
     cu[1:] = torch.cumsum(torch.tensor(lens), 0)
     cu = cu.cuda()
-    ctx = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    ctx = torch.tensor(ctx_l, dtype=torch.int32, device="cuda")
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device="cuda").to(torch.bfloat16)
     q = qkv[:, :Hq * D].view(T, Hq, D)
-    pos = torch.cat([torch.arange(n, dtype=torch.int32) for n in lens]).cuda()
+    pos = torch.cat([torch.arange(prefix, prefix + n, dtype=torch.int32) for n in lens]).cuda()
     cs = ops.reference.rope_cos_sin(ops.reference.llama3_inv_freq(D, 500000.0, None), 8192).cuda()
     mx = int(max(lens))
-    flop = sum(4.0 * Hq * D * n * (n + 1) / 2 for n in lens)
+    flop = sum(4.0 * Hq * D * n * ((n + 1) / 2 + prefix) for n in lens)
     res = {"case": name, "seqs": B, "tokens": T}
     times = {a: [] for a in ARMS}
     base = None
@@ -72,17 +79,19 @@ ROUNDS = 3
 
 def main():
     g = torch.Generator().manual_seed(0)
-    case("uniform-16x1024", [1024] * 16)
     case("uniform-32x1024", [1024] * 32)
-    case("uniform-30x1088", [1088] * 30)
-    case("uniform-30x1089", [1089] * 30)
-    case("uniform-30x1152", [1152] * 30)
-    case("uniform-8x4096", [4096] * 8)
-    case("uniform-2x8192", [8192] * 2)
-    case("uniform-4x300", [300] * 4)
+    # the engine's headline prefill step: 1089 +- 100-token prompts minus the 64-token cached system
+    # block, packed up to 32,768 query tokens; and the classify fast step (774-token prompts)
+    real, tot = [], 0
+    while tot < 32768:
+        n = min(int(torch.randint(989, 1190, (1,), generator=g)) - 64, 32768 - tot)
+        real.append(n)
+        tot += n
+    case("engine-step", real, prefix=64)
+    case("engine-step-scattered", real, prefix=64, pool_blocks=12000)
+    case("engine-classify", [710] * 46, prefix=64)
     lens = torch.randint(989, 1190, (30,), generator=g).tolist()
     case("ragged-30x989..1189", lens)
-    case("ragged-sorted", sorted(lens, reverse=True))
 
 
 if __name__ == "__main__":
