@@ -49,8 +49,12 @@ def case(name, lens, prefix=0, pool_blocks=0):
     res = {"case": name, "seqs": B, "tokens": T}
     times = {a: [] for a in ARMS}
     base = None
+    npairs = (-(-max(lens) // 128) + 1) // 2
+    g_r5 = max(1, min(npairs, npairs * Hq * B // 1024))
     for _ in range(ROUNDS):  # interleaved rounds: no arm is always the first one timed
         for arm, env in ARMS.items():
+            if env is None:
+                env = {"DAB_FLASH_LPT": "0", "DAB_FLASH_G": str(g_r5)}
             for k in ("DAB_FLASH_G", "DAB_FLASH_PAIR", "DAB_FLASH_LPT"):
                 os.environ.pop(k, None)
             os.environ.update(env)
@@ -70,9 +74,10 @@ def case(name, lens, prefix=0, pool_blocks=0):
     print(json.dumps(res), flush=True)
 
 
-# default = heaviest-first walk with the fill-based G; "fifo" = the round-5 alternating walk with the
-# same G; gN = heaviest-first with G forced to N
-ARMS = {"default": {}, "fifo": {"DAB_FLASH_LPT": "0"}, "g1": {"DAB_FLASH_G": "1"}, "g2": {"DAB_FLASH_G": "2"},
+# default = heaviest-first walk, G = 2 (1 below 1024 workgroups); "r5" = the round-5 choice (G = pairs
+# x heads x seqs / 1024, alternating walk); "fifo" = the alternating walk with the default G; gN =
+# heaviest-first with G forced to N
+ARMS = {"default": {}, "r5": None, "fifo": {"DAB_FLASH_LPT": "0"}, "g1": {"DAB_FLASH_G": "1"}, "g2": {"DAB_FLASH_G": "2"},
         "g4": {"DAB_FLASH_G": "4"}, "nopair": {"DAB_FLASH_PAIR": "0"}}
 ROUNDS = 3
 
@@ -80,6 +85,8 @@ ROUNDS = 3
 def main():
     g = torch.Generator().manual_seed(0)
     case("uniform-32x1024", [1024] * 32)
+    case("uniform-8x4096", [4096] * 8)
+    case("uniform-4x300", [300] * 4)
     # the engine's headline prefill step: 1089 +- 100-token prompts minus the 64-token cached system
     # block, packed up to 32,768 query tokens; and the classify fast step (774-token prompts)
     real, tot = [], 0
@@ -89,6 +96,7 @@ def main():
         tot += n
     case("engine-step", real, prefix=64)
     case("engine-step-scattered", real, prefix=64, pool_blocks=12000)
+    case("engine-step-33", [990] * 33, prefix=64)  # the traced step: 33 sequences (1056 units)
     case("engine-classify", [710] * 46, prefix=64)
     lens = torch.randint(989, 1190, (30,), generator=g).tolist()
     case("ragged-30x989..1189", lens)

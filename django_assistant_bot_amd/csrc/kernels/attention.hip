@@ -1902,15 +1902,15 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
     // bit-identical: profiles/attn_vpipe_r5.md); DAB_FLASH_PAIR=0 selects one workgroup per block
     const char* pe = std::getenv("DAB_FLASH_PAIR");
     if (causal && vpipe && !(pe && pe[0] == '0')) {
-      // G pairs per workgroup: enough workgroups for ~2 rounds of the chip's 512 slots (2 per CU),
-      // fewer start-ups beyond that.  The workgroups are walked heaviest-first (lpt): the groups of
-      // a (sequence, head) differ in work whenever G does not divide its pair count (9 query blocks
-      // = 5 pairs at G = 4), and greedy dispatch of alternating long / short workgroups stranded
-      // long ones at the end -- the headline's ~1.1k-token prompts ran at 350 TF/s on the
-      // alternating walk, ~575 TF/s on this one (profiles/attn_prefill_shape_r6.md).
-      // DAB_FLASH_G / DAB_FLASH_LPT=0 override (A/B)
+      // G = 2 pairs per workgroup (1 when that leaves < 1024 workgroups), walked heaviest-first
+      // (lpt).  Large G made the workgroups few and long: the headline's prefill step (33 prompts of
+      // ~1.03k queries, G = 5 = all pairs) ran 1056 workgroups of equal work on 512 slots, i.e.
+      // three rounds where the third held 32 -- 770 us against ~520 (profiles/attn_prefill_shape_r6.md).
+      // With G < pairs the groups of a (sequence, head) differ in work (9 query blocks = 5 pairs), and
+      // dispatching them alternately stranded long ones at the end: heaviest-first walks all first
+      // groups, then all second groups.  DAB_FLASH_G / DAB_FLASH_LPT=0 override (A/B)
       const int npairs = ((max_seqlen_q + 127) / 128 + 1) / 2;
-      int G = (int)((long)npairs * Hq * batch / 1024);
+      int G = (long)npairs * Hq * batch >= 2048 ? 2 : 1;
       if (const char* ge = std::getenv("DAB_FLASH_G")) G = std::atoi(ge);
       G = G < 1 ? 1 : (G > npairs ? npairs : G);
       prm.pairs_per_wg = G;
