@@ -256,6 +256,7 @@ class LlamaModel:
     STREAM_CFG_M16, STREAM_CFG_M32, STREAM_CFG_M64, STREAM_CFG_M128, STREAM_CFG_M256 = 30, 31, 13, 10, 27
     STREAM_WIDE = {"gate_up": 20, "lm_head": 28}
     STREAM_MAX_M = ops.STREAM_MAX_M
+    PREFILL_STREAM_MAX_M = 128  # prefill steps of at most this many tokens stream too (0: off)
 
     def _stream_cfg(self, name: str, M: int, N: int) -> int:
         nat = ops.native()
@@ -334,9 +335,14 @@ class LlamaModel:
         T = ids.numel()
         x = ops.embed_gather(ids, self.embed)
         # decode-sized batches stream the weights through the split-K MFMA kernel; its fp32 slabs
-        # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction
-        sk = meta.decode and T <= self.STREAM_MAX_M and x.is_cuda
-        if sk and T <= self.SMALL_FUSED_MAX_M and self.small_norm_fused and self.fold_norms and self.tp_size == 1:
+        # are summed by the consumers (RoPE/KV write, RMSNorm) instead of a separate reduction.  So
+        # do short prefill steps (an interactive prompt, the tail of a batch): at T <= 128 the MFMA
+        # tiles read every weight for a handful of rows (qkv / o / gate_up / down 54 / 54 / 65 /
+        # 183 us against 16-21 / 15-19 / 42-49 / 27-32 streamed, profiles/small_prefill_r6.md)
+        small_pf = (not meta.decode and not meta.n_decode and T <= self.PREFILL_STREAM_MAX_M and self.frag
+                    and self.tp_size == 1)
+        sk = (meta.decode and T <= self.STREAM_MAX_M or small_pf) and x.is_cuda
+        if sk and meta.decode and T <= self.SMALL_FUSED_MAX_M and self.small_norm_fused and self.fold_norms and self.tp_size == 1:
             h = x  # the residual stream itself: no RMSNorm launches (``_layer_small``)
             for li, L in enumerate(self.layers):
                 h = self._layer_small(li, L, h, meta, kv)
@@ -438,7 +444,7 @@ class LlamaModel:
         else:
             h, residual = self._norm(x, L.attn_norm, residual)
         qkv = self._proj(h, L.qkv_w, sk, name="qkv")
-        if (not meta.decode and not meta.n_decode and qkv.is_cuda and qkv.dtype == torch.bfloat16
+        if (not meta.decode and not meta.n_decode and qkv.is_cuda and qkv.dtype == torch.bfloat16 and qkv.dim() == 2
                 and ops.kernels.flash_rope_ok(D, kv.block_size)):
             # prefill: the RoPE/KV-write kernel writes only K / V; the attention rotates Q on load
             # straight from the projection (a [T, Hq*D] write and read less per layer)

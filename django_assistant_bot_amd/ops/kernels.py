@@ -345,7 +345,11 @@ def paged_decode(q, k_cache, v_cache, block_tables, ctx_lens, part_size=512, wor
 GEMM256_MIN_M = 1024  # the phased 256x256 kernel from here on; the 128x128 kernel below
 
 
-GEMM_MID_MIN_M = 192
+# gemm_mid from the first row: at M <= 191 the 128 x 128 kernel re-reads the weights per row tile
+# and leaves most CUs idle -- Llama-3-8B qkv / o / gate_up / down at M = 129-187: 54 / 54 / 72 / 181
+# us against 31 / 29 / 67 / 47 (profiles/small_prefill_r6.md; decode-sized prefill steps of the
+# fragment-layout decoder stream instead, models/llama.py PREFILL_STREAM_MAX_M)
+GEMM_MID_MIN_M = 1
 GEMM_MID_FILL = 192  # gemm256 keeps a shape whose 256 x 256 tiles fill this many of the 256 CUs
 
 

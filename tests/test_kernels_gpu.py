@@ -321,7 +321,8 @@ def test_gemm256(M, N, K, shuffled):
 
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (300, 512, 256), (129, 768, 640), (640, 4096, 4096),
                                    (768, 6144, 4096), (1000, 1024, 14336), (4096, 512, 128), (2048, 2048, 1024),
-                                   (384, 28672, 4096)])
+                                   (384, 28672, 4096), (1, 512, 256), (37, 1024, 512), (128, 4096, 4096),
+                                   (187, 28672, 4096)])
 def test_gemm_mid(M, N, K):
     """Mid-M stream-K kernel (gemm_mid.hip) against the fp32 reference: ragged M, tiles split over
     1..8 groups (in-launch last-arriver combine), a single iteration, 32 row tiles; plain, residual

@@ -118,6 +118,43 @@ def test_grouped_gate_up_layout_is_bit_identical(B):
         assert torch.equal(fused[0][0], fused[1][0]) and torch.equal(fused[0][1], fused[1][1])
 
 
+@pytest.mark.parametrize("T", [1, 37, 128, 129])
+def test_short_prefill_streams_the_weights(T, monkeypatch):
+    """Prefill steps of <= ``PREFILL_STREAM_MAX_M`` tokens run the decode layer (stream_gemm split-K
+    slabs summed by the RMSNorm / RoPE consumers, flash attention over the cache): within bf16 noise
+    of the MFMA-GEMM prefill and of the fp32 reference; the step above the bound keeps the GEMMs."""
+    cfg = decoder_config("tiny-llama")
+    w32 = random_decoder_weights(cfg, dtype=torch.float32, seed=21, interleave_mlp=True)
+    wbf = {k: v.to(torch.bfloat16) for k, v in w32.items()}
+    m = LlamaModel(cfg, dict(wbf), DEV, interleaved_mlp=True)
+    ids = torch.randint(0, cfg.vocab_size, (T,), generator=torch.Generator().manual_seed(T), dtype=torch.int32)
+    bs = 64
+    nb = -(-T // bs)
+
+    def prefill(model, dev, dtype):
+        kv = KVCache(cfg.layers, nb, cfg.kv_heads, bs, cfg.head_dim, dev, dtype=dtype)
+        meta = AttnMeta(decode=False, positions=torch.arange(T, dtype=torch.int32, device=dev),
+                        slots=torch.arange(T, device=dev), block_tables=torch.arange(nb, dtype=torch.int32,
+                                                                                     device=dev).view(1, nb),
+                        ctx_lens=torch.tensor([T], dtype=torch.int32, device=dev),
+                        cu_q=torch.tensor([0, T], dtype=torch.int32, device=dev), max_q=T)
+        return model.forward(ids.to(dev), meta, kv), kv
+
+    calls = []
+    orig = ops.stream_gemm
+    monkeypatch.setattr(ops, "stream_gemm", lambda *a, **k: calls.append(1) or orig(*a, **k))
+    h_s, kv_s = prefill(m, DEV, torch.bfloat16)
+    monkeypatch.setattr(ops, "stream_gemm", orig)
+    assert bool(calls) == (T <= LlamaModel.PREFILL_STREAM_MAX_M)
+    m.PREFILL_STREAM_MAX_M = 0
+    h_g, kv_g = prefill(m, DEV, torch.bfloat16)
+    torch.testing.assert_close(h_s.float(), h_g.float(), atol=6e-2, rtol=5e-2)
+    torch.testing.assert_close(kv_s.k.float(), kv_g.k.float(), atol=6e-2, rtol=5e-2)
+    m_ref = LlamaModel(cfg, {k: v.bfloat16().float() for k, v in w32.items()}, "cpu", interleaved_mlp=True)
+    h_ref, _ = prefill(m_ref, "cpu", torch.float32)
+    assert (h_s.float().cpu() - h_ref).abs().max().item() < 0.15
+
+
 @pytest.mark.parametrize("B", [4, 128])
 def test_default_path_keeps_unfolded_norm_gains(B):
     """the default GPU model does NOT fold the RMSNorm gains into the projections (one
