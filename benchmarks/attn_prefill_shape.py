@@ -84,6 +84,10 @@ ROUNDS = 3
 
 def main():
     g = torch.Generator().manual_seed(0)
+    if os.environ.get("ATTN_SINGLE"):  # single prompts (time to first token): pairs vs one block per workgroup
+        for lens in ([512], [1024], [2048], [4096], [1024] * 2, [1024] * 4):
+            case(f"single-{len(lens)}x{lens[0]}", lens)
+        return
     case("uniform-32x1024", [1024] * 32)
     case("uniform-8x4096", [4096] * 8)
     case("uniform-4x300", [300] * 4)

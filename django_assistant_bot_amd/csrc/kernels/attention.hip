@@ -1899,9 +1899,13 @@ int flash_attention(const void* q, long q_stride_tok, long q_stride_head, const 
       return hipGetLastError();
     }
     // causal: one workgroup per (long, short) query-block pair by default (+8 % on 16 x 1024,
-    // bit-identical: profiles/attn_vpipe_r5.md); DAB_FLASH_PAIR=0 selects one workgroup per block
+    // bit-identical: profiles/attn_vpipe_r5.md), unless the pairs would leave CUs idle (a single
+    // prompt of <= 1k tokens: 1 x 1024 37.2 vs 42.8 us one block per workgroup,
+    // profiles/attn_prefill_shape_r6.md); DAB_FLASH_PAIR=0 / 1 forces either
     const char* pe = std::getenv("DAB_FLASH_PAIR");
-    if (causal && vpipe && !(pe && pe[0] == '0')) {
+    const long pair_wgs = (long)(((max_seqlen_q + 127) / 128 + 1) / 2) * Hq * batch;
+    const bool pair = pe && pe[0] == '1' ? true : !(pe && pe[0] == '0') && pair_wgs >= 256;
+    if (causal && vpipe && pair) {
       // G = 2 pairs per workgroup (1 when that leaves < 1024 workgroups), walked heaviest-first
       // (lpt).  Large G made the workgroups few and long: the headline's prefill step (33 prompts of
       // ~1.03k queries, G = 5 = all pairs) ran 1056 workgroups of equal work on 512 slots, i.e.
