@@ -93,6 +93,7 @@ ARMS = {
     "all_g8": {"_groups": {"qkv": 8, "o": 8, "down": 8}},
     "down_g8": {"_groups": {"down": 8}},
     "qkvo_g8": {"_groups": {"qkv": 8, "o": 8}},
+    "gu27": {"gate_up": (27, 1)},  # batches 129..256: gate_up on the M <= 256 streaming tiles (round-6 default: gemm_mid)
     "gu41": {"gate_up": (41, 1)},
     "gu42": {"gate_up": (42, 1)},
 }

@@ -260,6 +260,10 @@ class LlamaModel:
 
     def _stream_cfg(self, name: str, M: int, N: int) -> int:
         nat = ops.native()
+        if M > 128 and name == "gate_up":
+            # decode batches of 129..256: gate_up (+SwiGLU8) on the mid-M GEMM, 67-72 us against 90-96
+            # on the M <= 256 streaming tiles (profiles/small_prefill_r6.md); qkv / o / down stream
+            return -1
         if M > 128:
             cfg = self.STREAM_CFG_M256
         elif M <= 16 and N % nat.stream_gemm_bn(self.STREAM_CFG_M16) == 0:
